@@ -1,0 +1,119 @@
+/*
+ * libmythgpu — C ABI of the MI355X batched constraint-evaluation engine.
+ *
+ * Drop-in boundary: the reference's only solver entry point is
+ *   mythril/support/model.py:15-49   get_model(constraints, minimize, maximize,
+ *                                              enforce_execution_time)
+ * which builds a z3.Optimize and calls check()/model() through
+ *   mythril/laser/smt/solver/solver.py:47-64  BaseSolver.check / .model.
+ * The Python shim (mythril_amd/model.py) keeps get_model's signature and
+ * contract and calls this library through ctypes for the witness search; the
+ * entries below replace, respectively:
+ *   mg_load_program   — Optimize.add(constraints)       solver.py:28-37
+ *   mg_search         — Optimize.check() (SAT side)     solver.py:47-57
+ *   mg_eval*          — Model.eval over many models     laser/smt/model.py:44-59
+ *   mg_keccak256      — find_concrete_keccak            keccak_function_manager.py:43-57
+ *
+ * All pointers are caller-owned.  Functions return 0 on success and a
+ * negative MG_E* code on failure (message: mg_last_error).  No exceptions
+ * cross the ABI.  Calls on one mg_ctx are synchronous unless they take a
+ * stream argument; use one mg_ctx per host thread.
+ */
+#ifndef MYTHGPU_H
+#define MYTHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MG_OK 0
+#define MG_E_ARG (-1)      /* invalid argument / malformed program          */
+#define MG_E_HIP (-2)      /* HIP runtime error                              */
+#define MG_E_NODEV (-3)    /* no usable GPU                                  */
+#define MG_E_NOMEM (-4)
+
+typedef struct mg_ctx mg_ctx;
+typedef struct mg_prog mg_prog;
+typedef struct mg_batch mg_batch;
+
+/* Device candidate generator for one leaf (free variable / table cell).
+ * A draw picks a class by (r >> 32) % 100:
+ *   < pct_uniform                    uniform random (masked to width)
+ *   < pct_small                      random < 2^64
+ *   < pct_boundary                   {0, 1, 2^(w-1), 2^w-1, 2^k+1, 2^k-1}
+ *   otherwise                        consts[pool_off + e] + {-1, 0, +1}
+ * (thresholds are cumulative percentages). */
+typedef struct mg_leafgen {
+    uint32_t width;
+    uint32_t pool_off;
+    uint32_t pool_n;
+    uint32_t pct_uniform;
+    uint32_t pct_small;
+    uint32_t pct_boundary;
+} mg_leafgen;
+
+typedef struct mg_gen {
+    uint64_t seed;          /* stream seed                                  */
+    uint64_t first_index;   /* candidate index of the first lane (sharding) */
+} mg_gen;
+
+int mg_init(int device, mg_ctx** out);
+void mg_free(mg_ctx* ctx);
+const char* mg_last_error(const mg_ctx* ctx);
+/* CU count, device name; available after mg_init. */
+int mg_device_info(mg_ctx* ctx, char* name, size_t name_len, int* n_cus);
+
+/* Upload one compiled program (IR of include/mythgpu_ir.h).  n_spill_slots
+ * spill slots are used by SPILL/RELOAD; the first MG_MAX_LDS of them live in
+ * LDS, the rest (<= MG_MAX_PSLOTS) in per-lane scratch. */
+int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins,
+                    const uint32_t* consts, uint32_t n_consts,
+                    const mg_leafgen* leaves, uint32_t n_leaves,
+                    uint32_t n_spill_slots, uint32_t n_probes, uint64_t prog_seed,
+                    mg_prog** out);
+void mg_free_program(mg_prog* prog);
+
+/* Evaluate under caller assignments (host buffers).
+ *   leaves_soa : [n_leaves][8][n_assign] u32 limbs, little-endian
+ *   root_bits  : [ceil(n_assign/64)] u64, bit i = conjunction of ROOTs
+ *   probes     : [n_probes][8][n_assign] u32, or NULL */
+int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, uint64_t n_assign,
+            uint64_t* root_bits, uint32_t* probes);
+
+/* Evaluate under device-generated assignments (candidate indices
+ * gen->first_index ...).  leaves_out: [n_leaves][8][n_assign] or NULL. */
+int mg_eval_gen(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_assign,
+                uint64_t* root_bits, uint32_t* probes, uint32_t* leaves_out);
+
+/* Witness search: smallest candidate index in [gen->first_index,
+ * gen->first_index + n_cand) whose assignment satisfies every ROOT, or -1.
+ * witness_leaves ([n_leaves][8], may be NULL) receives its leaf values. */
+int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_cand,
+              int64_t* first_sat, uint32_t* witness_leaves);
+
+/* Corpus batches: many programs, one launch.  Device-pointer API for
+ * resident benchmarking; stream is a hipStream_t (NULL = default stream).
+ *   d_root_bits : device [n_progs][ceil(n_assign/64)] u64 (may be NULL)
+ *   d_first_sat : device [n_progs] u64, atomicMin'ed (preset to ~0)     */
+int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, mg_batch** out);
+void mg_batch_free(mg_batch* batch);
+int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* batch, uint64_t seed, uint64_t first_index,
+                      uint64_t n_assign, uint64_t* d_root_bits, uint64_t* d_first_sat,
+                      void* stream);
+
+/* Keccak-256 (0x01 padding) of n messages, one GPU lane per message.
+ *   data/offsets/lens describe the messages in one host byte buffer;
+ *   out: n x 32 bytes. */
+int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
+                 const uint32_t* lens, uint32_t n, uint8_t* out);
+
+/* Library/ABI version (no GPU needed). */
+int mg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

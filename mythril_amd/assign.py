@@ -1,0 +1,101 @@
+"""Candidate assignments (models) and their SoA packing for the engine.
+
+An assignment interprets every free symbol of a constraint set the way a z3
+model does (``mythril/laser/smt/model.py``): bit-vector / Bool variables get a
+value, free arrays and uninterpreted functions get a finite table of
+``(key -> value)`` entries (first match wins) plus an ``else`` value.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+from .ir import CHUNK, Program
+
+Table = Tuple[List[Tuple[int, int]], int]
+
+
+class Assignment:
+    def __init__(self, vars: Dict[str, int] = None, arrays: Dict[str, Table] = None,
+                 funcs: Dict[str, Table] = None):
+        self.vars = dict(vars or {})
+        self.arrays = dict(arrays or {})
+        self.funcs = dict(funcs or {})
+
+    def table(self, name: str) -> Table:
+        if name in self.arrays:
+            return self.arrays[name]
+        if name in self.funcs:
+            return self.funcs[name]
+        return ([], 0)
+
+    def __repr__(self):
+        return "Assignment(vars=%r, arrays=%r, funcs=%r)" % (self.vars, self.arrays, self.funcs)
+
+
+def _padded_entries(tab: Table, n: int) -> List[Tuple[int, int]]:
+    entries, default = tab
+    if len(entries) > n:
+        raise ValueError("table has %d entries, program was compiled for %d" % (len(entries), n))
+    entries = list(entries)
+    filler = entries[0] if entries else (0, default)
+    return entries + [filler] * (n - len(entries))
+
+
+def leaf_values(program: Program, asg: Assignment) -> List[int]:
+    out = []
+    for leaf in program.leaves:
+        if leaf.kind == "var":
+            v = asg.vars.get(leaf.source, 0)
+        else:
+            tab = asg.table(leaf.source)
+            if leaf.kind == "else":
+                v = tab[1]
+            else:
+                ent = _padded_entries(tab, program.table_sizes[leaf.source])[leaf.entry]
+                v = ent[0] if leaf.kind == "key" else ent[1]
+        v = int(v) >> (CHUNK * leaf.chunk)
+        out.append(v & ((1 << leaf.width) - 1))
+    return out
+
+
+def pack(program: Program, assignments: Sequence[Assignment]) -> np.ndarray:
+    """(n_leaves, 8, n) uint32 little-endian limbs."""
+    n = len(assignments)
+    out = np.zeros((len(program.leaves), 8, n), dtype=np.uint32)
+    for a, asg in enumerate(assignments):
+        for i, v in enumerate(leaf_values(program, asg)):
+            for j in range(8):
+                out[i, j, a] = (v >> (32 * j)) & 0xFFFFFFFF
+    return out
+
+
+def unpack(program: Program, leaves: np.ndarray) -> Assignment:
+    """Inverse of :func:`pack` for one candidate: leaves is (n_leaves, 8)."""
+    vals = []
+    for i in range(len(program.leaves)):
+        v = 0
+        for j in reversed(range(8)):
+            v = (v << 32) | int(leaves[i, j])
+        vals.append(v)
+    vars_: Dict[str, int] = {}
+    tables: Dict[str, dict] = {}
+    for leaf, v in zip(program.leaves, vals):
+        part = v << (CHUNK * leaf.chunk)
+        if leaf.kind == "var":
+            vars_[leaf.source] = vars_.get(leaf.source, 0) | part
+        else:
+            t = tables.setdefault(leaf.source, {"k": {}, "v": {}, "else": 0})
+            if leaf.kind == "else":
+                t["else"] |= part
+            else:
+                d = t["k" if leaf.kind == "key" else "v"]
+                d[leaf.entry] = d.get(leaf.entry, 0) | part
+    arrays, funcs = {}, {}
+    for name, t in tables.items():
+        n = program.table_sizes.get(name, 0)
+        tab = ([(t["k"].get(e, 0), t["v"].get(e, 0)) for e in range(n)], t["else"])
+        (funcs if program.table_kinds.get(name) == "func" else arrays)[name] = tab
+    return Assignment(vars_, arrays, funcs)

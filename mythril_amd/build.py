@@ -1,0 +1,55 @@
+"""Build libmythgpu.so in-tree (hipcc, gfx950).  The .so travels to the GPU
+box with the repo snapshot; nothing is JIT-compiled at run time."""
+
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "mythril_amd", "csrc")
+LIBDIR = os.path.join(ROOT, "mythril_amd", "lib")
+LIB = os.path.join(LIBDIR, "libmythgpu.so")
+SOURCES = ["mg_kernels.hip", "mg_keccak.hip", "mg_api.cpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
+
+
+def _deps():
+    files = [os.path.join(CSRC, s) for s in SOURCES]
+    files += [os.path.join(CSRC, "mg_device.h"), os.path.join(ROOT, "include", "mythgpu.h"),
+              os.path.join(ROOT, "include", "mythgpu_ir.h")]
+    return files
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(f) <= t for f in _deps())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, src + ".o")
+        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
+               "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-c",
+               os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs,
+                   check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,245 @@
+"""ctypes binding of libmythgpu (include/mythgpu.h).
+
+The product path has no CPU evaluator: if the shared library or the GPU is
+missing, :func:`get_engine` raises :class:`EngineUnavailable` and the caller
+(``mythril_amd.model.get_model``) falls back to z3 — never to a host
+re-implementation.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .ir import Program
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmythgpu.so")
+
+EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
+           "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
+           "mg_batch_free", "mg_batch_eval_gen", "mg_keccak256", "mg_version")
+
+
+class EngineUnavailable(RuntimeError):
+    pass
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class LeafGen(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("pool_off", C.c_uint32), ("pool_n", C.c_uint32),
+                ("pct_uniform", C.c_uint32), ("pct_small", C.c_uint32),
+                ("pct_boundary", C.c_uint32)]
+
+
+class Gen(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("first_index", C.c_uint64)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = _LIB_PATH):
+    """Load libmythgpu.so (no GPU needed) and declare every export."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise EngineUnavailable("libmythgpu.so not built (%s); run "
+                                    "`python -m mythril_amd.build`" % path)
+        lib = C.CDLL(path)
+        p, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
+        lib.mg_version.restype = C.c_int
+        lib.mg_init.argtypes = [C.c_int, C.POINTER(p)]
+        lib.mg_free.argtypes = [p]
+        lib.mg_free.restype = None
+        lib.mg_last_error.argtypes = [p]
+        lib.mg_last_error.restype = C.c_char_p
+        lib.mg_device_info.argtypes = [p, C.c_char_p, C.c_size_t, C.POINTER(C.c_int)]
+        lib.mg_load_program.argtypes = [p, p, u32, p, u32, p, u32, u32, u32, u64, C.POINTER(p)]
+        lib.mg_free_program.argtypes = [p]
+        lib.mg_free_program.restype = None
+        lib.mg_eval.argtypes = [p, p, p, u64, p, p]
+        lib.mg_eval_gen.argtypes = [p, p, C.POINTER(Gen), u64, p, p, p]
+        lib.mg_search.argtypes = [p, p, C.POINTER(Gen), u64, C.POINTER(i64), p]
+        lib.mg_batch_create.argtypes = [p, C.POINTER(p), u32, C.POINTER(p)]
+        lib.mg_batch_free.argtypes = [p]
+        lib.mg_batch_free.restype = None
+        lib.mg_batch_eval_gen.argtypes = [p, p, u64, u64, u64, p, p, p]
+        lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
+        for name in EXPORTS:
+            getattr(lib, name)
+        _lib = lib
+        return lib
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def default_leafgen(program: Program, pct=(50, 70, 85)) -> List[LeafGen]:
+    """C2 value distribution: 50 % uniform, 20 % < 2^64, 15 %
+    boundary values, 15 % DAG constants +-1 (pool = the program's constants)."""
+    n_c = len(program.const_values)
+    return [LeafGen(l.width, 0, n_c, pct[0], pct[1], pct[2]) for l in program.leaves]
+
+
+class LoadedProgram:
+    def __init__(self, engine: "Engine", program: Program, handle):
+        self.engine = engine
+        self.program = program
+        self.handle = handle
+
+    def __del__(self):
+        try:
+            if self.handle and self.engine._ctx:
+                self.engine.lib.mg_free_program(self.handle)
+        except Exception:
+            pass
+        self.handle = None
+
+
+class Engine:
+    """One HIP device context (one per host thread)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        ctx = C.c_void_p()
+        rc = self.lib.mg_init(device, C.byref(ctx))
+        if rc != 0:
+            raise EngineUnavailable("mg_init(%d) failed with %d (no usable GPU?)" % (device, rc))
+        self._ctx = ctx
+        name = C.create_string_buffer(256)
+        cus = C.c_int()
+        self.lib.mg_device_info(ctx, name, 256, C.byref(cus))
+        self.device_name = name.value.decode()
+        self.n_cus = cus.value
+
+    def close(self):
+        if self._ctx:
+            self.lib.mg_free(self._ctx)
+            self._ctx = None
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise EngineError("%s failed (%d): %s" % (what, rc,
+                              self.lib.mg_last_error(self._ctx).decode(errors="replace")))
+
+    def load(self, program: Program, leafgen: Optional[Sequence[LeafGen]] = None,
+             prog_seed: int = 0) -> LoadedProgram:
+        code = np.ascontiguousarray(program.code, dtype=np.uint32)
+        consts = np.ascontiguousarray(program.consts, dtype=np.uint32)
+        gens = list(leafgen) if leafgen is not None else default_leafgen(program)
+        garr = (LeafGen * max(1, len(gens)))(*gens)
+        h = C.c_void_p()
+        rc = self.lib.mg_load_program(self._ctx, _ptr(code), code.shape[0], _ptr(consts),
+                                      consts.shape[0], C.cast(garr, C.c_void_p), len(gens),
+                                      program.n_lds, program.n_probes, prog_seed & (2**64 - 1),
+                                      C.byref(h))
+        self._check(rc, "mg_load_program")
+        return LoadedProgram(self, program, h)
+
+    def eval(self, lp: LoadedProgram, leaves_soa: np.ndarray, want_probes: bool = False):
+        """leaves_soa: (n_leaves, 8, n) uint32.  Returns (root bool array,
+        probes (n_probes, 8, n) uint32 or None)."""
+        prog = lp.program
+        leaves_soa = np.ascontiguousarray(leaves_soa, dtype=np.uint32)
+        n = leaves_soa.shape[2] if leaves_soa.ndim == 3 else 0
+        if leaves_soa.shape[:2] != (len(prog.leaves), 8):
+            raise ValueError("leaves_soa must be (n_leaves, 8, n)")
+        bits = np.zeros((n + 63) // 64, dtype=np.uint64)
+        probes = np.zeros((prog.n_probes, 8, n), dtype=np.uint32) if want_probes else None
+        rc = self.lib.mg_eval(self._ctx, lp.handle, _ptr(leaves_soa), n, _ptr(bits), _ptr(probes))
+        self._check(rc, "mg_eval")
+        return unpack_bits(bits, n), probes
+
+    def eval_gen(self, lp: LoadedProgram, seed: int, first_index: int, n: int,
+                 want_probes: bool = False, want_leaves: bool = False):
+        prog = lp.program
+        bits = np.zeros((n + 63) // 64, dtype=np.uint64)
+        probes = np.zeros((prog.n_probes, 8, n), dtype=np.uint32) if want_probes else None
+        leaves = np.zeros((len(prog.leaves), 8, n), dtype=np.uint32) if want_leaves else None
+        g = Gen(seed & (2**64 - 1), first_index)
+        rc = self.lib.mg_eval_gen(self._ctx, lp.handle, C.byref(g), n, _ptr(bits), _ptr(probes),
+                                  _ptr(leaves))
+        self._check(rc, "mg_eval_gen")
+        return unpack_bits(bits, n), probes, leaves
+
+    def search(self, lp: LoadedProgram, seed: int, n_cand: int,
+               first_index: int = 0) -> Tuple[int, Optional[np.ndarray]]:
+        prog = lp.program
+        first = C.c_int64(-1)
+        wit = np.zeros((max(1, len(prog.leaves)), 8), dtype=np.uint32)
+        g = Gen(seed & (2**64 - 1), first_index)
+        rc = self.lib.mg_search(self._ctx, lp.handle, C.byref(g), n_cand, C.byref(first),
+                                _ptr(wit))
+        self._check(rc, "mg_search")
+        if first.value < 0:
+            return -1, None
+        return first.value, wit[:len(prog.leaves)]
+
+    def keccak256(self, msgs: Sequence[bytes]) -> List[bytes]:
+        n = len(msgs)
+        if n == 0:
+            return []
+        lens = np.array([len(m) for m in msgs], dtype=np.uint32)
+        offs = np.zeros(n, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        data = np.frombuffer(b"".join(msgs) or b"\0", dtype=np.uint8).copy()
+        out = np.zeros((n, 32), dtype=np.uint8)
+        rc = self.lib.mg_keccak256(self._ctx, _ptr(data), _ptr(offs), _ptr(lens), n, _ptr(out))
+        self._check(rc, "mg_keccak256")
+        return [bytes(out[i]) for i in range(n)]
+
+    # corpus batches (device pointers; used by bench.py)
+    def batch_create(self, loaded: Sequence[LoadedProgram]):
+        arr = (C.c_void_p * len(loaded))(*[lp.handle for lp in loaded])
+        h = C.c_void_p()
+        rc = self.lib.mg_batch_create(self._ctx, arr, len(loaded), C.byref(h))
+        self._check(rc, "mg_batch_create")
+        return h
+
+    def batch_free(self, h):
+        self.lib.mg_batch_free(h)
+
+    def batch_eval_gen(self, h, seed: int, first_index: int, n_assign: int,
+                       d_root_bits: int = 0, d_first_sat: int = 0, stream: int = 0):
+        rc = self.lib.mg_batch_eval_gen(self._ctx, h, seed & (2**64 - 1), first_index, n_assign,
+                                        C.c_void_p(d_root_bits or None),
+                                        C.c_void_p(d_first_sat or None), C.c_void_p(stream or None))
+        self._check(rc, "mg_batch_eval_gen")
+
+
+def unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:
+    b = np.unpackbits(bits.view(np.uint8), bitorder="little")
+    return b[:n].astype(bool)
+
+
+def int_to_limbs(v: int) -> List[int]:
+    return [(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)]
+
+
+def limbs_to_int(limbs) -> int:
+    v = 0
+    for j in reversed(range(8)):
+        v = (v << 32) | int(limbs[j])
+    return v
+
+
+_engines: Dict[int, Engine] = {}
+
+
+def get_engine(device: int = 0) -> Engine:
+    e = _engines.get(device)
+    if e is None:
+        e = Engine(device)
+        _engines[device] = e
+    return e

@@ -1,0 +1,622 @@
+"""Host compiler: ``get_model`` constraint DAG → mythgpu IR program.
+
+Pipeline:
+
+1. **Lowering** — SMT-LIB nodes (``mythril_amd.smt.node``) become kernel-level
+   operations on values of width <= 256 (``LNode``), hash-consed so DAG sharing
+   survives.  Rewrites:
+   * n-ary ``bvadd/bvmul/bvand/bvor/bvxor/and/or`` → binary chains;
+   * ``bvugt/bvuge/bvsgt/bvsge`` → swapped ``ult/ule/slt/sle``; ``=>`` →
+     ``or(not a, b)``; ``distinct`` → ``not(=)``; ``zero_extend`` is free
+     (values are kept canonical);
+   * ``select`` over ``store`` chains → ``ite(i = j, v, ...)`` chains
+     (``select(store(A,i,v),j) = ite(i=j, v, select(A,j))``), over ``K`` →
+     the constant, over a free array or an uninterpreted-function application
+     → an ite chain over the model's table entries, each entry a pair of leaf
+     values (``name#k<e>``, ``name#v<e>``) plus ``name#else`` — exactly how a
+     z3 model interprets arrays and functions (``laser/smt/model.py``);
+   * values wider than 256 bits (Keccak inputs are 512-bit concats,
+     ``instructions.py:1029-1035``) are split into 256-bit chunks: only
+     concat / extract / zero_extend / = / distinct / ite / table keys are
+     supported on them, which is every use LASER makes of them;
+   * the carry test z3 builds for ``BVAddNoOverflow``
+     (``extract(w, w, bvadd(zext1 a, zext1 b))``) becomes ``ult(a+b, a)``.
+   Anything else raises :class:`Unsupported` (the caller falls back to z3).
+2. **Scheduling** — source creation order (topological, short live ranges),
+   each sink (``ROOT`` per constraint, ``OUT`` per probe) right after its
+   operand.
+3. **Register allocation** — linear scan over 15 VGPR slots with Belady
+   eviction (furthest next use); evicted values go to LDS (``SPILL`` /
+   ``RELOAD``), constants are rematerialised.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import irdefs as I
+from .smt.node import Node, topo_order
+
+CHUNK = 256
+MAX_SPILL = I.MAX_LDS + I.MAX_PSLOTS   # LDS tier first, then per-lane scratch
+
+
+class Unsupported(Exception):
+    """The DAG uses something the GPU path does not evaluate (→ z3)."""
+
+
+class LNode:
+    __slots__ = ("op", "width", "args", "imm", "id", "birth")
+
+    def __init__(self, op, width, args, imm, nid, birth):
+        self.op = op
+        self.width = width
+        self.args = args
+        self.imm = imm
+        self.id = nid
+        self.birth = birth     # id of the source node being lowered at creation
+
+    def __repr__(self):
+        return "L%d:%s/%d%s" % (self.id, I.OPNAME.get(self.op, self.op), self.width,
+                                 "" if self.imm is None else "[%s]" % (self.imm,))
+
+
+@dataclass
+class Leaf:
+    """One input slot of an assignment.  ``kind``: var | key | val | else;
+    ``source`` is the variable / array / function name, ``chunk`` the 256-bit
+    chunk of a wide value, ``entry`` the table entry index."""
+    name: str
+    width: int
+    kind: str
+    source: str
+    chunk: int = 0
+    entry: int = 0
+    pool: Tuple[int, ...] = ()
+
+
+@dataclass
+class Program:
+    code: np.ndarray                  # (n_ins, 4) uint32
+    consts: np.ndarray                # (n_consts, 8) uint32
+    const_values: List[int]
+    leaves: List[Leaf]
+    n_lds: int
+    n_probes: int
+    n_roots: int
+    table_sizes: Dict[str, int]
+    table_kinds: Dict[str, str] = field(default_factory=dict)   # name -> array | func
+    stats: Dict[str, object] = field(default_factory=dict)
+
+    @property
+    def n_ins(self) -> int:
+        return int(self.code.shape[0])
+
+    def leaf_index(self) -> Dict[str, int]:
+        return {l.name: i for i, l in enumerate(self.leaves)}
+
+
+# ----------------------------------------------------------------------------
+# lowering
+# ----------------------------------------------------------------------------
+
+def _limbs(value: int) -> List[int]:
+    return [(value >> (32 * j)) & 0xFFFFFFFF for j in range(8)]
+
+
+class _Lowerer:
+    def __init__(self, table_sizes: Dict[str, int], default_entries: int):
+        self.table = {}
+        self.nid = 0
+        self.leaves: List[Leaf] = []
+        self.leaf_ids: Dict[str, int] = {}
+        self.memo: Dict[int, List[LNode]] = {}
+        self.sel_memo: Dict[Tuple[int, Tuple[int, ...]], List[LNode]] = {}
+        self.table_sizes = dict(table_sizes)
+        self.table_kinds: Dict[str, str] = {}
+        self.default_entries = default_entries
+        self.consts_seen: set = set()
+        self.birth = 0
+
+    # -- hash-consed constructors ------------------------------------------
+    def mk(self, op: int, width: int, args=(), imm=None) -> LNode:
+        key = (op, width, tuple(a.id for a in args), imm)
+        n = self.table.get(key)
+        if n is None:
+            self.nid += 1
+            birth = self.birth
+            for a in args:          # keep (birth, id) order topological
+                if a.birth > birth:
+                    birth = a.birth
+            n = LNode(op, width, tuple(args), imm, self.nid, birth)
+            self.table[key] = n
+        return n
+
+    def const(self, value: int, width: int) -> LNode:
+        value &= (1 << width) - 1
+        self.consts_seen.add(value)
+        return self.mk(I.CONST, width, (), value)
+
+    def leaf(self, name: str, width: int, kind: str, source: str, chunk=0, entry=0) -> LNode:
+        idx = self.leaf_ids.get(name)
+        if idx is None:
+            idx = len(self.leaves)
+            self.leaf_ids[name] = idx
+            self.leaves.append(Leaf(name, width, kind, source, chunk, entry))
+        return self.mk(I.LEAF, width, (), idx)
+
+    # -- chunk helpers --------------------------------------------------------
+    @staticmethod
+    def nchunks(w: int) -> int:
+        return (w + CHUNK - 1) // CHUNK
+
+    @staticmethod
+    def chunk_width(w: int, i: int) -> int:
+        return min(CHUNK, w - CHUNK * i)
+
+    def bits(self, chunks: Sequence[LNode], w: int, lo: int, hi: int) -> LNode:
+        """Bits [lo, hi] (inclusive) of a chunked value, hi - lo < 256."""
+        ci, cj = lo // CHUNK, hi // CHUNK
+        if ci == cj:
+            c = chunks[ci]
+            cw = self.chunk_width(w, ci)
+            l0, h0 = lo - CHUNK * ci, hi - CHUNK * ci
+            if l0 == 0 and h0 == cw - 1:
+                return c
+            return self.mk(I.EXTRACT, h0 - l0 + 1, (c,), l0)
+        low_w = CHUNK * (ci + 1) - lo
+        low = self.bits(chunks, w, lo, CHUNK * (ci + 1) - 1)
+        high = self.bits(chunks, w, CHUNK * cj, hi)
+        return self.mk(I.CONCAT, hi - lo + 1, (high, low), low_w)
+
+    def assemble(self, pieces: List[Tuple[List[LNode], int]]) -> List[LNode]:
+        """Concatenate (chunks, width) pieces given MSB first."""
+        total = sum(w for _, w in pieces)
+        # segments LSB first: (chunks, width, offset in result)
+        segs, off = [], 0
+        for ch, w in reversed(pieces):
+            segs.append((ch, w, off))
+            off += w
+        out = []
+        for k in range(self.nchunks(total)):
+            lo_k, hi_k = CHUNK * k, min(total, CHUNK * (k + 1)) - 1
+            acc: Optional[LNode] = None
+            acc_w = 0
+            for ch, w, o in segs:
+                a, b = max(lo_k, o), min(hi_k, o + w - 1)
+                if a > b:
+                    continue
+                part = self.bits(ch, w, a - o, b - o)
+                pw = b - a + 1
+                if acc is None:
+                    acc, acc_w = part, pw
+                else:
+                    acc = self.mk(I.CONCAT, acc_w + pw, (part, acc), acc_w)
+                    acc_w += pw
+            out.append(acc)
+        return out
+
+    # -- main lowering ---------------------------------------------------------
+    def lower(self, n: Node) -> List[LNode]:
+        r = self.memo.get(n.id)
+        if r is not None:
+            return r
+        # iterative post-order so deep DAGs do not hit the recursion limit
+        nodes = topo_order([n])
+        skip = set()
+        for m in nodes:            # operands consumed only through the carry pattern
+            if m.op == "extract" and self._is_carry(m):
+                s = m.args[0]
+                skip.update((s.id, s.args[0].id, s.args[1].id))
+        saved = self.birth
+        for m in nodes:
+            if m.id in self.memo or m.is_array() or (m.id in skip and m is not n):
+                continue
+            try:
+                self.birth = m.id
+                self.memo[m.id] = self._lower_one(m)
+            except KeyError as e:   # a skipped operand was needed elsewhere
+                raise Unsupported("operand lowered only as part of a pattern") from e
+            finally:
+                self.birth = m.id
+        self.birth = max(saved, self.birth) if saved else self.birth
+        return self.memo[n.id]
+
+    def _narrow(self, n: Node) -> LNode:
+        ch = self.memo[n.id]
+        if len(ch) != 1:
+            raise Unsupported("%s on a %d-bit value" % (n.op, n.width))
+        return ch[0]
+
+    def _fold(self, op: int, width: int, args: List[LNode]) -> LNode:
+        acc = args[0]
+        for a in args[1:]:
+            acc = self.mk(op, width, (acc, a))
+        return acc
+
+    def _lower_one(self, n: Node) -> List[LNode]:
+        op, w = n.op, n.width
+        if w > CHUNK:
+            return self._lower_wide(n)
+        A = lambda i: self._narrow(n.args[i])  # noqa: E731
+        if op == "bvnum":
+            return [self.const(n.params[0], w)]
+        if op == "true":
+            return [self.const(1, 1)]
+        if op == "false":
+            return [self.const(0, 1)]
+        if op == "var":
+            return [self.leaf(n.params[0], w, "var", n.params[0])]
+        simple = {"bvsub": I.SUB, "bvudiv": I.UDIV, "bvurem": I.UREM, "bvsdiv": I.SDIV,
+                  "bvsrem": I.SREM, "bvsmod": I.SMOD, "bvshl": I.SHL, "bvlshr": I.LSHR,
+                  "bvashr": I.ASHR}
+        if op in simple:
+            return [self.mk(simple[op], w, (A(0), A(1)))]
+        nary = {"bvadd": I.ADD, "bvmul": I.MUL, "bvand": I.AND, "bvor": I.OR, "bvxor": I.XOR,
+                "and": I.AND, "or": I.OR}
+        if op in nary:
+            return [self._fold(nary[op], w, [A(i) for i in range(len(n.args))])]
+        if op in ("bvneg",):
+            return [self.mk(I.NEG, w, (A(0),))]
+        if op in ("bvnot", "not"):
+            return [self.mk(I.NOT, w, (A(0),))]
+        if op == "xor":
+            return [self.mk(I.XOR, 1, (A(0), A(1)))]
+        if op == "=>":
+            return [self.mk(I.OR, 1, (self.mk(I.NOT, 1, (A(0),)), A(1)))]
+        cmp = {"bvult": (I.ULT, False), "bvule": (I.ULE, False), "bvugt": (I.ULT, True),
+               "bvuge": (I.ULE, True), "bvslt": (I.SLT, False), "bvsle": (I.SLE, False),
+               "bvsgt": (I.SLT, True), "bvsge": (I.SLE, True), "bvumul_noovfl": (I.UMULNO, False)}
+        if op in cmp:
+            kop, swap = cmp[op]
+            a, b = A(0), A(1)
+            if swap:
+                a, b = b, a
+            return [self.mk(kop, n.args[0].width, (a, b))]
+        if op in ("=", "distinct"):
+            if any(x.is_array() for x in n.args):
+                raise Unsupported("array equality")
+            return [self._eq_or_distinct(op, n)]
+        if op == "ite":
+            if n.is_array():
+                raise Unsupported("array-valued ite outside select")
+            return [self.mk(I.ITE, w, (A(0), A(1), A(2)))]
+        if op == "concat":
+            return self.assemble([(self.memo[a.id], a.width) for a in n.args])
+        if op == "extract":
+            hi, lo = n.params
+            src = n.args[0]
+            carry = self._carry_pattern(n)
+            if carry is not None:
+                return [carry]
+            return [self.bits(self.memo[src.id], src.width, lo, hi)]
+        if op == "zero_extend":
+            return [self._narrow(n.args[0])]
+        if op == "sign_extend":
+            return [self.mk(I.SEXT, w, (A(0),), n.args[0].width)]
+        if op == "select":
+            return self._select(n.args[0], self.memo[n.args[1].id], n.args[1].width, w)
+        if op == "apply":
+            fname, dom = n.params
+            return self._table(fname, self.memo[n.args[0].id], dom, w, "func")
+        raise Unsupported("operator %s" % op)
+
+    def _eq_or_distinct(self, op: str, n: Node) -> LNode:
+        args = [self.memo[a.id] for a in n.args]
+        w = n.args[0].width
+
+        def eq(x, y):
+            parts = [self.mk(I.EQ, self.chunk_width(w, k) if w > CHUNK else w, (x[k], y[k]))
+                     for k in range(len(x))]
+            return self._fold(I.AND, 1, parts)
+        if op == "=":
+            return eq(args[0], args[1])
+        terms = []
+        for i in range(len(args)):
+            for j in range(i + 1, len(args)):
+                terms.append(self.mk(I.NOT, 1, (eq(args[i], args[j]),)))
+        return self._fold(I.AND, 1, terms)
+
+    @staticmethod
+    def _is_carry(n: Node) -> bool:
+        hi, lo = n.params
+        s = n.args[0]
+        if hi != lo or s.op != "bvadd" or len(s.args) != 2 or hi != s.width - 1:
+            return False
+        a, b = s.args
+        return (a.op == "zero_extend" and b.op == "zero_extend" and a.params == (1,) and
+                b.params == (1,) and a.args[0].width <= CHUNK)
+
+    def _carry_pattern(self, n: Node) -> Optional[LNode]:
+        if not self._is_carry(n):
+            return None
+        x, y = n.args[0].args[0].args[0], n.args[0].args[1].args[0]
+        lx, ly = self.lower(x)[0], self.lower(y)[0]
+        return self.mk(I.ULT, x.width, (self.mk(I.ADD, x.width, (lx, ly)), lx))
+
+    def _lower_wide(self, n: Node) -> List[LNode]:
+        op, w = n.op, n.width
+        if op == "bvnum":
+            v = n.params[0]
+            return [self.const(v >> (CHUNK * k), self.chunk_width(w, k)) for k in range(self.nchunks(w))]
+        if op == "var":
+            return [self.leaf("%s#%d" % (n.params[0], k), self.chunk_width(w, k), "var",
+                              n.params[0], chunk=k) for k in range(self.nchunks(w))]
+        if op == "concat":
+            return self.assemble([(self.memo[a.id], a.width) for a in n.args])
+        if op == "extract":
+            src = n.args[0]
+            hi, lo = n.params
+            return self.assemble([([self.bits(self.memo[src.id], src.width, lo + CHUNK * k,
+                                              min(hi, lo + CHUNK * k + CHUNK - 1))],
+                                   min(CHUNK, hi - lo + 1 - CHUNK * k))
+                                  for k in reversed(range(self.nchunks(w)))])
+        if op == "zero_extend":
+            src = n.args[0]
+            pad = w - src.width
+            pieces = []
+            while pad > 0:
+                pw = min(CHUNK, pad)
+                pieces.append(([self.const(0, pw)], pw))
+                pad -= pw
+            return self.assemble(pieces + [(self.memo[src.id], src.width)])
+        if op == "ite":
+            c = self._narrow(n.args[0])
+            a, b = self.memo[n.args[1].id], self.memo[n.args[2].id]
+            return [self.mk(I.ITE, x.width, (c, x, y)) for x, y in zip(a, b)]
+        if op == "select":
+            return self._select(n.args[0], self.memo[n.args[1].id], n.args[1].width, w)
+        if op == "apply":
+            fname, dom = n.params
+            return self._table(fname, self.memo[n.args[0].id], dom, w, "func")
+        raise Unsupported("%s on a %d-bit value" % (op, w))
+
+    # -- arrays and uninterpreted functions ------------------------------------
+    def _chunk_eq(self, x: List[LNode], y: List[LNode], w: int) -> LNode:
+        parts = [self.mk(I.EQ, self.chunk_width(w, k), (x[k], y[k])) for k in range(len(x))]
+        return self._fold(I.AND, 1, parts)
+
+    def _ite_chunks(self, c: LNode, a: List[LNode], b: List[LNode]) -> List[LNode]:
+        return [self.mk(I.ITE, x.width, (c, x, y)) for x, y in zip(a, b)]
+
+    def _table(self, name: str, key: List[LNode], kw: int, vw: int, kind: str) -> List[LNode]:
+        self.table_kinds[name] = kind
+        memo_key = (("T", name), tuple(k.id for k in key))
+        hit = self.sel_memo.get(memo_key)
+        if hit is not None:
+            return hit
+        entries = self.table_sizes.setdefault(name, self.default_entries)
+
+        def cell(kind: str, e: int, width: int) -> List[LNode]:
+            tag = {"key": "k%d" % e, "val": "v%d" % e, "else": "else"}[kind]
+            return [self.leaf("%s#%s#%d" % (name, tag, k), self.chunk_width(width, k), kind,
+                              name, chunk=k, entry=e)
+                    for k in range(self.nchunks(width))]
+        acc = cell("else", 0, vw)
+        for e in reversed(range(entries)):
+            acc = self._ite_chunks(self._chunk_eq(key, cell("key", e, kw), kw),
+                                   cell("val", e, vw), acc)
+        self.sel_memo[memo_key] = acc
+        return acc
+
+    def _select(self, arr: Node, idx: List[LNode], iw: int, vw: int) -> List[LNode]:
+        memo_key = (arr.id, tuple(i.id for i in idx))
+        hit = self.sel_memo.get(memo_key)
+        if hit is not None:
+            return hit
+        # walk the store chain iteratively
+        chain = []
+        a = arr
+        while a.op == "store":
+            chain.append(a)
+            a = a.args[0]
+        if a.op == "K":
+            base = self.lower(a.args[0])
+        elif a.op == "array":
+            base = self._table(a.params[0], idx, iw, vw, "array")
+        elif a.op == "ite":
+            c = self._narrow_node(a.args[0])
+            base = self._ite_chunks(c, self._select(a.args[1], idx, iw, vw),
+                                    self._select(a.args[2], idx, iw, vw))
+        else:
+            raise Unsupported("array term %s" % a.op)
+        acc = base
+        for st in reversed(chain):
+            j = self.lower(st.args[1])
+            v = self.lower(st.args[2])
+            acc = self._ite_chunks(self._chunk_eq(idx, j, iw), v, acc)
+        self.sel_memo[memo_key] = acc
+        return acc
+
+    def _narrow_node(self, n: Node) -> LNode:
+        ch = self.lower(n)
+        if len(ch) != 1:
+            raise Unsupported("wide condition")
+        return ch[0]
+
+
+# ----------------------------------------------------------------------------
+# scheduling + register allocation + emission
+# ----------------------------------------------------------------------------
+
+def _schedule(sinks: List[LNode]) -> List[LNode]:
+    """Evaluation order: every reachable LNode sorted by (birth, id).
+
+    Source nodes are hash-consed in creation order, and a node is always
+    created after its operands, so source-id order is topological; it is also
+    the order LASER built the expressions in (``instructions.py`` lowers one
+    opcode at a time), which keeps live ranges short.  LNodes born while
+    lowering one source node keep their creation order.  A sink (ROOT / OUT)
+    is born with its operand, so it is placed right after it and the value
+    dies as early as possible."""
+    seen = set()
+    out = []
+    stack = list(sinks)
+    while stack:
+        n = stack.pop()
+        if n.id in seen:
+            continue
+        seen.add(n.id)
+        out.append(n)
+        stack.extend(a for a in n.args if a.id not in seen)
+    out.sort(key=lambda n: (n.birth, n.id))
+    return out
+
+
+def _allocate(order: List[LNode], const_index: Dict[int, int]):
+    uses: Dict[int, List[int]] = {}
+    for i, n in enumerate(order):
+        for a in n.args:
+            uses.setdefault(a.id, []).append(i)
+    ptr: Dict[int, int] = {}
+    reg_of: Dict[int, int] = {}
+    lds_of: Dict[int, int] = {}
+    holder: Dict[int, LNode] = {}          # reg -> value
+    free_regs = list(range(I.NREG - 1))[::-1]
+    free_lds: List[int] = []
+    n_lds = 0
+    ins: List[Tuple[int, int, int, int, int, int, int]] = []
+    n_spill = n_reload = 0
+
+    def next_use(v: LNode, i: int) -> int:
+        u = uses.get(v.id, [])
+        p = ptr.get(v.id, 0)
+        while p < len(u) and u[p] < i:
+            p += 1
+        ptr[v.id] = p
+        return u[p] if p < len(u) else 1 << 60
+
+    def alloc_reg(i: int, protect: set) -> int:
+        nonlocal n_lds, n_spill
+        if free_regs:
+            return free_regs.pop()
+        victim, far = None, -1
+        for r, v in holder.items():
+            if v.id in protect:
+                continue
+            nu = next_use(v, i)
+            if nu > far:
+                victim, far = v, nu
+        if victim is None:
+            raise Unsupported("register pressure")
+        r = reg_of.pop(victim.id)
+        del holder[r]
+        if victim.op != I.CONST and victim.id not in lds_of:
+            if free_lds:
+                s = free_lds.pop()
+            else:
+                s = n_lds
+                n_lds += 1
+                if n_lds > MAX_SPILL:
+                    raise Unsupported("spill budget exceeded")
+            lds_of[victim.id] = s
+            ins.append((I.SPILL, 1, I.TRASH, r, 0, 0, s))
+            n_spill += 1
+        return r
+
+    def materialise(v: LNode, r: int):
+        nonlocal n_reload
+        if v.op == I.CONST:
+            ins.append((I.CONST, v.width, r, 0, 0, 0, const_index[v.imm]))
+        else:
+            ins.append((I.RELOAD, v.width, r, 0, 0, 0, lds_of[v.id]))
+            n_reload += 1
+
+    def release(v: LNode, i: int):
+        if next_use(v, i + 1) >= (1 << 60):
+            r = reg_of.pop(v.id, None)
+            if r is not None:
+                del holder[r]
+                free_regs.append(r)
+            s = lds_of.pop(v.id, None)
+            if s is not None:
+                free_lds.append(s)
+
+    for i, n in enumerate(order):
+        protect = {a.id for a in n.args}
+        for a in n.args:
+            if a.id not in reg_of:
+                r = alloc_reg(i, protect)
+                materialise(a, r)
+                reg_of[a.id] = r
+                holder[r] = a
+        slots = [reg_of[a.id] for a in n.args]
+        for a in set(n.args):
+            release(a, i)
+        if n.op in (I.ROOT, I.OUT):
+            ins.append((n.op, 1, I.TRASH, slots[0], 0, 0, n.imm or 0))
+            continue
+        if not uses.get(n.id):
+            d = I.TRASH
+        else:
+            d = alloc_reg(i, set())
+            reg_of[n.id] = d
+            holder[d] = n
+        op = n.op
+        a = slots[0] if len(slots) > 0 else 0
+        b = slots[1] if len(slots) > 1 else 0
+        c = 0
+        imm = 0
+        width = n.width
+        if op == I.CONST:
+            imm = const_index[n.imm]
+        elif op == I.LEAF:
+            imm = n.imm
+        elif op in (I.EXTRACT, I.CONCAT, I.SEXT):
+            imm = n.imm
+        elif op in (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO):
+            width = n.imm
+        elif op == I.ITE:
+            c, a, b = slots[0], slots[1], slots[2]
+        ins.append((op, width, d, a, b, c, imm))
+    return ins, n_lds, n_spill, n_reload
+
+
+def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
+                        table_sizes: Optional[Dict[str, int]] = None,
+                        default_entries: int = 2) -> Program:
+    """Compile Bool constraint nodes (their conjunction is the root bit) and
+    optional probe nodes (256-bit values written per assignment)."""
+    lw = _Lowerer(table_sizes or {}, default_entries)
+    sinks: List[LNode] = []
+    for c in constraints:
+        if not c.is_bool():
+            raise Unsupported("constraint is not Bool")
+        ch = lw.lower(c)
+        lw.birth = c.id
+        sinks.append(lw.mk(I.ROOT, 1, (ch[0],), None))
+    probe_chunks = 0
+    for p in probes:
+        if p.is_array():
+            raise Unsupported("array probe")
+        for ch in lw.lower(p):
+            lw.birth = p.id
+            sinks.append(lw.mk(I.OUT, 1, (ch,), probe_chunks))
+            probe_chunks += 1
+    if not sinks:
+        sinks.append(lw.mk(I.ROOT, 1, (lw.const(1, 1),), None))
+    # comparisons carry their operand width in imm for emission
+    for n in list(lw.table.values()):
+        if n.op in (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO):
+            n.imm = n.width
+            n.width = 1
+    order = _schedule(sinks)
+    const_values = sorted({n.imm & ((1 << 256) - 1) for n in order if n.op == I.CONST})
+    const_index = {v: i for i, v in enumerate(const_values)}
+    ins, n_lds, n_spill, n_reload = _allocate(order, const_index)
+    code = np.zeros((len(ins), 4), dtype=np.uint32)
+    for k, (op, width, d, a, b, c, imm) in enumerate(ins):
+        code[k, 0] = I.w0(op, width)
+        code[k, 1] = I.w1(d, a, b, c)
+        code[k, 2] = imm
+    consts = np.array([_limbs(v) for v in const_values], dtype=np.uint32).reshape(-1, 8)
+    hist: Dict[str, int] = {}
+    for n in order:
+        hist[I.OPNAME[n.op]] = hist.get(I.OPNAME[n.op], 0) + 1
+    stats = {"lnodes": len(order), "n_ins": len(ins), "spills": n_spill, "reloads": n_reload,
+             "hist": hist}
+    return Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
+                   len(constraints), lw.table_sizes, lw.table_kinds, stats)

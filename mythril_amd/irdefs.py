@@ -1,0 +1,39 @@
+"""Opcode table of the mythgpu IR, read from ``include/mythgpu_ir.h`` so the
+Python compiler and the HIP interpreter can never disagree."""
+
+import os
+import re
+
+_HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                    "mythgpu_ir.h")
+
+
+def _parse():
+    ops, defs = {}, {}
+    with open(_HDR) as fh:
+        text = fh.read()
+    for m in re.finditer(r"\bMG_([A-Z0-9_]+)\s*=\s*(\d+)\s*[,\n]", text):
+        ops[m.group(1)] = int(m.group(2))
+    for m in re.finditer(r"#define\s+MG_([A-Z_]+)\s+(\d+)", text):
+        defs[m.group(1)] = int(m.group(2))
+    return ops, defs
+
+
+OPS, DEFINES = _parse()
+NREG = DEFINES["NREG"]
+TRASH = DEFINES["TRASH"]
+MAX_WIDTH = DEFINES["MAX_WIDTH"]
+MAX_LDS = DEFINES["MAX_LDS"]
+MAX_PSLOTS = DEFINES["MAX_PSLOTS"]
+NUM_OPS = OPS["NUM_OPS"]
+OPNAME = {v: k for k, v in OPS.items() if k != "NUM_OPS"}
+
+globals().update({k: v for k, v in OPS.items()})
+
+
+def w0(op: int, width: int) -> int:
+    return op | (width << 8)
+
+
+def w1(d: int, a: int = 0, b: int = 0, c: int = 0) -> int:
+    return d | (a << 8) | (b << 16) | (c << 24)

@@ -1,0 +1,45 @@
+"""ORACLE — test infrastructure only.
+
+Host restatement of the device candidate generator (``gen_leaf`` in
+``mythril_amd/csrc/mg_kernels.hip``; contract in ``include/mythgpu.h``
+``mg_leafgen``), so tests can rebuild the exact assignment a GPU lane
+evaluated and check the lane against ``oracle/smtlib_ref.py``.
+"""
+
+M64 = (1 << 64) - 1
+
+
+def _sm64(s):
+    s = (s + 0x9E3779B97F4A7C15) & M64
+    z = s
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return s, z ^ (z >> 31)
+
+
+def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
+             pct=(50, 70, 85)) -> int:
+    s = (seed ^ ((prog_seed * 0xD1B54A32D192ED03) & M64) ^
+         (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64) ^ ((idx * 0x9E3779B97F4A7C15) & M64)) & M64
+    s, r0 = _sm64(s)
+    cls = (r0 >> 32) % 100
+    lo = r0 & 0xFFFFFFFF
+    mask = (1 << width) - 1
+    if pct[0] <= cls < pct[1]:
+        s, r = _sm64(s)
+        v = r
+    elif pct[1] <= cls < pct[2]:
+        kind = lo % 6
+        k = (lo >> 8) % width
+        v = {0: 0, 1: 1, 2: 1 << (width - 1), 3: (1 << 256) - 1,
+             4: (1 << k) + 1, 5: (1 << k) - 1}[kind]
+    elif cls >= pct[2] and len(pool) > 0:
+        e = (lo >> 3) % len(pool)
+        delta = ((r0 >> 16) & 0xFFFFFFFF) % 3
+        v = (pool[e] + delta - 1) % (1 << 256)
+    else:
+        v = 0
+        for j in range(4):
+            s, r = _sm64(s)
+            v |= r << (64 * j)
+    return v & mask

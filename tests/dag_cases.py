@@ -1,0 +1,177 @@
+"""Test infrastructure: named constraint sets with probes and assignment
+generators, shared by the CPU compiler tests (tests/test_compiler.py, through
+tests/ir_sim.py) and the GPU parity tests (tests/test_gpu_parity.py).
+
+Every probe is a DAG node whose value the engine writes out per assignment,
+so a case checks every intermediate value bit-exactly, not only the root.
+"""
+
+import random
+
+from mythril_amd.smt import node as N
+from oracle.smtlib_ref import Assignment
+
+WIDTHS = (1, 7, 8, 31, 32, 33, 63, 64, 65, 127, 128, 160, 200, 255, 256)
+
+
+def edge_value(rng: random.Random, w: int) -> int:
+    m = (1 << w) - 1
+    k = rng.randrange(10)
+    if k == 0:
+        return 0
+    if k == 1:
+        return 1
+    if k == 2:
+        return m
+    if k == 3:
+        return 1 << (w - 1)
+    if k == 4:
+        return (1 << (w - 1)) - 1
+    if k == 5:
+        return rng.getrandbits(min(w, 64))
+    if k == 6:
+        b = rng.randrange(w)
+        return ((1 << b) + rng.choice((-1, 0, 1))) & m
+    return rng.getrandbits(w)
+
+
+BIN = ["bvadd", "bvsub", "bvmul", "bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod",
+       "bvand", "bvor", "bvxor", "bvshl", "bvlshr", "bvashr"]
+CMP = ["bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge", "bvumul_noovfl"]
+
+
+def all_ops_case(w: int):
+    """Every bit-vector operator at width w on two variables (and a small
+    shift amount), every node probed."""
+    x, y = N.bv_var("x%d" % w, w), N.bv_var("y%d" % w, w)
+    probes = []
+    for op in BIN:
+        probes.append(N.bv_op(op, x, y))
+    probes += [N.bv_op("bvneg", x), N.bv_op("bvnot", y)]
+    bools = [N.bv_cmp(op, x, y) for op in CMP] + [N.eq(x, y), N.distinct(x, y)]
+    probes += [N.ite(b, x, y) for b in bools]
+    if w > 1:
+        lo = w // 3
+        probes.append(N.extract(w - 1, lo, x))
+        probes.append(N.zero_extend(256 - w, x) if w < 256 else x)
+        probes.append(N.sign_extend(256 - w, y) if w < 256 else y)
+        probes.append(N.concat(N.extract(w // 2, 0, x), N.extract(w - 1, w // 2 + 1, y))
+                      if w > 2 else x)
+    if w <= 128:
+        probes.append(N.concat(x, y))
+    constraints = [N.bool_op("or", bools[0], bools[1])]
+
+    def gen(rng):
+        return Assignment(vars={x.params[0]: edge_value(rng, w), y.params[0]: edge_value(rng, w)})
+    return constraints, probes, gen
+
+
+def bool_case():
+    a, b, c = N.bool_var("a"), N.bool_var("b"), N.bool_var("c")
+    x, y = N.bv_var("bx", 256), N.bv_var("by", 256)
+    probes = [N.bool_op("and", a, b, c), N.bool_op("or", a, b, c), N.bool_op("xor", a, b),
+              N.bool_op("not", a), N.bool_op("=>", a, b), N.eq(a, b), N.distinct(a, b, c),
+              N.ite(a, b, c), N.ite(N.bool_op("xor", a, c), x, y),
+              N.distinct(x, y, N.bv_num(3, 256))]
+    constraints = [N.bool_op("or", a, N.bool_op("not", b)), N.bool_op("=>", c, a)]
+
+    def gen(rng):
+        return Assignment(vars={"a": rng.randrange(2), "b": rng.randrange(2), "c": rng.randrange(2),
+                                "bx": edge_value(rng, 256), "by": rng.choice((3, 4, edge_value(rng, 256)))})
+    return constraints, probes, gen
+
+
+def array_case(entries=3):
+    """select over store chains, K arrays, free arrays (model tables), and an
+    array-valued ite — the shapes of calldata/storage/balance reads."""
+    A = N.array_var("A", 256, 256)
+    cd = N.array_var("cd", 256, 8)
+    i, j, k, v = (N.bv_var(n, 256) for n in ("ai", "aj", "ak", "av"))
+    st = N.store(N.store(A, i, v), j, N.bv_op("bvadd", v, N.bv_num(1, 256)))
+    kst = N.store(N.const_array(256, N.bv_num(0, 256)), i, v)
+    c = N.bv_cmp("bvult", i, j)
+    probes = [N.select(A, k), N.select(st, k), N.select(st, i), N.select(st, j),
+              N.select(kst, k), N.select(kst, i), N.select(cd, k),
+              N.select(N.ite(c, st, kst), k)]
+    # calldata word as LASER builds it (calldata.py:219-232): concat of 4 bytes
+    size = N.bv_var("cdsize", 256)
+    parts = []
+    for off in range(4):
+        idx = N.bv_op("bvadd", k, N.bv_num(off, 256))
+        parts.append(N.ite(N.bv_cmp("bvslt", idx, size), N.select(cd, idx), N.bv_num(0, 8)))
+    word = N.concat(*parts)
+    probes.append(word)
+    constraints = [N.eq(N.select(cd, k), N.bv_num(0xA9, 8))]
+
+    def gen(rng):
+        keys = [edge_value(rng, 256) for _ in range(entries)]
+        ivals = [rng.choice(keys + [edge_value(rng, 256)]) for _ in range(3)]
+        tabA = ([(kk, edge_value(rng, 256)) for kk in keys[:rng.randrange(entries + 1)]],
+                edge_value(rng, 256))
+        base = rng.choice(ivals)
+        tabcd = ([((base + o) % (1 << 256), rng.randrange(256)) for o in range(rng.randrange(entries + 1))],
+                 rng.randrange(256))
+        return Assignment(vars={"ai": ivals[0], "aj": ivals[1], "ak": base,
+                                "av": edge_value(rng, 256), "cdsize": rng.choice((0, 2, 4, 100))},
+                          arrays={"A": tabA, "cd": tabcd})
+    return constraints, probes, gen, {"A": entries, "cd": entries}
+
+
+def keccak_uf_case():
+    """The UF-pair shape of keccak_function_manager.py:121-149 on a 512-bit
+    (mapping-slot) input: keccak256_512(concat(key, slot)) with the interval /
+    mod-64 conditions and the inverse function."""
+    key, slot = N.bv_var("kkey", 256), N.bv_var("kslot", 256)
+    data = N.concat(key, slot)
+    f = lambda t: N.apply_uf("keccak256_512", 512, 256, t)        # noqa: E731
+    inv = lambda t: N.apply_uf("keccak256_512-1", 256, 512, t)    # noqa: E731
+    h = f(data)
+    TOTAL_PARTS = 10 ** 40
+    PART = (2 ** 256 - 1) // TOTAL_PARTS
+    lo = (TOTAL_PARTS - 34534) * PART
+    cond = N.bool_op("and", N.eq(inv(h), data),
+                     N.bool_op("or", N.bv_cmp("bvult", N.bv_num(lo, 256), h), N.eq(N.bv_num(lo, 256), h)),
+                     N.bv_cmp("bvult", h, N.bv_num(lo + PART, 256)),
+                     N.eq(N.bv_op("bvurem", h, N.bv_num(64, 256)), N.bv_num(0, 256)))
+    probes = [h, inv(h), N.extract(300, 100, data), N.extract(511, 256, inv(h)),
+              N.zero_extend(256, key)]
+    constraints = [cond]
+
+    def gen(rng):
+        kv, sv = edge_value(rng, 256), rng.randrange(8)
+        d = (kv << 256) | sv
+        hv = lo + 64 * rng.randrange(1 << 20) if rng.randrange(3) else edge_value(rng, 256)
+        fent = [(d, hv)] if rng.randrange(4) else []
+        ient = [(hv, d)] if rng.randrange(4) else [(hv, edge_value(rng, 256))]
+        return Assignment(vars={"kkey": kv, "kslot": sv},
+                          funcs={"keccak256_512": (fent, edge_value(rng, 256)),
+                                 "keccak256_512-1": (ient, rng.getrandbits(512))})
+    return constraints, probes, gen, {"keccak256_512": 2, "keccak256_512-1": 2}
+
+
+def overflow_case():
+    """Mythril's integer-overflow predicates (integer.py:143-157)."""
+    from mythril_amd.smt import BVAddNoOverflow, BVMulNoOverflow, BVSubNoUnderflow, BitVec
+    a, b = N.bv_var("oa", 256), N.bv_var("ob", 256)
+    A, B = BitVec(a), BitVec(b)
+    probes = [BVAddNoOverflow(A, B, False).raw, BVMulNoOverflow(A, B, False).raw,
+              BVSubNoUnderflow(A, B, False).raw]
+    constraints = [N.bool_op("not", probes[0])]
+
+    def gen(rng):
+        return Assignment(vars={"oa": edge_value(rng, 256), "ob": edge_value(rng, 256)})
+    return constraints, probes, gen
+
+
+def named_cases():
+    out = {}
+    for w in WIDTHS:
+        c, p, g = all_ops_case(w)
+        out["ops_w%d" % w] = (c, p, g, {})
+    c, p, g = bool_case()
+    out["bool"] = (c, p, g, {})
+    out["array"] = array_case()
+    out["keccak_uf"] = keccak_uf_case()
+    c, p, g = overflow_case()
+    out["overflow"] = (c, p, g, {})
+    return out

@@ -1,0 +1,135 @@
+"""Host compiler checks on the CPU: compiled IR executed by the reference
+executor (tests/ir_sim.py) must equal direct oracle evaluation of the source
+DAG, for every probe and the root, on every case."""
+
+import random
+
+import numpy as np
+import pytest
+
+import dag_cases
+import ir_sim
+from evm_mini import lower_program
+from mythril_amd import irdefs as I
+from mythril_amd.assign import Assignment as PAssignment, leaf_values, pack, unpack
+from mythril_amd.corpus import make_dag
+from mythril_amd.ir import Unsupported, compile_constraints
+from mythril_amd.smt import node as N
+from oracle import gen_ref
+from oracle import smtlib_ref as R
+from test_oracle_golden import load, oracle_eval
+
+CASES = dag_cases.named_cases()
+
+
+def to_product(asg: R.Assignment) -> PAssignment:
+    return PAssignment(asg.vars, asg.arrays, asg.funcs)
+
+
+def check_program(prog, constraints, probes, assignments):
+    for asg in assignments:
+        lv = leaf_values(prog, to_product(asg))
+        root, got = ir_sim.run(prog, lv)
+        want = R.evaluate(list(probes), asg)
+        # probes of width > 256 come out as consecutive 256-bit chunks
+        flat = []
+        for p, v in zip(probes, want):
+            for k in range((p.width + 255) // 256):
+                flat.append((v >> (256 * k)) & ((1 << min(256, p.width - 256 * k)) - 1))
+        assert got == flat, (asg, [(i, g, w) for i, (g, w) in enumerate(zip(got, flat)) if g != w][:3])
+        assert root == R.eval_constraints(constraints, asg)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_case_through_ir(name):
+    constraints, probes, gen, tables = CASES[name]
+    prog = compile_constraints(constraints, probes, table_sizes=tables)
+    rng = random.Random(hash(name) & 0xFFFF)
+    check_program(prog, constraints, probes, [gen(rng) for _ in range(60)])
+
+
+@pytest.mark.parametrize("t", load("vmtests.json")[::3], ids=lambda t: t["name"])
+def test_vmtest_through_ir(t):
+    vars_, stores, divergent = lower_program(t["code"], oracle_eval)
+    probes = [v.raw for _, v in stores] + [k.raw for k, _ in stores]
+    prog = compile_constraints([], probes)
+    asg = R.Assignment(vars=vars_)
+    lv = leaf_values(prog, to_product(asg))
+    _, got = ir_sim.run(prog, lv)
+    n = len(stores)
+    storage = {}
+    for k, v in zip(got[n:], got[:n]):
+        storage[k] = v
+    storage = {k: v for k, v in storage.items() if v}
+    if not divergent:
+        assert storage == {int(k, 16): int(v, 16) for k, v in t["storage"].items()}
+
+
+@pytest.mark.parametrize("dag_id", range(0, 40, 3))
+def test_corpus_dag_through_ir(dag_id):
+    roots, _ = make_dag(dag_id)
+    prog = compile_constraints(roots)
+    assert prog.stats["lnodes"] > 0
+    pool = prog.const_values
+    for idx in range(12):
+        lv = [gen_ref.gen_leaf(0x1234, dag_id, li, idx, l.width, pool)
+              for li, l in enumerate(prog.leaves)]
+        asg = to_oracle(prog, lv)
+        root, _ = ir_sim.run(prog, lv)
+        assert root == R.eval_constraints(roots, asg)
+
+
+def to_oracle(prog, lv):
+    arr = np.zeros((len(prog.leaves), 8), dtype=np.uint32)
+    for i, v in enumerate(lv):
+        for j in range(8):
+            arr[i, j] = (v >> (32 * j)) & 0xFFFFFFFF
+    a = unpack(prog, arr)
+    return R.Assignment(a.vars, a.arrays, a.funcs)
+
+
+def test_code_invariants():
+    roots, _ = make_dag(5)
+    prog = compile_constraints(roots)
+    code = prog.code
+    ops = code[:, 0] & 0xFF
+    assert (ops < I.NUM_OPS).all()
+    for k in range(4):
+        assert (((code[:, 1] >> (8 * k)) & 0xFF) < I.NREG).all()
+    assert prog.n_lds <= I.MAX_LDS + I.MAX_PSLOTS
+    assert (ops == I.ROOT).sum() == len(roots)
+
+
+def test_pack_unpack_roundtrip():
+    constraints, probes, gen, tables = CASES["keccak_uf"]
+    prog = compile_constraints(constraints, probes, table_sizes=tables)
+    rng = random.Random(3)
+    asgs = [to_product(gen(rng)) for _ in range(5)]
+    soa = pack(prog, asgs)
+    assert soa.shape == (len(prog.leaves), 8, 5)
+    for a in range(5):
+        back = unpack(prog, soa[:, :, a])
+        assert leaf_values(prog, back) == leaf_values(prog, asgs[a])
+
+
+def test_unsupported_array_equality():
+    A, B = N.array_var("A", 256, 256), N.array_var("B", 256, 256)
+    with pytest.raises(Unsupported):
+        compile_constraints([N.eq(A, B)])
+
+
+def test_wide_arithmetic_is_unsupported():
+    x = N.bv_var("w512", 512)
+    with pytest.raises(Unsupported):
+        compile_constraints([N.eq(N.bv_op("bvadd", x, x), x)])
+
+
+def test_deep_concat_chain_compiles():
+    # a 32-byte calldata-style word: 31 CONCATs, and a deep chain of adds
+    bytes_ = [N.bv_var("b%d" % i, 8) for i in range(32)]
+    w = N.concat(*bytes_)
+    acc = w
+    for i in range(3000):
+        acc = N.bv_op("bvadd", acc, N.bv_num(i, 256))
+    prog = compile_constraints([N.bv_cmp("bvult", acc, w)])
+    assert prog.n_ins > 3000

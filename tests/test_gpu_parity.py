@@ -1,0 +1,162 @@
+"""GPU parity: the HIP interpreter (through the C ABI) against the oracle.
+
+Bit-exact for every probed node and every root bit.  Small sizes check every
+lane against ``oracle/smtlib_ref.py``; the full-size test checks a sample of
+lanes of a 2^20-lane launch plus determinism.
+"""
+
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import dag_cases
+from evm_mini import lower_program
+from mythril_amd.assign import Assignment as PAssignment, pack, unpack
+from mythril_amd.corpus import make_dag
+from mythril_amd.engine import limbs_to_int
+from mythril_amd.ir import compile_constraints
+from mythril_amd.smt import node as N
+from oracle import gen_ref
+from oracle import smtlib_ref as R
+from oracle.keccak_ref import keccak256
+from test_oracle_golden import load, oracle_eval
+
+pytestmark = pytest.mark.gpu
+CASES = dag_cases.named_cases()
+
+
+def probe_ints(probes_arr, k, a):
+    return limbs_to_int(probes_arr[k, :, a])
+
+
+def flat_expected(probes, vals):
+    out = []
+    for p, v in zip(probes, vals):
+        for k in range((p.width + 255) // 256):
+            out.append((v >> (256 * k)) & ((1 << min(256, p.width - 256 * k)) - 1))
+    return out
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_case_parity(engine, name):
+    constraints, probes, gen, tables = CASES[name]
+    prog = compile_constraints(constraints, probes, table_sizes=tables)
+    lp = engine.load(prog)
+    rng = random.Random(1000 + len(name))
+    asgs = [gen(rng) for _ in range(333)]          # not a multiple of 64 on purpose
+    soa = pack(prog, [PAssignment(a.vars, a.arrays, a.funcs) for a in asgs])
+    roots, pr = engine.eval(lp, soa, want_probes=True)
+    for a, asg in enumerate(asgs):
+        want = flat_expected(probes, R.evaluate(list(probes), asg))
+        got = [probe_ints(pr, k, a) for k in range(prog.n_probes)]
+        assert got == want, (name, a, [(i, hex(g), hex(w)) for i, (g, w) in
+                                       enumerate(zip(got, want)) if g != w][:4])
+        assert bool(roots[a]) == bool(R.eval_constraints(constraints, asg)), (name, a)
+
+
+def test_vmtests_on_gpu(engine):
+    checked = 0
+    for t in load("vmtests.json"):
+        vars_, stores, divergent = lower_program(t["code"], oracle_eval)
+        if divergent or not stores:
+            continue
+        probes = [v.raw for _, v in stores] + [k.raw for k, _ in stores]
+        prog = compile_constraints([], probes)
+        lp = engine.load(prog)
+        soa = pack(prog, [PAssignment(vars=vars_)])
+        _, pr = engine.eval(lp, soa, want_probes=True)
+        n = len(stores)
+        storage = {}
+        for i in range(n):
+            storage[probe_ints(pr, n + i, 0)] = probe_ints(pr, i, 0)
+        storage = {k: v for k, v in storage.items() if v}
+        assert storage == {int(k, 16): int(v, 16) for k, v in t["storage"].items()}, t["name"]
+        checked += 1
+    assert checked >= 150
+
+
+def test_eip145_on_gpu(engine):
+    vecs = load("eip145.json")
+    x, k = N.bv_var("x", 256), N.bv_var("k", 256)
+    progs = {"shl": N.bv_op("bvshl", x, k), "shr": N.bv_op("bvlshr", x, k),
+             "sar": N.bv_op("bvashr", x, k)}
+    for op, expr in progs.items():
+        vs = [v for v in vecs if v["op"] == op]
+        prog = compile_constraints([], [expr])
+        lp = engine.load(prog)
+        soa = pack(prog, [PAssignment(vars={"x": int(v["value"], 16), "k": int(v["shift"], 16)})
+                          for v in vs])
+        _, pr = engine.eval(lp, soa, want_probes=True)
+        for a, v in enumerate(vs):
+            assert probe_ints(pr, 0, a) == int(v["expected"], 16), v
+
+
+@pytest.mark.parametrize("dag_id", [0, 1, 2, 7, 33, 100, 777, 4095])
+def test_corpus_dag_generated_lanes(engine, dag_id):
+    roots, _ = make_dag(dag_id)
+    prog = compile_constraints(roots)
+    lp = engine.load(prog, prog_seed=dag_id)
+    n = 300
+    seed, first = 0xC0FFEE, 12345
+    bits, _, leaves = engine.eval_gen(lp, seed, first, n, want_leaves=True)
+    pool = prog.const_values
+    for a in range(0, n, 7):
+        lv = [gen_ref.gen_leaf(seed, dag_id, li, first + a, l.width, pool)
+              for li, l in enumerate(prog.leaves)]
+        got_lv = [limbs_to_int(leaves[li, :, a]) for li in range(len(prog.leaves))]
+        assert got_lv == lv, (dag_id, a)
+        asg = unpack(prog, leaves[:, :, a])
+        want = R.eval_constraints(roots, R.Assignment(asg.vars, asg.arrays, asg.funcs))
+        assert bool(bits[a]) == bool(want), (dag_id, a)
+
+
+def test_full_size_sampled_and_deterministic(engine):
+    roots, _ = make_dag(42)
+    prog = compile_constraints(roots)
+    lp = engine.load(prog, prog_seed=42)
+    n = 1 << 20
+    bits1, _, _ = engine.eval_gen(lp, 99, 0, n)
+    bits2, _, _ = engine.eval_gen(lp, 99, 0, n)
+    assert np.array_equal(bits1, bits2)
+    rng = random.Random(5)
+    sample = sorted(rng.sample(range(n), 48)) + [n - 1]
+    for idx in sample:
+        _, _, lv = engine.eval_gen(lp, 99, idx, 1, want_leaves=True)
+        asg = unpack(prog, lv[:, :, 0])
+        want = R.eval_constraints(roots, R.Assignment(asg.vars, asg.arrays, asg.funcs))
+        assert bool(bits1[idx]) == bool(want), idx
+
+
+def test_search_finds_verified_witness(engine):
+    x, y = N.bv_var("sx", 256), N.bv_var("sy", 256)
+    c = [N.bv_cmp("bvult", x, y), N.eq(N.extract(7, 0, x), N.bv_num(0x2A, 8))]
+    prog = compile_constraints(c)
+    lp = engine.load(prog)
+    idx, wit = engine.search(lp, seed=7, n_cand=1 << 22)
+    assert idx >= 0
+    asg = unpack(prog, wit)
+    assert R.eval_constraints(c, R.Assignment(asg.vars)) == 1
+
+
+def test_search_never_claims_unsat_case(engine):
+    x = N.bv_var("ux", 256)
+    c = [N.bv_cmp("bvult", x, N.bv_num(5, 256)), N.bv_cmp("bvugt", x, N.bv_num(9, 256))]
+    prog = compile_constraints(c)
+    idx, _ = engine.search(engine.load(prog), seed=1, n_cand=1 << 20)
+    assert idx == -1
+
+
+def test_keccak_kernel(engine):
+    kats = load("keccak_kat.json")
+    msgs = [bytes.fromhex(k["msg_hex"]) for k in kats]
+    rng = random.Random(11)
+    msgs += [bytes(rng.randrange(256) for _ in range(n)) for n in
+             list(range(0, 140)) + [271, 272, 273, 500, 1000]]
+    got = engine.keccak256(msgs)
+    for m, g in zip(msgs, got):
+        assert g == keccak256(m), len(m)
+    for k, g in zip(kats, got):
+        assert g.hex() == k["digest"][2:]
