@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark: constraint-node evaluations/s on the synthetic corpus (BASELINE
+config C2: 4096 random 256-bit DAGs x 2^20 candidate assignments per GPU).
+
+One step = every DAG of the corpus evaluated under 2^20 device-generated
+candidates (every node, no short-circuit), root bits written to HBM, the
+per-DAG first satisfying candidate reduced with atomicMin and then across
+ranks with an RCCL all-reduce(MIN) — the search's one exchange step.
+Weak scaling: rank r evaluates candidate indices [r*2^20, (r+1)*2^20) of
+every DAG's stream.
+
+Prints ONE JSON line on rank 0 (contract in the task statement).  Extra
+fields: roofline (INT32 VALU bound, see mythril_amd/roofline.py) and
+cpu_baseline (oracle/evalref.c, the C restatement of z3 model evaluation —
+z3 itself is not installed — on host cores, bounded sample).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 0x6D797468
+
+
+def _compile_one(dag_id):
+    from mythril_amd.corpus import make_dag
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.roofline import dag_work
+    roots, _ = make_dag(dag_id, SEED)
+    prog = compile_constraints(roots)
+    nodes, weight = dag_work(roots, prog.table_sizes)
+    return dag_id, prog, nodes, weight
+
+
+def build_corpus(n_dags, workers):
+    if workers <= 1:
+        return [_compile_one(d) for d in range(n_dags)]
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    with ctx.Pool(workers) as pool:
+        return sorted(pool.map(_compile_one, range(n_dags), chunksize=16), key=lambda t: t[0])
+
+
+def cpu_baseline(corpus, budget_s=12.0):
+    """Time the C restatement oracle on a bounded sample of the same workload
+    (same DAGs, same generator) with all host cores."""
+    from mythril_amd.corpus import make_dag
+    from oracle import build as obuild
+    from oracle import evalref
+    obuild.build()
+    threads = min(os.cpu_count() or 1, 64)
+    # calibrate on the first DAG, then spread the budget over a DAG sample
+    sample = corpus[:: max(1, len(corpus) // 64)][:64]
+    total_nodes = 0
+    t_total = 0.0
+    per_dag = None
+    for dag_id, prog, nodes, _ in sample:
+        roots, _ = make_dag(dag_id, SEED)
+        S = evalref.serialize(roots, prog)
+        if per_dag is None:
+            t0 = time.perf_counter()
+            evalref.run_gen(S, prog, SEED, dag_id, 0, 2048, threads)
+            rate = 2048 * nodes / max(time.perf_counter() - t0, 1e-6)
+            per_dag = max(256, int(rate * budget_s / len(sample) / max(nodes, 1)))
+        t0 = time.perf_counter()
+        evalref.run_gen(S, prog, SEED, dag_id, 0, per_dag, threads)
+        t_total += time.perf_counter() - t0
+        total_nodes += nodes * per_dag
+    return {"value": total_nodes / t_total, "unit": "node-evals/s", "cores": threads,
+            "kind": "port",
+            "sample": "%d corpus DAGs x %d generated assignments (%.3g node-evals, %.1f s); "
+                      "oracle/evalref.c restates z3 model evaluation (z3 not installed)"
+                      % (len(sample), per_dag, total_nodes, t_total)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--dags", type=int, default=4096)
+    ap.add_argument("--assign-log2", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    # host-side corpus compile (before any GPU initialisation, so fork is safe)
+    ncpu = os.cpu_count() or 1
+    workers = max(1, min(16, ncpu // max(1, world)))
+    t0 = time.time()
+    corpus = build_corpus(args.dags, workers)
+    t_compile = time.time() - t0
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+
+    from mythril_amd.engine import Engine, default_leafgen
+    eng = Engine(local)
+    loaded = [eng.load(p, default_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
+    batch = eng.batch_create(loaded)
+    n_assign = 1 << args.assign_log2
+    words = (n_assign + 63) // 64
+    d_bits = torch.empty((args.dags, words), dtype=torch.int64, device="cuda")
+    d_first = torch.empty(args.dags, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream()
+    nodes_per_lane = sum(n for _, _, n, _ in corpus)
+    weight_per_lane = sum(w for _, _, _, w in corpus)
+
+    def step(i, ev=None):
+        d_first.fill_(0x7FFFFFFFFFFFFFFF)
+        first = (i * world + rank) * n_assign
+        if ev:
+            ev[0].record(stream)
+        eng.batch_eval_gen(batch, SEED, first, n_assign, d_bits.data_ptr(), d_first.data_ptr(),
+                           stream.cuda_stream)
+        if ev:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_reduce(d_first, op=dist.ReduceOp.MIN)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i, evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    sat_dags = int((d_first != 0x7FFFFFFFFFFFFFFF).sum().item())
+
+    if rank == 0:
+        from mythril_amd.roofline import VALU_PEAK_OPS
+        ms_step = elapsed * 1000.0 / args.steps
+        evals = nodes_per_lane * n_assign * world * args.steps
+        ops_launch = weight_per_lane * n_assign
+        achieved = ops_launch / (kern_ms / 1000.0)
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                with open(args.traffic_json) as fh:
+                    tj = json.load(fh)
+                if tj.get("dags") == args.dags and tj.get("assign_log2") == args.assign_log2:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        out = {
+            "metric": "constraint-node evals/sec",
+            "value": evals / elapsed,
+            "unit": "node-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32x8 (256-bit bit-vectors)",
+            "data": "synthetic (corpus seed 0x6d797468, device-generated candidates)",
+            "config": {"workload": "C2 synthetic corpus: %d random 256-bit DAGs (64-512 nodes) "
+                                   "x 2^%d assignments per GPU" % (args.dags, args.assign_log2),
+                       "dags": args.dags, "assignments_per_gpu": n_assign,
+                       "nodes_total": nodes_per_lane, "parallelism": "dp%d" % world},
+            "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
+                         "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
+                         "traffic": traffic, "kernel_ms": kern_ms,
+                         "int32_ops_per_launch": ops_launch},
+            "sat_dags": sat_dags,
+            "compile_s": round(t_compile, 2),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(corpus)
+            out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

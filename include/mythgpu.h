@@ -95,7 +95,8 @@ int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_ca
               int64_t* first_sat, uint32_t* witness_leaves);
 
 /* Corpus batches: many programs, one launch.  Device-pointer API for
- * resident benchmarking; stream is a hipStream_t (NULL = default stream).
+ * resident benchmarking; stream is a hipStream_t (NULL = the context's own
+ * stream, which the synchronous calls also use).
  *   d_root_bits : device [n_progs][ceil(n_assign/64)] u64 (may be NULL)
  *   d_first_sat : device [n_progs] u64, atomicMin'ed (preset to ~0)     */
 int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, mg_batch** out);

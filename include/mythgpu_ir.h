@@ -8,15 +8,18 @@
  * at and above the width are zero).  Bool is width 1.
  *
  * Instruction = 4 x uint32 (16 bytes, read by scalar loads, wave-uniform):
- *   w0 = op | width << 8                 (width: result width, or operand
- *                                         width for comparisons / UMULNO)
+ *   w0 = op | width << 8 | flags         (width: result width, or operand
+ *                                         width for comparisons / UMULNO;
+ *                                         MG_ROOT_FLAG: result is a conjunct
+ *                                         of the root, ROOT fused in)
  *   w1 = dst | a << 8 | b << 16 | c << 24 (register slots)
  *   w2 = imm0, w3 = imm1                 (per-op immediates, below)
  *
  * Register slots 0..MG_NREG-2 live in VGPRs (per-limb GPR-indexed vectors);
  * slot MG_TRASH receives results nobody reads.  Values that do not fit are
  * spilled with SPILL/RELOAD: the first n_lds spill slots live in LDS, the
- * rest in per-lane scratch.  Every instruction writes `dst`.
+ * rest in per-lane scratch.  Every instruction writes `dst`.  The code array
+ * is followed by one NOP so the interpreter can prefetch instruction pc+1.
  *
  * The semantics of each op is SMT-LIB 2.6 FixedSizeBitVectors as z3 evaluates
  * it (bvudiv x 0 = ~0, bvurem x 0 = x, signed forms per the standard), the
@@ -71,6 +74,8 @@ enum mg_op {
     MG_MOV = 33,     /* dst = R[a]                                            */
     MG_NUM_OPS = 34
 };
+
+#define MG_ROOT_FLAG (1u << 18)
 
 #define MG_INS_W0(op, width) ((unsigned)(op) | ((unsigned)(width) << 8))
 #define MG_INS_W1(d, a, b, c) \

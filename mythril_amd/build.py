@@ -28,27 +28,35 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _deps())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+# Keep uniform (wave-uniform) control flow unstructured: the opcode switch
+# then lowers to a plain scalar binary search with direct branches instead
+# of structurizer "Flow" blocks on every join (fewer SALU per instruction).
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-structurizecfg-skip-uniform-regions=true"]
+
+
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(),
+          flags=None) -> str:
+    if not force and out == LIB and up_to_date():
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     objs = []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, src + ".o")
-        cmd = [HIPCC, "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
+        obj = out + "." + src + ".o"
+        cmd = [HIPCC, "--offload-arch=" + ARCH] + (HIP_FLAGS if flags is None else flags) + \
+              ["-D" + d for d in defines] + [
                "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-c",
                os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs,
                    check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, out)
     for o in objs:
         os.remove(o)
-    return LIB
+    return out
 
 
 if __name__ == "__main__":

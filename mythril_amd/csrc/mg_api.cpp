@@ -144,7 +144,8 @@ static int validate(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, uint32_t 
         const uint32_t* in = code + 4 * pc;
         const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm0 = in[2];
         if (op >= MG_NUM_OPS) return fail(ctx, MG_E_ARG, "ins %u: bad opcode %u", pc, op);
-        if ((in[0] >> 18) != 0) return fail(ctx, MG_E_ARG, "ins %u: reserved bits set", pc);
+        if ((in[0] & ~(0x3FFFFu | MG_ROOT_FLAG)) != 0)
+            return fail(ctx, MG_E_ARG, "ins %u: reserved bits set", pc);
         for (int k = 0; k < 4; ++k)
             if (((in[1] >> (8 * k)) & 0xFF) >= MG_NREG)
                 return fail(ctx, MG_E_ARG, "ins %u: slot out of range", pc);
@@ -193,13 +194,13 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
                       n_probes);
     if (rc) return rc;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
-    const size_t code_b = (size_t)n_ins * 16, const_b = (size_t)n_consts * 32,
+    const size_t code_b = (size_t)(n_ins + 1) * 16, const_b = (size_t)n_consts * 32,
                  gen_b = (size_t)n_leaves * sizeof(mg_leafgen);
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t off_const = align(code_b), off_gen = off_const + align(const_b),
                  off_desc = off_gen + align(gen_b), total = off_desc + align(sizeof(mg_pdesc));
     std::vector<uint8_t> blob(total, 0);
-    if (code_b) memcpy(blob.data(), code, code_b);
+    if (n_ins) memcpy(blob.data(), code, (size_t)n_ins * 16);   // + zeroed NOP pad
     if (const_b) memcpy(blob.data() + off_const, consts, const_b);
     if (gen_b) memcpy(blob.data() + off_gen, leaves, gen_b);
     void* d = nullptr;
@@ -404,7 +405,7 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
                       uint64_t n_assign, uint64_t* d_root_bits, uint64_t* d_first_sat,
                       void* stream) {
     if (!ctx || !b) return fail(ctx, MG_E_ARG, "null argument");
-    hipStream_t s = (hipStream_t)stream;
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     const uint64_t words = (n_assign + 63) / 64;
     for (uint32_t p0 = 0; p0 < b->n; p0 += 65535) {
         const uint32_t np = b->n - p0 < 65535 ? b->n - p0 : 65535;

@@ -211,12 +211,15 @@ DEV void udivrem256(const uint32_t* u, const uint32_t* v, uint32_t* q, uint32_t*
             un[j + i] = __builtin_subc(un[j + i], (uint32_t)p, bo, &bo);
         }
         un[j + 8] = __builtin_subc(un[j + 8], carry, bo, &bo);
-        // add back when the partial remainder went negative (rare)
-        const uint32_t m = 0u - bo;
-        unsigned c = 0;
+        // add back when the partial remainder went negative (probability
+        // ~2/2^32 per lane: skipped unless some lane of the wave needs it)
+        if (__any(bo)) {
+            const uint32_t m = 0u - bo;
+            unsigned c = 0;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) un[j + i] = __builtin_addc(un[j + i], vn[i] & m, c, &c);
-        un[j + 8] += c & bo;
+            for (int i = 0; i < 8; ++i) un[j + i] = __builtin_addc(un[j + i], vn[i] & m, c, &c);
+            un[j + 8] += c & bo;
+        }
         q[j] = qh - bo;
     }
     shr_n<9, 8>(un, sh, rem);
@@ -359,18 +362,30 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
     const uint32_t n_lds = D->n_lds;
     uint4 pspill[2 * MG_MAX_PSLOTS];   // per-lane scratch tier (uniform index)
 
+    // software-pipelined fetch: the next instruction's scalar loads are in
+    // flight while the current one executes (the host pads code with a NOP)
+    // The next instruction is fetched with an explicit s_load issued BEFORE
+    // the current one executes and waited for only at the end of the
+    // iteration (left to itself the compiler sinks the load to the back-edge
+    // and exposes the scalar-cache latency on every instruction).
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const uint32_t* ip = (const uint32_t*)code;
+    u32x4 cur;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)"
+                 : "=s"(cur) : "s"(ip) : "memory");
     for (uint32_t pc = 0; pc < n_ins; ++pc) {
-        const uint32_t w0 = code[4 * pc + 0];
-        const uint32_t w1 = code[4 * pc + 1];
-        const uint32_t imm0 = code[4 * pc + 2];
+        u32x4 nxt;
+        asm volatile("s_load_dwordx4 %0, %1, 0x10" : "=s"(nxt) : "s"(ip) : "memory");
+        const uint32_t c_w0 = cur.x, c_w1 = cur.y, c_imm = cur.z;
+        const uint32_t w0 = c_w0, w1 = c_w1, imm0 = c_imm;
         const uint32_t op = w0 & 0xFF;
         const uint32_t w = (w0 >> 8) & 0x3FF;
         const uint32_t sd = w1 & 15, sa = (w1 >> 8) & 15, sb = (w1 >> 16) & 15, sc = (w1 >> 24) & 15;
 
+        // operands are read inside the cases that need them (GPR-index moves)
         uint32_t x[8], y[8], r[8];
-        READ_SLOT(x, sa);
-        READ_SLOT(y, sb);
-        const uint32_t cflag = F0[sc] & 1u;
+#define RX READ_SLOT(x, sa)
+#define RY READ_SLOT(y, sb)
 #pragma unroll
         for (int j = 0; j < 8; ++j) r[j] = 0;
 
@@ -399,6 +414,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             break;
         }
         case MG_SPILL: {
+            RX;
             const uint4 a = make_uint4(x[0], x[1], x[2], x[3]);
             const uint4 b = make_uint4(x[4], x[5], x[6], x[7]);
             if (imm0 < n_lds) {
@@ -427,29 +443,34 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
             break;
         }
-        case MG_ADD: add256(x, y, r); mask_to(r, w); break;
-        case MG_SUB: (void)sub256(x, y, r); mask_to(r, w); break;
-        case MG_NEG: neg256(x, r); mask_to(r, w); break;
-        case MG_MUL: mul256(x, y, r); mask_to(r, w); break;
+        case MG_ADD: RX; RY; add256(x, y, r); mask_to(r, w); break;
+        case MG_SUB: RX; RY; (void)sub256(x, y, r); mask_to(r, w); break;
+        case MG_NEG: RX; neg256(x, r); mask_to(r, w); break;
+        case MG_MUL: RX; RY; mul256(x, y, r); mask_to(r, w); break;
         case MG_AND:
+            RX; RY;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = x[j] & y[j];
             break;
         case MG_OR:
+            RX; RY;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = x[j] | y[j];
             break;
         case MG_XOR:
+            RX; RY;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = x[j] ^ y[j];
             break;
         case MG_NOT:
+            RX;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = ~x[j];
             mask_to(r, w);
             break;
         case MG_UDIV:
         case MG_UREM: {
+            RX; RY;
             const uint32_t z = is_zero256(y);
             y[0] |= z;                               // divisor 0 -> 1 (fixed below)
             uint32_t q[8], m[8];
@@ -467,6 +488,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
         case MG_SDIV:
         case MG_SREM:
         case MG_SMOD: {
+            RX; RY;
             sext_from(x, w);
             sext_from(y, w);
             const uint32_t ns = sign256(x), nt = sign256(y);
@@ -514,6 +536,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
         case MG_SHL:
         case MG_LSHR:
         case MG_ASHR: {
+            RX; RY;
             uint32_t hi = y[1] | y[2] | y[3] | y[4] | y[5] | y[6] | y[7];
             const bool over = hi != 0 || y[0] >= w;
             const uint32_t s = y[0] & 255u;
@@ -539,16 +562,18 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             break;
         }
         case MG_EQ: {
+            RX; RY;
             uint32_t o = 0;
 #pragma unroll
             for (int j = 0; j < 8; ++j) o |= x[j] ^ y[j];
             r[0] = o == 0;
             break;
         }
-        case MG_ULT: r[0] = ult256(x, y); break;
-        case MG_ULE: r[0] = 1u - ult256(y, x); break;
+        case MG_ULT: RX; RY; r[0] = ult256(x, y); break;
+        case MG_ULE: RX; RY; r[0] = 1u - ult256(y, x); break;
         case MG_SLT:
         case MG_SLE: {
+            RX; RY;
             sext_from(x, w);
             sext_from(y, w);
             x[7] ^= 0x80000000u;
@@ -557,6 +582,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             break;
         }
         case MG_UMULNO: {
+            RX; RY;
             uint32_t p[16];
             mul512(x, y, p);
             uint32_t o = 0;
@@ -565,11 +591,15 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             r[0] = o == 0;
             break;
         }
-        case MG_ITE:
+        case MG_ITE: {
+            RX; RY;
+            const uint32_t cflag = F0[sc] & 1u;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = cflag ? x[j] : y[j];
             break;
+        }
         case MG_CONCAT: {
+            RX; RY;
             uint32_t t[8];
             shl_n<8>(x, imm0, t);
 #pragma unroll
@@ -578,33 +608,44 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             break;
         }
         case MG_EXTRACT:
+            RX;
             shr_n<8, 8>(x, imm0, r);
             mask_to(r, w);
             break;
         case MG_SEXT:
+            RX;
             sext_from(x, imm0);
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = x[j];
             mask_to(r, w);
             break;
         case MG_OUT:
+            RX;
             if (run.probes && active) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     run.probes[((size_t)imm0 * 8 + j) * run.stride + gid] = x[j];
             }
             break;
-        case MG_ROOT: root &= x[0] & 1u; break;
+        case MG_ROOT: root &= F0[sa] & 1u; break;
         case MG_MOV:
+            RX;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = x[j];
             break;
         default: break;
         }
+#undef RX
+#undef RY
+        // fused ROOT: the result of this instruction is a conjunct of the root
+        if (w0 & MG_ROOT_FLAG) root &= r[0] & 1u;
 
         // single write point: F[sd] = r  (gpr_idx(DST) moves, no file copies)
         F0[sd] = r[0]; F1[sd] = r[1]; F2[sd] = r[2]; F3[sd] = r[3];
         F4[sd] = r[4]; F5[sd] = r[5]; F6[sd] = r[6]; F7[sd] = r[7];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        cur = nxt;
+        ip += 4;
     }
 
     const unsigned long long bits = __ballot(active && root);

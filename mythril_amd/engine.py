@@ -42,16 +42,16 @@ class Gen(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("first_index", C.c_uint64)]
 
 
-_lib = None
+_libs: Dict[str, object] = {}
 _lib_lock = threading.Lock()
 
 
 def load_library(path: str = _LIB_PATH):
-    """Load libmythgpu.so (no GPU needed) and declare every export."""
-    global _lib
+    """Load libmythgpu.so (no GPU needed) and declare every export.  Other
+    paths (A/B builds of the same ABI) load side by side."""
     with _lib_lock:
-        if _lib is not None:
-            return _lib
+        if path in _libs:
+            return _libs[path]
         if not os.path.exists(path):
             raise EngineUnavailable("libmythgpu.so not built (%s); run "
                                     "`python -m mythril_amd.build`" % path)
@@ -77,7 +77,7 @@ def load_library(path: str = _LIB_PATH):
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
         for name in EXPORTS:
             getattr(lib, name)
-        _lib = lib
+        _libs[path] = lib
         return lib
 
 
@@ -110,8 +110,8 @@ class LoadedProgram:
 class Engine:
     """One HIP device context (one per host thread)."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_library()
+    def __init__(self, device: int = 0, lib_path: str = _LIB_PATH):
+        self.lib = load_library(lib_path)
         ctx = C.c_void_p()
         rc = self.lib.mg_init(device, C.byref(ctx))
         if rc != 0:

@@ -24,6 +24,7 @@ NREG = DEFINES["NREG"]
 TRASH = DEFINES["TRASH"]
 MAX_WIDTH = DEFINES["MAX_WIDTH"]
 MAX_LDS = DEFINES["MAX_LDS"]
+ROOT_FLAG = 1 << 18          # MG_ROOT_FLAG: w0 bit 18, ROOT fused into the producer
 MAX_PSLOTS = DEFINES["MAX_PSLOTS"]
 NUM_OPS = OPS["NUM_OPS"]
 OPNAME = {v: k for k, v in OPS.items() if k != "NUM_OPS"}

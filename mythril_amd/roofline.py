@@ -1,0 +1,87 @@
+"""Algorithmic work accounting for the constraint-node-evals/s metric.
+
+Unit of work: one source-DAG node (after hash-consing CSE)
+evaluated under one assignment.  The roofline is INT32 VALU: each node is
+priced with a FIXED int32-op weight chosen independently of the
+implementation (SURVEY.md §8d "Algorithmic work per unit"):
+
+    ADD/SUB/NEG, AND/OR/XOR/NOT, EQ/DISTINCT/ULT/ULE/SLT/SLE(/GT/GE), BV ITE,
+    CONCAT/EXTRACT/ZERO_EXT/SIGN_EXT                        8
+    Bool and/or/xor/not/implies with k args                  max(1, k-1)
+    SHL/LSHR/ASHR                                            24
+    MUL                                                      192
+    bvumul_noovfl                                            320
+    UDIV/UREM/SDIV/SREM/SMOD                                 512
+    SELECT over a store chain of length s                    8*s + 8
+    free-array / UF lookup with e table entries              8*e + 8
+
+A w-bit op scales by ceil(w/32)/8 (a 256-bit op is the unit).  Leaves
+(variables, numerals, free and constant arrays) are not nodes; store nodes
+are nodes of weight 0 (they are priced inside the selects that read them).
+
+Peak: MI355X vector ALU, 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz =
+78.6 T int32 lane-ops/s (MI355X_MICROARCH.md: a wave64 VALU op issues in 2
+cycles on a SIMD-32, FP32 vector peak 157.3 TFLOPS = 78.6 T FMA/s).
+"""
+
+from __future__ import annotations
+
+from typing import Dict, Iterable, Tuple
+
+from .smt.node import Node, topo_order
+
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9          # int32 lane-ops/s
+HBM_PEAK_BPS = 8.0e12
+
+_W8 = {"bvadd", "bvsub", "bvneg", "bvand", "bvor", "bvxor", "bvnot", "=", "distinct",
+       "bvult", "bvule", "bvugt", "bvuge", "bvslt", "bvsle", "bvsgt", "bvsge", "ite",
+       "concat", "extract", "zero_extend", "sign_extend"}
+_BOOL = {"and", "or", "xor", "not", "=>"}
+_LEAF = {"var", "bvnum", "true", "false", "array", "K"}
+
+
+def _scale(w: int) -> float:
+    return ((w + 31) // 32) / 8.0
+
+
+def node_weight(n: Node, table_sizes: Dict[str, int]) -> float:
+    op = n.op
+    if op in _LEAF or op == "store":
+        return 0.0
+    if n.is_bool() and op in _BOOL:
+        return float(max(1, len(n.args) - 1))
+    w = n.args[0].width if n.args and n.args[0].is_bv() else n.width
+    if op in ("ite", "=", "distinct") and n.args and n.args[-1].is_bool():
+        return 1.0
+    if op in _W8:
+        return 8.0 * _scale(max(w, n.width))
+    if op in ("bvshl", "bvlshr", "bvashr"):
+        return 24.0 * _scale(w)
+    if op == "bvmul":
+        return 192.0 * _scale(w) * (len(n.args) - 1)
+    if op == "bvumul_noovfl":
+        return 320.0 * _scale(w)
+    if op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod"):
+        return 512.0 * _scale(w)
+    if op == "select":
+        s, a = 0, n.args[0]
+        while a.op == "store":
+            s, a = s + 1, a.args[0]
+        extra = 8 * table_sizes.get(a.params[0], 2) + 8 if a.op == "array" else 0
+        return 8.0 * s + 8.0 + extra
+    if op == "apply":
+        return 8.0 * table_sizes.get(n.params[0], 2) + 8.0
+    return 8.0
+
+
+def dag_work(roots: Iterable[Node], table_sizes: Dict[str, int] = None) -> Tuple[int, float]:
+    """(node count, int32-op weight) of the DAG reachable from ``roots``."""
+    ts = table_sizes or {}
+    nodes = 0
+    weight = 0.0
+    for n in topo_order(list(roots)):
+        if n.op in _LEAF:
+            continue
+        nodes += 1
+        weight += node_weight(n, ts)
+    return nodes, weight

@@ -1,0 +1,225 @@
+"""ORACLE — test infrastructure / CPU baseline only.
+
+ctypes wrapper of ``oracle/evalref.c`` (the C restatement of z3's evaluation
+of a get_model DAG).  :func:`serialize` flattens a SOURCE constraint DAG into
+the C oracle's node records; leaves are numbered like the compiled
+:class:`mythril_amd.ir.Program` so both sides read the same assignment.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from mythril_amd.smt.node import Node, topo_order
+
+from . import build as _build
+
+E = {name: i + 1 for i, name in enumerate(
+    "NUM VAR TRUE FALSE ADD SUB MUL UDIV UREM SDIV SREM SMOD AND OR XOR NOT NEG SHL LSHR ASHR "
+    "CONCAT EXTRACT ZEXT SEXT EQ ULT ULE SLT SLE UMULNO ITE BAND BOR BXOR BNOT SELECT STORE "
+    "KARR ARRVAR APPLY".split())}
+
+_BIN = {"bvadd": "ADD", "bvsub": "SUB", "bvmul": "MUL", "bvudiv": "UDIV", "bvurem": "UREM",
+        "bvsdiv": "SDIV", "bvsrem": "SREM", "bvsmod": "SMOD", "bvand": "AND", "bvor": "OR",
+        "bvxor": "XOR", "bvshl": "SHL", "bvlshr": "LSHR", "bvashr": "ASHR"}
+_CMP = {"bvult": ("ULT", 0), "bvule": ("ULE", 0), "bvugt": ("ULT", 1), "bvuge": ("ULE", 1),
+        "bvslt": ("SLT", 0), "bvsle": ("SLE", 0), "bvsgt": ("SLT", 1), "bvsge": ("SLE", 1),
+        "bvumul_noovfl": ("UMULNO", 0)}
+
+
+class TableDesc(C.Structure):
+    _fields_ = [("key_w", C.c_uint32), ("val_w", C.c_uint32), ("entries", C.c_uint32),
+                ("else_leaf", C.c_uint32), ("key_leaf_off", C.c_uint32),
+                ("val_leaf_off", C.c_uint32)]
+
+
+class Serialized:
+    def __init__(self):
+        self.recs: List[List[int]] = []
+        self.consts: List[int] = []
+        self.roots: List[int] = []
+        self.tables: List[TableDesc] = []
+        self.leafidx: List[int] = []
+        self.node_index: Dict[int, int] = {}
+
+
+def serialize(constraints: Sequence[Node], program, probes: Sequence[Node] = ()) -> Serialized:
+    li = program.leaf_index()
+    S = Serialized()
+    const_ix: Dict[int, int] = {}
+    table_ix: Dict[str, int] = {}
+
+    def rec(op, w, a0=0, a1=0, a2=0, p0=0, p1=0):
+        S.recs.append([E[op], w, a0, a1, a2, p0, p1, 0])
+        return len(S.recs) - 1
+
+    def const(v):
+        if v not in const_ix:
+            const_ix[v] = len(S.consts)
+            S.consts.append(v)
+        return const_ix[v]
+
+    def table(name, key_w, val_w):
+        if name not in table_ix:
+            n = program.table_sizes[name]
+            koff = len(S.leafidx)
+            S.leafidx += [li["%s#k%d#0" % (name, e)] for e in range(n)]
+            voff = len(S.leafidx)
+            S.leafidx += [li["%s#v%d#0" % (name, e)] for e in range(n)]
+            table_ix[name] = len(S.tables)
+            S.tables.append(TableDesc(key_w, val_w, n, li["%s#else#0" % name], koff, voff))
+        return table_ix[name]
+
+    ix = S.node_index
+    for n in topo_order(list(constraints) + list(probes)):
+        op, w = n.op, n.width
+        a = [ix.get(x.id, 0) for x in n.args]
+        if op == "bvnum":
+            r = rec("NUM", w, p0=const(n.params[0]))
+        elif op == "var":
+            name = n.params[0] if w <= 256 else n.params[0] + "#0"
+            r = rec("VAR", w, p0=li[name])
+        elif op in ("true", "false"):
+            r = rec(op.upper(), 1)
+        elif op in _BIN:
+            r = a[0]
+            for x in a[1:]:
+                r = rec(_BIN[op], w, r, x)
+        elif op in ("bvnot", "not"):
+            r = rec("NOT" if op == "bvnot" else "BNOT", w, a[0])
+        elif op == "bvneg":
+            r = rec("NEG", w, a[0])
+        elif op in ("and", "or"):
+            r = a[0]
+            for x in a[1:]:
+                r = rec("BAND" if op == "and" else "BOR", 1, r, x)
+        elif op == "xor":
+            r = rec("BXOR", 1, a[0], a[1])
+        elif op == "=>":
+            r = rec("BOR", 1, rec("BNOT", 1, a[0]), a[1])
+        elif op in _CMP:
+            name, swap = _CMP[op]
+            x, y = (a[1], a[0]) if swap else (a[0], a[1])
+            r = rec(name, 1, x, y, p0=n.args[0].width)
+        elif op == "=":
+            r = rec("EQ", 1, a[0], a[1])
+        elif op == "distinct":
+            terms = [rec("BNOT", 1, rec("EQ", 1, a[i], a[j]))
+                     for i in range(len(a)) for j in range(i + 1, len(a))]
+            r = terms[0]
+            for t in terms[1:]:
+                r = rec("BAND", 1, r, t)
+        elif op == "ite":
+            r = rec("ITE", w, a[0], a[1], a[2])
+        elif op == "concat":
+            r, acc_w = a[0], n.args[0].width
+            for x, arg in zip(a[1:], n.args[1:]):
+                acc_w += arg.width
+                r = rec("CONCAT", acc_w, r, x, p0=arg.width)
+        elif op == "extract":
+            hi, lo = n.params
+            r = rec("EXTRACT", w, a[0], p1=lo)
+        elif op == "zero_extend":
+            r = rec("ZEXT", w, a[0])
+        elif op == "sign_extend":
+            r = rec("SEXT", w, a[0], p0=n.params[0])
+        elif op == "array":
+            r = rec("ARRVAR", w, p0=table(n.params[0], n.dom, w))
+        elif op == "K":
+            r = rec("KARR", w, a[0])
+        elif op == "store":
+            r = rec("STORE", w, a[0], a[1], a[2])
+        elif op == "select":
+            r = rec("SELECT", w, a[0], a[1])
+        elif op == "apply":
+            fname, dom = n.params
+            r = rec("APPLY", w, a[0], p0=table(fname, dom, w))
+        else:
+            raise NotImplementedError(op)
+        ix[n.id] = r
+    S.roots = [ix[c.id] for c in constraints]
+    return S
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = _build.LIB
+        if not os.path.exists(path):
+            _build.build()
+        L = C.CDLL(path)
+        p = C.c_void_p
+        L.ev_run_gen.argtypes = [p, C.c_uint32, p, p, C.c_uint32, p, p, C.c_uint32, p, C.c_uint32,
+                                 p, C.c_uint32, p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64,
+                                 p, C.c_int]
+        L.ev_run_leaves.argtypes = [p, C.c_uint32, p, p, C.c_uint32, p, p, C.c_uint32, C.c_uint32,
+                                    p, C.c_uint64, p, p]
+        _lib = L
+    return _lib
+
+
+def _arrays(S: Serialized):
+    nodes = np.ascontiguousarray(np.array(S.recs, dtype=np.uint32).reshape(-1, 8))
+    consts = np.zeros((max(1, len(S.consts)), 8), dtype=np.uint64)
+    for i, v in enumerate(S.consts):
+        for k in range(8):
+            consts[i, k] = (v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
+    tabs = (TableDesc * max(1, len(S.tables)))(*S.tables)
+    leafidx = np.array(S.leafidx or [0], dtype=np.uint32)
+    roots = np.array(S.roots or [0], dtype=np.uint32)
+    return nodes, consts, tabs, leafidx, roots
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def run_gen(S: Serialized, program, seed: int, prog_seed: int, first: int, n: int,
+            threads: int = 0, pct=(50, 70, 85)) -> np.ndarray:
+    nodes, consts, tabs, leafidx, roots = _arrays(S)
+    widths = np.array([l.width for l in program.leaves] or [1], dtype=np.uint32)
+    pool = np.zeros((max(1, len(program.const_values)), 8), dtype=np.uint64)
+    for i, v in enumerate(program.const_values):
+        for k in range(4):
+            pool[i, k] = (v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
+    pctv = np.array(pct, dtype=np.uint32)
+    out = np.zeros(n, dtype=np.uint8)
+    rc = lib().ev_run_gen(_p(nodes), nodes.shape[0], _p(consts), C.cast(tabs, C.c_void_p),
+                          len(S.tables), _p(leafidx), _p(roots), len(S.roots), _p(widths),
+                          len(program.leaves), _p(pool), len(program.const_values), _p(pctv),
+                          seed & (2**64 - 1), prog_seed & (2**64 - 1), first, n, _p(out), threads)
+    assert rc == 0
+    return out.astype(bool)
+
+
+def run_leaves(S: Serialized, program, leaf_vals: Sequence[Sequence[int]], want_nodes=False):
+    """leaf_vals: per assignment, the program's leaf values (<= 256 bits)."""
+    nodes, consts, tabs, leafidx, roots = _arrays(S)
+    n = len(leaf_vals)
+    nl = len(program.leaves)
+    lv = np.zeros((max(1, n), max(1, nl), 4), dtype=np.uint64)
+    for a, vals in enumerate(leaf_vals):
+        for i, v in enumerate(vals):
+            for k in range(4):
+                lv[a, i, k] = (v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
+    vals_out = np.zeros((n, nodes.shape[0], 8), dtype=np.uint64) if want_nodes else None
+    out = np.zeros(max(1, n), dtype=np.uint8)
+    rc = lib().ev_run_leaves(_p(nodes), nodes.shape[0], _p(consts), C.cast(tabs, C.c_void_p),
+                             len(S.tables), _p(leafidx), _p(roots), len(S.roots), nl, _p(lv), n,
+                             None if vals_out is None else _p(vals_out), _p(out))
+    assert rc == 0
+    return out[:n].astype(bool), vals_out
+
+
+def node_value(vals_out, a: int, rec_index: int) -> int:
+    v = 0
+    for k in reversed(range(8)):
+        v = (v << 64) | int(vals_out[a, rec_index, k])
+    return v

@@ -93,9 +93,13 @@ def run(program, leaf_vals):
             probes[imm] = x
         elif op == I.ROOT:
             root &= x & 1
+        elif op == I.NOP:
+            pass
         elif op == I.MOV:
             r = x
         else:
             raise AssertionError("op %d" % op)
+        if w0 & I.ROOT_FLAG:
+            root &= r & 1
         regs[d] = r
     return root, [probes.get(i, 0) for i in range(program.n_probes)]

@@ -97,7 +97,9 @@ def test_code_invariants():
     for k in range(4):
         assert (((code[:, 1] >> (8 * k)) & 0xFF) < I.NREG).all()
     assert prog.n_lds <= I.MAX_LDS + I.MAX_PSLOTS
-    assert (ops == I.ROOT).sum() == len(roots)
+    fused = (code[:, 0] & I.ROOT_FLAG) != 0
+    assert (ops == I.ROOT).sum() + fused.sum() == len(roots)
+    assert fused.sum() > 0
 
 
 def test_pack_unpack_roundtrip():
