@@ -113,6 +113,9 @@ int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
 
 /* Library/ABI version (no GPU needed). */
 int mg_version(void);
+/* Build configuration (no GPU needed): out[0..3] = version, MG_NREG,
+ * MG_MAX_LDS, MG_MAX_PSLOTS — programs must be compiled for these. */
+int mg_config(uint32_t* out, uint32_t n);
 
 #ifdef __cplusplus
 }

@@ -19,7 +19,7 @@
  * slot MG_TRASH receives results nobody reads.  Values that do not fit are
  * spilled with SPILL/RELOAD: the first n_lds spill slots live in LDS, the
  * rest in per-lane scratch.  Every instruction writes `dst`.  The code array
- * is followed by one NOP so the interpreter can prefetch instruction pc+1.
+ * is followed by 8 NOPs so the interpreter can prefetch ahead.
  *
  * The semantics of each op is SMT-LIB 2.6 FixedSizeBitVectors as z3 evaluates
  * it (bvudiv x 0 = ~0, bvurem x 0 = x, signed forms per the standard), the
@@ -29,8 +29,12 @@
 #ifndef MYTHGPU_IR_H
 #define MYTHGPU_IR_H
 
-#define MG_NREG 16           /* VGPR slots per lane (per-limb v16 vectors)   */
-#define MG_TRASH 15          /* result sink                                   */
+#ifdef MG_NREG_OVERRIDE      /* A/B builds only                               */
+#define MG_NREG MG_NREG_OVERRIDE
+#else
+#define MG_NREG 16           /* VGPR slots per lane (per-limb GPR-indexed vectors) */
+#endif
+#define MG_TRASH (MG_NREG - 1) /* result sink                                 */
 #define MG_LIMBS 8           /* 8 x 32-bit limbs = 256 bits                   */
 #define MG_MAX_WIDTH 256
 #define MG_MAX_LDS 10        /* LDS spill slots: 10 x 8 KiB per 256-lane block

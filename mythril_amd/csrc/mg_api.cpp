@@ -82,6 +82,13 @@ extern "C" {
 
 int mg_version(void) { return MG_VERSION; }
 
+int mg_config(uint32_t* out, uint32_t n) {
+    const uint32_t cfg[4] = {MG_VERSION, MG_NREG, MG_MAX_LDS, MG_MAX_PSLOTS};
+    if (!out) return MG_E_ARG;
+    for (uint32_t i = 0; i < n && i < 4; ++i) out[i] = cfg[i];
+    return MG_OK;
+}
+
 int mg_init(int device, mg_ctx** out) {
     if (!out) return MG_E_ARG;
     *out = nullptr;
@@ -194,13 +201,14 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
                       n_probes);
     if (rc) return rc;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
-    const size_t code_b = (size_t)(n_ins + 1) * 16, const_b = (size_t)n_consts * 32,
+    // 8 zeroed NOPs after the code: the interpreter prefetches up to 8 ahead
+    const size_t code_b = (size_t)(n_ins + 8) * 16, const_b = (size_t)n_consts * 32,
                  gen_b = (size_t)n_leaves * sizeof(mg_leafgen);
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t off_const = align(code_b), off_gen = off_const + align(const_b),
                  off_desc = off_gen + align(gen_b), total = off_desc + align(sizeof(mg_pdesc));
     std::vector<uint8_t> blob(total, 0);
-    if (n_ins) memcpy(blob.data(), code, (size_t)n_ins * 16);   // + zeroed NOP pad
+    if (n_ins) memcpy(blob.data(), code, (size_t)n_ins * 16);   // + zeroed NOP padding
     if (const_b) memcpy(blob.data() + off_const, consts, const_b);
     if (gen_b) memcpy(blob.data() + off_gen, leaves, gen_b);
     void* d = nullptr;

@@ -24,7 +24,9 @@
 #include "mythgpu_ir.h"
 #include "mg_device.h"
 
-typedef uint32_t v16u __attribute__((ext_vector_type(16)));
+// one GPR-indexed vector per limb; MG_NREG must be a register-tuple size
+// (8, 12 or 16) for index-mode moves
+typedef uint32_t vfile __attribute__((ext_vector_type(MG_NREG)));
 // constant address space: uniform loads through it become s_load (scalar
 // cache), which keeps opcodes and slot indices in SGPRs
 typedef __attribute__((address_space(4))) const uint32_t cu32;
@@ -220,8 +222,13 @@ DEV void udivrem256(const uint32_t* u, const uint32_t* v, uint32_t* q, uint32_t*
             for (int i = 0; i < 8; ++i) un[j + i] = __builtin_addc(un[j + i], vn[i] & m, c, &c);
             un[j + 8] += c & bo;
         }
-        q[j] = qh - bo;
+        // the window's top digit is now 0 and never read again: keep the
+        // quotient digit there (no separate live quotient registers)
+        un[j + 8] = qh - bo;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) q[j] = un[j + 8];
+    un[8] = 0;
     shr_n<9, 8>(un, sh, rem);
 }
 
@@ -337,8 +344,12 @@ DEV void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t idx
         dst[4] = F4[idx]; dst[5] = F5[idx]; dst[6] = F6[idx]; dst[7] = F7[idx];  \
     } while (0)
 
+#ifndef MG_WAVES_PER_SIMD
+#define MG_WAVES_PER_SIMD 2
+#endif
+
 template <int GEN>
-__global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict__ descs,
+__global__ __launch_bounds__(BLOCK, MG_WAVES_PER_SIMD) void mg_interp(const mg_pdesc* __restrict__ descs,
                                                       mg_run run) {
     extern __shared__ uint4 lds[];
     const uint32_t prog = blockIdx.y;
@@ -352,9 +363,9 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
     const bool active = gid < run.n_assign;
     const uint64_t lane_idx = active ? gid : 0;   // inactive lanes replay lane 0
 
-    v16u F0, F1, F2, F3, F4, F5, F6, F7;
+    vfile F0, F1, F2, F3, F4, F5, F6, F7;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
+    for (int i = 0; i < MG_NREG; ++i) {
         F0[i] = 0; F1[i] = 0; F2[i] = 0; F3[i] = 0;
         F4[i] = 0; F5[i] = 0; F6[i] = 0; F7[i] = 0;
     }
@@ -364,10 +375,10 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
 
     // software-pipelined fetch: the next instruction's scalar loads are in
     // flight while the current one executes (the host pads code with a NOP)
-    // The next instruction is fetched with an explicit s_load issued BEFORE
-    // the current one executes and waited for only at the end of the
-    // iteration (left to itself the compiler sinks the load to the back-edge
-    // and exposes the scalar-cache latency on every instruction).
+    // Instruction fetch: the next instruction's s_load is issued before the
+    // current one executes and waited for only at the end of the iteration
+    // (left to itself the compiler sinks the load to the back-edge and
+    // exposes the scalar-cache latency on every instruction).
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t* ip = (const uint32_t*)code;
     u32x4 cur;
@@ -376,11 +387,11 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
     for (uint32_t pc = 0; pc < n_ins; ++pc) {
         u32x4 nxt;
         asm volatile("s_load_dwordx4 %0, %1, 0x10" : "=s"(nxt) : "s"(ip) : "memory");
-        const uint32_t c_w0 = cur.x, c_w1 = cur.y, c_imm = cur.z;
-        const uint32_t w0 = c_w0, w1 = c_w1, imm0 = c_imm;
+        const uint32_t w0 = cur.x, w1 = cur.y, imm0 = cur.z;
         const uint32_t op = w0 & 0xFF;
         const uint32_t w = (w0 >> 8) & 0x3FF;
-        const uint32_t sd = w1 & 15, sa = (w1 >> 8) & 15, sb = (w1 >> 16) & 15, sc = (w1 >> 24) & 15;
+        // slot fields are < MG_NREG (validated on upload)
+        const uint32_t sd = w1 & 31, sa = (w1 >> 8) & 31, sb = (w1 >> 16) & 31, sc = (w1 >> 24) & 31;
 
         // operands are read inside the cases that need them (GPR-index moves)
         uint32_t x[8], y[8], r[8];
@@ -394,6 +405,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             cu32* p = consts + (size_t)imm0 * 8;
 #pragma unroll
             for (int j = 0; j < 8; ++j) r[j] = p[j];
+            __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0)
             break;
         }
         case MG_LEAF: {
@@ -409,6 +421,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
                 const uint32_t* p = run.leaves + (size_t)imm0 * 8 * run.stride + lane_idx;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) r[j] = p[(size_t)j * run.stride];
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
                 mask_to(r, w);
             }
             break;
@@ -441,6 +454,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             }
             r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
             r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+            __builtin_amdgcn_s_waitcnt(0);            // LDS / scratch results in
             break;
         }
         case MG_ADD: RX; RY; add256(x, y, r); mask_to(r, w); break;
@@ -475,13 +489,14 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             y[0] |= z;                               // divisor 0 -> 1 (fixed below)
             uint32_t q[8], m[8];
             udivrem256(x, y, q, m);
+            // with the divisor forced to 1, q == x: x need not stay live
             if (op == MG_UDIV) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) r[j] = z ? 0xFFFFFFFFu : q[j];
                 mask_to(r, w);
             } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) r[j] = z ? x[j] : m[j];
+                for (int j = 0; j < 8; ++j) r[j] = z ? q[j] : m[j];
             }
             break;
         }
@@ -505,8 +520,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
             udivrem256(as, at, q, m);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
+                m[j] = z ? q[j] : m[j];         // |t| forced to 1: q == |s|
                 q[j] = z ? 0xFFFFFFFFu : q[j];
-                m[j] = z ? as[j] : m[j];
             }
             if (op == MG_SDIV) {
                 neg256(q, tmp);
@@ -519,6 +534,8 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
                 for (int j = 0; j < 8; ++j) r[j] = ns ? tmp[j] : m[j];
             } else {
                 // bvsmod: u == 0 -> 0; (+,+) u; (-,+) t-u; (+,-) u+t; (-,-) -u
+                RY;                     // t again (not kept live across the division)
+                sext_from(y, w);
                 const uint32_t uz = is_zero256(m);
                 uint32_t nu[8], s1[8], s2[8];
                 neg256(m, nu);
@@ -638,7 +655,7 @@ __global__ __launch_bounds__(BLOCK, 2) void mg_interp(const mg_pdesc* __restrict
 #undef RX
 #undef RY
         // fused ROOT: the result of this instruction is a conjunct of the root
-        if (w0 & MG_ROOT_FLAG) root &= r[0] & 1u;
+        root &= r[0] | ((w0 & MG_ROOT_FLAG) ? 0u : 1u);   // Bool results are 0/1
 
         // single write point: F[sd] = r  (gpr_idx(DST) moves, no file copies)
         F0[sd] = r[0]; F1[sd] = r[1]; F2[sd] = r[2]; F3[sd] = r[3];

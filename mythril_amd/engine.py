@@ -21,7 +21,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
-           "mg_batch_free", "mg_batch_eval_gen", "mg_keccak256", "mg_version")
+           "mg_batch_free", "mg_batch_eval_gen", "mg_keccak256", "mg_version", "mg_config")
 
 
 class EngineUnavailable(RuntimeError):
@@ -75,6 +75,7 @@ def load_library(path: str = _LIB_PATH):
         lib.mg_batch_free.restype = None
         lib.mg_batch_eval_gen.argtypes = [p, p, u64, u64, u64, p, p, p]
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
+        lib.mg_config.argtypes = [p, u32]
         for name in EXPORTS:
             getattr(lib, name)
         _libs[path] = lib
@@ -117,6 +118,9 @@ class Engine:
         if rc != 0:
             raise EngineUnavailable("mg_init(%d) failed with %d (no usable GPU?)" % (device, rc))
         self._ctx = ctx
+        cfg = (C.c_uint32 * 4)()
+        self.lib.mg_config(cfg, 4)
+        self.nreg = int(cfg[1])
         name = C.create_string_buffer(256)
         cus = C.c_int()
         self.lib.mg_device_info(ctx, name, 256, C.byref(cus))

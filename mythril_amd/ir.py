@@ -480,7 +480,9 @@ def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
     return out, fused
 
 
-def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = frozenset()):
+def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = frozenset(),
+              nreg: int = I.NREG):
+    trash = nreg - 1
     uses: Dict[int, List[int]] = {}
     for i, n in enumerate(order):
         for a in n.args:
@@ -489,7 +491,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
     reg_of: Dict[int, int] = {}
     lds_of: Dict[int, int] = {}
     holder: Dict[int, LNode] = {}          # reg -> value
-    free_regs = list(range(I.NREG - 1))[::-1]
+    free_regs = list(range(nreg - 1))[::-1]
     free_lds: List[int] = []
     n_lds = 0
     ins: List[Tuple[int, int, int, int, int, int, int]] = []
@@ -527,7 +529,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
                 if n_lds > MAX_SPILL:
                     raise Unsupported("spill budget exceeded")
             lds_of[victim.id] = s
-            ins.append((I.SPILL, 1, I.TRASH, r, 0, 0, s))
+            ins.append((I.SPILL, 1, trash, r, 0, 0, s))
             n_spill += 1
         return r
 
@@ -561,11 +563,11 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         for a in set(n.args):
             release(a, i)
         if n.op in (I.ROOT, I.OUT):
-            ins.append((n.op, 1, I.TRASH, slots[0], 0, 0, n.imm or 0))
+            ins.append((n.op, 1, trash, slots[0], 0, 0, n.imm or 0))
             continue
         flags = I.ROOT_FLAG if n.id in fused else 0
         if not uses.get(n.id):
-            d = I.TRASH
+            d = trash
         else:
             d = alloc_reg(i, set())
             reg_of[n.id] = d
@@ -592,9 +594,10 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
 
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
-                        default_entries: int = 2) -> Program:
+                        default_entries: int = 2, nreg: int = I.NREG) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
-    optional probe nodes (256-bit values written per assignment)."""
+    optional probe nodes (256-bit values written per assignment).  ``nreg``
+    is the library's register-file size (``Engine.nreg``)."""
     lw = _Lowerer(table_sizes or {}, default_entries)
     sinks: List[LNode] = []
     for c in constraints:
@@ -621,7 +624,7 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
     order, fused = _fuse_roots(_schedule(sinks))
     const_values = sorted({n.imm & ((1 << 256) - 1) for n in order if n.op == I.CONST})
     const_index = {v: i for i, v in enumerate(const_values)}
-    ins, n_lds, n_spill, n_reload = _allocate(order, const_index, fused)
+    ins, n_lds, n_spill, n_reload = _allocate(order, const_index, fused, nreg)
     code = np.zeros((len(ins), 4), dtype=np.uint32)
     for k, (op, width, d, a, b, c, imm, *fl) in enumerate(ins):
         code[k, 0] = op | (width << 8) | (fl[0] if fl else 0)

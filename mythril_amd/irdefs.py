@@ -21,7 +21,7 @@ def _parse():
 
 OPS, DEFINES = _parse()
 NREG = DEFINES["NREG"]
-TRASH = DEFINES["TRASH"]
+TRASH = NREG - 1
 MAX_WIDTH = DEFINES["MAX_WIDTH"]
 MAX_LDS = DEFINES["MAX_LDS"]
 ROOT_FLAG = 1 << 18          # MG_ROOT_FLAG: w0 bit 18, ROOT fused into the producer

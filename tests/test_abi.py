@@ -23,6 +23,8 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(EXPORTS)
+    cfg = (ctypes.c_uint32 * 4)()
+    assert lib.mg_config(cfg, 4) == 0 and cfg[1] >= 8
 
 
 def test_version_without_gpu():

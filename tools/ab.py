@@ -38,22 +38,22 @@ def main():
     args = ap.parse_args()
     engines = [Engine(0, lib_path=os.path.abspath(l)) for l in args.libs]
     lanes = 1 << args.lanes_log2
-    progs = {op: compile_constraints(chain(op)) for op in args.ops.split(",") if op}
-    corpus = []
-    nodes = 0
-    for d in range(args.dags):
-        r, _ = make_dag(d)
-        p = compile_constraints(r)
-        corpus.append((d, p))
-        nodes += dag_work(r)[0]
+    dags = [make_dag(d)[0] for d in range(args.dags)]
+    nodes = sum(dag_work(r)[0] for r in dags)
     loaded = []
+    progs_by_nreg = {}
     for e in engines:
+        if e.nreg not in progs_by_nreg:
+            progs_by_nreg[e.nreg] = (
+                {op: compile_constraints(chain(op), nreg=e.nreg) for op in args.ops.split(",") if op},
+                [compile_constraints(r, nreg=e.nreg) for r in dags])
+        progs, corpus = progs_by_nreg[e.nreg]
         lp = {op: e.load(p) for op, p in progs.items()}
-        lc = [e.load(p, prog_seed=d) for d, p in corpus]
-        loaded.append((e, lp, e.batch_create(lc), lc))
+        lc = [e.load(p, prog_seed=d) for d, p in enumerate(corpus)]
+        loaded.append((e, lp, e.batch_create(lc), lc, progs))
     res = {}
     for rnd in range(args.rounds):
-        for li, (e, lp, batch, _) in enumerate(loaded):
+        for li, (e, lp, batch, _, progs) in enumerate(loaded):
             for op, h in lp.items():
                 t = timeit(lambda: e.eval_gen(h, 1, 0, lanes), 3)
                 res.setdefault((li, op), []).append(t * 1e9 / (progs[op].n_ins * lanes) * 1e3)

@@ -39,11 +39,16 @@ def chain(op):
 
 
 def main():
-    eng = get_engine(0)
+    args = sys.argv[1:]
+    lib = None
+    if args and args[0].startswith("--lib="):
+        lib = args.pop(0).split("=", 1)[1]
+    from mythril_amd.engine import Engine
+    eng = Engine(0, lib_path=__import__("os").path.abspath(lib)) if lib else get_engine(0)
     res = {}
-    ops = sys.argv[1:] or BIN + ["eq", "ult", "extract", "concat", "umulno"]
+    ops = args or BIN + ["eq", "ult", "extract", "concat", "umulno"]
     for op in ops:
-        prog = compile_constraints(chain(op))
+        prog = compile_constraints(chain(op), nreg=eng.nreg)
         lp = eng.load(prog)
         eng.eval_gen(lp, 1, 0, LANES)
         t0 = time.perf_counter()
