@@ -594,10 +594,12 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
 
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
-                        default_entries: int = 2, nreg: int = I.NREG) -> Program:
+                        default_entries: int = 2, nreg: int = I.NREG,
+                        extra_consts: Sequence[int] = ()) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
     optional probe nodes (256-bit values written per assignment).  ``nreg``
-    is the library's register-file size (``Engine.nreg``)."""
+    is the library's register-file size (``Engine.nreg``); ``extra_consts``
+    are added to the constant pool (candidate-generator hints)."""
     lw = _Lowerer(table_sizes or {}, default_entries)
     sinks: List[LNode] = []
     for c in constraints:
@@ -622,7 +624,8 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
             n.imm = n.width
             n.width = 1
     order, fused = _fuse_roots(_schedule(sinks))
-    const_values = sorted({n.imm & ((1 << 256) - 1) for n in order if n.op == I.CONST})
+    const_values = sorted({n.imm & ((1 << 256) - 1) for n in order if n.op == I.CONST} |
+                          {v & ((1 << 256) - 1) for v in extra_consts})
     const_index = {v: i for i, v in enumerate(const_values)}
     ins, n_lds, n_spill, n_reload = _allocate(order, const_index, fused, nreg)
     code = np.zeros((len(ins), 4), dtype=np.uint32)

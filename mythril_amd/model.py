@@ -1,0 +1,326 @@
+"""Drop-in replacement of ``mythril.support.model.get_model``
+(reference ``mythril/support/model.py:15-49``).
+
+Contract kept from the reference, in the same order:
+
+1. ``@lru_cache(maxsize=2**23)`` keyed on (constraints, minimize, maximize,
+   enforce_execution_time);
+2. timeout = ``args.solver_timeout`` (ms), clipped to the execution time left
+   minus 500 ms when ``enforce_execution_time``; ``<= 0`` → ``UnsatError``
+   before any work (``model.py:26-31``);
+3. a Python ``False`` constraint → ``UnsatError``; Python bools are dropped
+   (``model.py:32-36``);
+4. z3 ``unknown`` is treated as UNSAT (``model.py:47-49``).
+
+Routing:
+
+* ``minimize``/``maximize`` non-empty (only ``analysis/solver.py:65``) →
+  stock z3 ``Optimize``: the reported transaction sequence depends on the
+  optimum, so the GPU never answers these.
+* otherwise → compile the DAG (``mythril_amd.ir``), GPU witness search
+  (``mg_search``); a witness is re-verified by z3 when z3 is present and a
+  genuine z3 model is returned; on a miss, an unsupported operator or any
+  engine error → stock z3.  **UNSAT is only ever concluded by z3**: without
+  z3 a miss raises :class:`SolverUnavailable`, never ``UnsatError``.
+"""
+
+from __future__ import annotations
+
+import logging
+import time
+from functools import lru_cache
+from typing import Dict, List, Optional, Sequence
+
+from . import z3bridge
+from .assign import Assignment, unpack
+from .engine import EngineError, EngineUnavailable, LeafGen, get_engine
+from .ir import Program, Unsupported, compile_constraints
+from .smt import node as N
+
+log = logging.getLogger(__name__)
+
+try:  # inside a Mythril installation use its exception and singletons
+    from mythril.exceptions import UnsatError  # type: ignore
+except Exception:  # noqa: BLE001 - z3/mythril absent here
+    class UnsatError(Exception):
+        """Mirror of ``mythril.exceptions.UnsatError`` (``exceptions.py:16-20``)."""
+
+
+class SolverUnavailable(RuntimeError):
+    """No witness found on the GPU and no z3 to conclude UNSAT."""
+
+
+class Args:
+    """Mirror of ``mythril.support.support_args.Args`` (``support_args.py:1-16``)."""
+
+    def __init__(self):
+        self.solver_timeout = 10000
+        self.sparse_pruning = True
+        self.unconstrained_storage = False
+        self.parallel_solving = False
+        self.call_depth_limit = 3
+        self.iprof = True
+
+
+class TimeHandler:
+    """Mirror of ``laser/ethereum/time_handler.py:5-18``."""
+
+    def __init__(self):
+        self._start_time = int(time.time() * 1000)
+        self._execution_time = 86400 * 1000
+
+    def start_execution(self, execution_time):
+        self._start_time = int(time.time() * 1000)
+        self._execution_time = execution_time * 1000
+
+    def time_remaining(self):
+        return self._execution_time - (int(time.time() * 1000) - self._start_time)
+
+
+args = Args()
+time_handler = TimeHandler()
+
+
+class SolverStatistics:
+    """``SolverStatistics`` (``solver_statistics.py:29-43``) plus the
+    pre-filter's own counters."""
+
+    def __init__(self):
+        self.enabled = False
+        self.query_count = 0
+        self.solver_time = 0.0
+        self.gpu_queries = 0
+        self.gpu_hits = 0
+        self.gpu_candidates = 0
+        self.gpu_time = 0.0
+        self.fallbacks = 0
+        self.unsupported = 0
+
+    def __repr__(self):
+        return ("Query count: {} \nSolver time: {}\nGPU queries: {} hits: {} candidates: {} "
+                "time: {:.3f}s fallbacks: {} unsupported: {}").format(
+            self.query_count, self.solver_time, self.gpu_queries, self.gpu_hits,
+            self.gpu_candidates, self.gpu_time, self.fallbacks, self.unsupported)
+
+
+stats = SolverStatistics()
+
+# candidate budget per query (device-generated, counter-based streams)
+SEARCH_CANDIDATES = 1 << 22
+SEARCH_SEED = 0x6D797468
+
+
+class Model:
+    """Result of :func:`get_model`.  Wraps z3 models when z3 verified the
+    witness (same interface as ``laser/smt/model.py``), otherwise the GPU
+    witness itself (``assignment``)."""
+
+    def __init__(self, models: Optional[List[object]] = None,
+                 assignment: Optional[Assignment] = None, program: Optional[Program] = None):
+        self.raw = models or []
+        self.assignment = assignment
+        self.program = program
+
+    def decls(self):
+        out = []
+        for m in self.raw:
+            out.extend(m.decls())
+        return out
+
+    def __getitem__(self, item):
+        for m in self.raw:
+            r = m[item]
+            if r is not None:
+                return r
+        if self.assignment is not None and isinstance(item, str):
+            return self.assignment.vars.get(item)
+        return None
+
+    def eval(self, expression, model_completion: bool = False):
+        if self.raw:
+            for i, m in enumerate(self.raw):
+                if expression.decl() in list(m.decls()) or i == len(self.raw) - 1:
+                    return m.eval(expression, model_completion)
+            return None
+        return self.eval_node(expression if isinstance(expression, N.Node) else expression.raw)
+
+    def eval_node(self, node: N.Node) -> int:
+        """Evaluate a DAG under the witness — on the GPU (one lane)."""
+        if self.assignment is None:
+            raise ValueError("no witness")
+        from .assign import pack
+        prog = compile_constraints([], [node], table_sizes=dict(self.program.table_sizes)
+                                   if self.program else None)
+        eng = get_engine()
+        lp = eng.load(prog)
+        _, probes = eng.eval(lp, pack(prog, [self.assignment]), want_probes=True)
+        v = 0
+        for k in reversed(range(prog.n_probes)):
+            for j in reversed(range(8)):
+                v = (v << 32) | int(probes[k, j, 0])
+        return v
+
+
+def _raw_nodes(constraints) -> List[N.Node]:
+    """laser.smt Bool objects → DAG nodes (z3 ASTs are flattened)."""
+    out = []
+    memo: Dict[int, N.Node] = {}
+    for c in constraints:
+        raw = getattr(c, "raw", c)
+        if isinstance(raw, N.Node):
+            out.append(raw)
+        else:
+            out.append(z3bridge.to_node(raw, memo))
+    return out
+
+
+def search_leafgen(prog: Program) -> List[LeafGen]:
+    """Candidate generator for witness search: 20 % uniform, 20 % small,
+    20 % boundary values, 40 % constants harvested from the query (+-1)."""
+    n_c = len(prog.const_values)
+    return [LeafGen(l.width, 0, n_c, 20, 40, 60) for l in prog.leaves]
+
+
+def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
+    """Extra candidate values: every numeral of the query rounded up to a
+    multiple of 64 (the keccak UF outputs are constrained to 64-aligned
+    intervals, keccak_function_manager.py:136-140) and byte-shifted selector
+    constants (calldata words are Concats of bytes)."""
+    out = set()
+    for n in N.topo_order(list(nodes)):
+        if n.op == "bvnum" and n.width >= 8:
+            v = n.params[0]
+            out.add((v + 63) & ~63)
+            if 0 < v < (1 << 32):
+                out.add(v << 224)       # 4-byte selector in the top of a word
+    return sorted(out)
+
+
+def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
+    """(assignment, program) of the first satisfying candidate, or None."""
+    prog = compile_constraints(nodes, extra_consts=harvest_hints(nodes))
+    eng = get_engine()
+    lp = eng.load(prog, search_leafgen(prog), prog_seed=0)
+    t0 = time.perf_counter()
+    chunk = 1 << 20
+    first = 0
+    while first < SEARCH_CANDIDATES:
+        idx, wit = eng.search(lp, SEARCH_SEED, chunk, first_index=first)
+        stats.gpu_candidates += chunk if idx < 0 else idx - first + 1
+        if idx >= 0:
+            return unpack(prog, wit), prog
+        first += chunk
+        if (time.perf_counter() - t0) * 1000.0 > budget_ms:
+            break
+    return None
+
+
+# Set by install(): the reference's own Optimize wrapper
+# (mythril/laser/smt/solver/solver.py:86-105, timed by @stat_smt_query), so
+# inside Mythril the fallback is literally the stock code path.
+_stock_optimize = None
+
+
+def _z3_check(constraints, minimize, maximize, timeout):
+    """Stock path: z3 Optimize, exactly as the reference."""
+    if _stock_optimize is not None:
+        s = _stock_optimize()
+        s.set_timeout(timeout)
+        for c in constraints:
+            s.add(c)
+        for e in minimize:
+            s.minimize(e)
+        for e in maximize:
+            s.maximize(e)
+        result = s.check()
+        import z3
+        if result == z3.sat:
+            return s.model()
+        if result == z3.unknown:
+            log.debug("Timeout encountered while solving expression using z3")
+        raise UnsatError
+    if not z3bridge.available():
+        raise SolverUnavailable("z3 is not installed; cannot decide this query")
+    z3 = z3bridge._z3()
+    s = z3.Optimize()
+    s.set(timeout=timeout)
+    memo: Dict[int, object] = {}
+    for c in constraints:
+        raw = getattr(c, "raw", c)
+        s.add(z3bridge.to_z3(raw, memo) if isinstance(raw, N.Node) else raw)
+    for e in minimize:
+        raw = getattr(e, "raw", e)
+        s.minimize(z3bridge.to_z3(raw, memo) if isinstance(raw, N.Node) else raw)
+    for e in maximize:
+        raw = getattr(e, "raw", e)
+        s.maximize(z3bridge.to_z3(raw, memo) if isinstance(raw, N.Node) else raw)
+    t0 = time.time()
+    result = s.check()
+    if stats.enabled:
+        stats.query_count += 1
+        stats.solver_time += time.time() - t0
+    if result == z3.sat:
+        return Model([s.model()])
+    if result == z3.unknown:
+        log.debug("Timeout encountered while solving expression using z3")
+    raise UnsatError
+
+
+@lru_cache(maxsize=2 ** 23)
+def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
+    timeout = args.solver_timeout
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:
+            raise UnsatError
+    for constraint in constraints:
+        if type(constraint) == bool and not constraint:
+            raise UnsatError
+    constraints = [c for c in constraints if type(c) != bool]
+
+    if not minimize and not maximize:
+        try:
+            nodes = _raw_nodes(constraints)
+            stats.gpu_queries += 1
+            t0 = time.perf_counter()
+            hit = gpu_search(nodes, budget_ms=min(timeout, 200))
+            stats.gpu_time += time.perf_counter() - t0
+            if hit is not None:
+                assignment, prog = hit
+                if z3bridge.available():
+                    raws = [getattr(c, "raw", c) for c in constraints]
+                    if all(not isinstance(r, N.Node) for r in raws):
+                        m = z3bridge.verify(raws, assignment, timeout)
+                        if m is not None:
+                            stats.gpu_hits += 1
+                            return Model([m], assignment, prog)
+                        log.warning("GPU witness rejected by z3; falling back")
+                    else:
+                        stats.gpu_hits += 1
+                        return Model(None, assignment, prog)
+                else:
+                    stats.gpu_hits += 1
+                    return Model(None, assignment, prog)
+        except Unsupported as e:
+            stats.unsupported += 1
+            log.debug("GPU pre-filter: unsupported (%s)", e)
+        except (EngineUnavailable, EngineError, z3bridge.Z3Unavailable) as e:
+            log.debug("GPU pre-filter unavailable: %s", e)
+        stats.fallbacks += 1
+    return _z3_check(constraints, minimize, maximize, timeout)
+
+
+def install() -> None:
+    """Rebind ``get_model`` in a Mythril installation: the three names bound
+    by ``from ... import get_model``, and share Mythril's
+    ``args`` / ``time_handler`` singletons and its ``Optimize`` wrapper."""
+    import importlib
+    global args, time_handler, _stock_optimize
+    args = importlib.import_module("mythril.support.support_args").args
+    time_handler = importlib.import_module("mythril.laser.ethereum.time_handler").time_handler
+    _stock_optimize = importlib.import_module("mythril.laser.smt").Optimize
+    get_model.cache_clear()
+    for mod in ("mythril.support.model", "mythril.analysis.solver",
+                "mythril.laser.ethereum.state.constraints"):
+        m = importlib.import_module(mod)
+        m.get_model = get_model

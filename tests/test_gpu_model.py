@@ -1,0 +1,93 @@
+"""The drop-in get_model on the GPU, on the reference's own sat/unsat
+expectations: tests/laser/keccak_tests.py (symbolic-hash UF encoding),
+tests/laser/smt/model_test.py (x == 2) and tests/laser/state/calldata_test.py
+(symbolic calldata).  z3 is absent here, so UNSAT can never be concluded:
+an expected-unsat query must raise SolverUnavailable (never return a model),
+and every returned witness is checked by the oracle."""
+
+import pytest
+
+import mythril_amd.model as M
+from keccak_mirror import KeccakManager
+from mythril_amd.smt import And, Array, If, symbol_factory
+from oracle import smtlib_ref as R
+
+pytestmark = pytest.mark.gpu
+BVV = symbol_factory.BitVecVal
+BVS = symbol_factory.BitVecSym
+
+
+@pytest.fixture(autouse=True)
+def fresh():
+    M.get_model.cache_clear()
+    M.time_handler.start_execution(3600)
+    yield
+
+
+def check(constraints):
+    """get_model → oracle-verified witness (True), or a miss (False)."""
+    try:
+        m = M.get_model(tuple(constraints), enforce_execution_time=False)
+    except M.SolverUnavailable:
+        return False
+    a = m.assignment
+    asg = R.Assignment(a.vars, a.arrays, a.funcs)
+    assert R.eval_constraints([c.raw for c in constraints], asg) == 1, "false SAT"
+    return True
+
+
+def keccak_pair(engine, i1, i2):
+    km = KeccakManager(lambda b: engine.keccak256([b])[0])
+    o1, c1 = km.create_keccak(i1)
+    o2, c2 = km.create_keccak(i2)
+    return [And(c1, c2), o1 == o2]
+
+
+@pytest.mark.parametrize("i1,i2,expected", [
+    (BVV(100, 8), BVV(101, 8), False),
+    (BVV(100, 8), BVV(100, 16), False),
+    (BVV(100, 8), BVV(100, 8), True),
+    (BVS("N1", 256), BVS("N2", 256), True),
+    (BVV(100, 256), BVS("N1", 256), True),
+    (BVV(100, 8), BVS("N1", 256), False),
+], ids=["diff8", "width", "same8", "sym", "val-sym", "val8-sym256"])
+def test_keccak_basic(engine, i1, i2, expected):
+    found = check(keccak_pair(engine, i1, i2))
+    if not expected:
+        assert not found
+    else:
+        assert found, "GPU search missed a satisfiable keccak query"
+
+
+def test_keccak_symbol_and_val_unsat(engine):
+    km = KeccakManager(lambda b: engine.keccak256([b])[0])
+    n = BVS("n", 256)
+    o1, c1 = km.create_keccak(BVV(100, 256))
+    o2, c2 = km.create_keccak(n)
+    assert not check([And(c1, c2), o1 == o2, n == BVV(10, 256)])
+
+
+def test_keccak_simple_number_unsat(engine):
+    km = KeccakManager(lambda b: engine.keccak256([b])[0])
+    o, c = km.create_keccak(BVS("a", 160))
+    assert not check([c, BVV(10, 256) == o])
+
+
+def test_model_x_equals_2(engine):
+    x = BVS("x", 256)
+    m = M.get_model((x == BVV(2, 256),), enforce_execution_time=False)
+    assert m["x"] == 2
+    assert m.eval(x + BVV(5, 256)) == 7          # Model.eval runs on the GPU
+
+
+def test_symbolic_calldata(engine):
+    # SymbolicCalldata._load (calldata.py:219-232): If(i < size, cd[i], 0)
+    cd = Array("1_calldata", 256, 8)
+    size = BVS("1_calldatasize", 256)
+
+    def load(i):
+        return If(i < size, cd[i], BVV(0, 8))
+    # index >= size reads 0: unsat with == 1
+    assert not check([load(BVV(51, 256)) == BVV(1, 8), size == BVV(50, 256)])
+    # a byte inside the calldata can take a value
+    assert check([load(BVV(3, 256)) == BVV(0xA9, 8), size == BVV(4, 256)])
