@@ -107,6 +107,7 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world,
                                 device_id=torch.device("cuda", local))
 
+    from mythril_amd import shard
     from mythril_amd.engine import Engine, default_leafgen
     eng = Engine(local)
     loaded = [eng.load(p, default_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
@@ -115,21 +116,24 @@ def main():
     words = (n_assign + 63) // 64
     d_bits = torch.empty((args.dags, words), dtype=torch.int64, device="cuda")
     d_first = torch.empty(args.dags, dtype=torch.int64, device="cuda")
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-default) stream: the library launches on exactly this
+    # stream, so the HIP events below bracket the kernel itself (a null
+    # handle would make the library fall back to its own internal stream)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     nodes_per_lane = sum(n for _, _, n, _ in corpus)
     weight_per_lane = sum(w for _, _, _, w in corpus)
 
     def step(i, ev=None):
-        d_first.fill_(0x7FFFFFFFFFFFFFFF)
-        first = (i * world + rank) * n_assign
+        d_first.fill_(shard.NONE)
+        first = shard.shard_first(i, rank, world, n_assign)
         if ev:
             ev[0].record(stream)
         eng.batch_eval_gen(batch, SEED, first, n_assign, d_bits.data_ptr(), d_first.data_ptr(),
                            stream.cuda_stream)
         if ev:
             ev[1].record(stream)
-        if world > 1:
-            dist.all_reduce(d_first, op=dist.ReduceOp.MIN)
+        shard.reduce_first_sat(d_first)      # the one exchange step (RCCL MIN)
 
     for i in range(args.warmup):
         step(i)
@@ -152,7 +156,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    sat_dags = int((d_first != 0x7FFFFFFFFFFFFFFF).sum().item())
+    sat_dags = int((d_first != shard.NONE).sum().item())
 
     if rank == 0:
         from mythril_amd.roofline import VALU_PEAK_OPS

@@ -19,9 +19,13 @@ A w-bit op scales by ceil(w/32)/8 (a 256-bit op is the unit).  Leaves
 (variables, numerals, free and constant arrays) are not nodes; store nodes
 are nodes of weight 0 (they are priced inside the selects that read them).
 
-Peak: MI355X vector ALU, 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz =
-78.6 T int32 lane-ops/s (MI355X_MICROARCH.md: a wave64 VALU op issues in 2
-cycles on a SIMD-32, FP32 vector peak 157.3 TFLOPS = 78.6 T FMA/s).
+Peak: MEASURED int32 VALU issue rate on MI355X (``tools/ubench.hip``,
+``profiles/r01/ubench.log``): independent ``v_add_u32`` (and equally
+``v_addc_co_u32`` / ``v_mad_u64_u32``) issue at 4.10 cycles per wave64
+instruction per SIMD at 8 waves/SIMD -> 256 CU x 4 SIMD x 64 lanes / 4.10 cyc
+x 2.4 GHz = 38.4 T int32 lane-ops/s.  (The 157.3 TFLOPS FP32 vector spec
+counts 2-cycle packed FP32 issue; plain int32 VALU does not reach it: the
+nominal int32 rate is 39.3 T at 4 cycles)
 """
 
 from __future__ import annotations
@@ -30,7 +34,7 @@ from typing import Dict, Iterable, Tuple
 
 from .smt.node import Node, topo_order
 
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9          # int32 lane-ops/s
+VALU_PEAK_OPS = 256 * 4 * 64 / 4.098 * 2.4e9  # measured int32 lane-ops/s (38.4 T)
 HBM_PEAK_BPS = 8.0e12
 
 _W8 = {"bvadd", "bvsub", "bvneg", "bvand", "bvor", "bvxor", "bvnot", "=", "distinct",
