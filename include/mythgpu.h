@@ -113,6 +113,16 @@ int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
 
 /* Library/ABI version (no GPU needed). */
 int mg_version(void);
+/* Host-only (no GPU): translate a validated IR program into the 8-word
+ * records of the assembly interpreter, given its handler offset table
+ * (mg_load_program does this with the table queried from the device).
+ *   records: (n_ins + 2) x 8 words; masks: mask entries appended after the
+ *   program's n_consts constants (8 words each).  Sizes are returned in
+ *   *n_record_words / *n_mask_words; MG_E_ARG when a buffer is too small. */
+int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32_t n_lds,
+                 const uint32_t* handler_off, uint32_t n_handlers, uint32_t* records,
+                 uint32_t max_record_words, uint32_t* n_record_words, uint32_t* masks,
+                 uint32_t max_mask_words, uint32_t* n_mask_words);
 /* Build configuration (no GPU needed): out[0..3] = version, MG_NREG,
  * MG_MAX_LDS, MG_MAX_PSLOTS — programs must be compiled for these. */
 int mg_config(uint32_t* out, uint32_t n);

@@ -1,0 +1,1296 @@
+"""Generator of the hand-written gfx950 (CDNA4) assembly interpreter for the
+mythgpu IR — the engine's hot kernel.
+
+Why assembly: on MI355X every instruction a wave issues, scalar or vector,
+costs ~4 SIMD cycles (``profiles/r01/ubench.log``).  The compiled C++
+interpreter spent ~40 scalar instructions per IR op on decoding and a binary
+search dispatch plus ~30 vector moves on register-file copies.  This one is
+written instruction by instruction:
+
+* **direct-threaded dispatch**: the host translates each IR instruction into
+  an 8-word record whose first word is the byte offset of its handler; every
+  handler ends with ``s_add_u32 / s_addc_u32 / s_setpc_b64`` to the next.
+  The next record is prefetched (``s_load_dwordx8``) into the other of two
+  SGPR banks at handler entry, so each handler exists in a bank-A and a
+  bank-B variant (heavy ops copy their record and always prefetch into A);
+* **pre-decoded fields**: register slots arrive as GPR-index values
+  (8 x slot); uniform shifts, funnel indices and constant-pool offsets are
+  computed by the translator (``mg_api.cpp``);
+* **GPR-indexed ALU**: one operand is consumed straight from the register
+  file by the arithmetic (``s_set_gpr_idx_on ... gpr_idx(SRC0)``), only the
+  other is copied; EXTRACT/CONCAT are one ``v_alignbit_b32`` per limb with
+  both sources indexed;
+* **variants**: ROOT-fused and width-masked forms of every handler, chosen
+  by the translator, so the common 256-bit non-root case pays nothing.
+
+Register file: 16 slots x 8 limbs at v[8 + 8*slot + limb]; X (v0..v7) and
+Y (v136..v143) double as guards below/above it for the funnel reads.
+
+This module writes ``csrc/mg_interp_gfx950.inc`` (the assembly, as the body
+of the inline asm in ``mg_interp_asm.hip``) and ``csrc/mg_asm_handlers.h``
+(handler numbering shared with the translator).  It runs at build time only
+(``mythril_amd/build.py``).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+NREG = 16                  # register-file slots (MG_NREG)
+FB = 8                     # first VGPR of the file
+XB = 0                     # X temps v0..v7   (guard below the file)
+YB = FB + 8 * NREG         # Y temps v136..v143 (guard above the file)
+RB = YB + 8                # R temps v144..v151
+TB = RB + 8                # T temps v152..v163
+NT = 12
+NVGPR_FIXED = TB + NT      # v0..v163 named here; root/lane/lds are operands
+
+# ---- SGPR plan (inputs are inline-asm operands used in place) --------------
+BANK = (40, 48)            # s[40:47], s[48:55]: the two record banks
+S_BASE = 56                # s[56:57] handler base PC
+S_CODE = 58                # s[58:59] translated code
+S_IP = 60                  # byte offset of the next record to prefetch
+S_VAR = 61                 # heavy ops: variant bits | op << 4
+S_CONST = 62               # s[62:63] constant pool
+S_CUR = 64                 # s[64:71] current record of a heavy op / LEAF descriptor
+S_M = 72                   # s[72:79] width masks (8)
+S_T = 80                   # s[80:87] temps; s[86:87] is also the jump target
+S_X = 88                   # s[88:95] division lane masks (ns, nt, z) + op
+S_JMP = S_T + 6
+S_M0 = S_X + 7             # m0 (GPR-index register) saved across the asm
+S_LAST = S_X + 7
+
+F_OFF, F_D, F_A, F_B, F_C, F_IMM, F_W, F_MOFF = range(8)
+
+AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", "RELOAD_SCR",
+        "ADD", "SUB", "MUL", "UDIV", "UREM", "SDIV", "SREM", "SMOD", "AND", "OR", "XOR",
+        "NOT", "SHL", "LSHR", "ASHR", "EQ", "ULT", "ULE", "SLT", "SLE", "UMULNO", "ITE",
+        "CONCAT", "EXTRACT", "SEXT", "NEG", "OUT", "ROOT", "MOV"]
+AOP = {n: i for i, n in enumerate(AOPS)}
+V_ROOT, V_MASK = 1, 2
+NVAR = 4
+
+
+def hid(aop: int, variant: int, bank: int) -> int:
+    return (aop * NVAR + variant) * 2 + bank
+
+
+NUM_HANDLERS = len(AOPS) * NVAR * 2
+
+
+def v(n: int) -> str:
+    return "v%d" % n
+
+
+def s(n: int) -> str:
+    return "s%d" % n
+
+
+def sp(n: int) -> str:
+    return "s[%d:%d]" % (n, n + 1)
+
+
+def vp(n: int) -> str:
+    return "v[%d:%d]" % (n, n + 1)
+
+
+X = [XB + j for j in range(8)]
+Y = [YB + j for j in range(8)]
+R = [RB + j for j in range(8)]
+T = [TB + j for j in range(NT)]
+F = [FB + j for j in range(8)]          # limb j of the indexed slot (index = 8*slot)
+G = [FB - 8 + j for j in range(10)]     # funnel base (index = 8*slot + limb shift + 8)
+TMP = T[11]
+
+# inline-asm operand names
+OP_ROOT, OP_LANE_LO, OP_LANE_HI, OP_LDS = "%[root]", "%[lane_lo]", "%[lane_hi]", "%[lds]"
+IN = {k: "%%[%s]" % k for k in ("desc", "seed", "first", "leaves", "stride", "lout", "probes",
+                                "mode", "scr", "active", "table")}
+
+
+class Asm:
+    def __init__(self):
+        self.lines: List[str] = []
+        self._n = 0
+
+    def __call__(self, text: str):
+        self.lines.append("    " + text)
+
+    def label(self, name: str):
+        self.lines.append(name + ":")
+
+    def uniq(self, stem: str) -> str:
+        self._n += 1
+        return ".L%s%d_%%=" % (stem, self._n)
+
+    def idx_on(self, sreg: int, mode: str):
+        self("s_set_gpr_idx_on %s, gpr_idx(%s)" % (s(sreg), mode))
+
+    def idx_off(self):
+        self("s_set_gpr_idx_off")
+
+    def read_slot(self, dst: List[int], fld_sgpr: int):
+        self.idx_on(fld_sgpr, "SRC0")
+        for j in range(8):
+            self("v_mov_b32 %s, %s" % (v(dst[j]), v(F[j])))
+        self.idx_off()
+
+    def write_slot(self, src: List[int], fld_sgpr: int, masks: Optional[int] = None):
+        self.idx_on(fld_sgpr, "DST")
+        for j in range(8):
+            if masks is None:
+                self("v_mov_b32 %s, %s" % (v(F[j]), v(src[j])))
+            else:
+                self("v_and_b32 %s, %s, %s" % (v(F[j]), s(masks + j), v(src[j])))
+        self.idx_off()
+
+    def root_and(self, reg: str):
+        self("v_and_b32 %s, %s, %s" % (OP_ROOT, reg, OP_ROOT))
+
+
+def fld(bank: int, k: int) -> int:
+    return BANK[bank] + k
+
+
+def cur(k: int) -> int:
+    return S_CUR + k
+
+
+# ---------------------------------------------------------------------------
+# scaffolding
+# ---------------------------------------------------------------------------
+
+def prologue(a: Asm, bank: int):
+    ob = BANK[1 - bank]
+    a("s_load_dwordx8 s[%d:%d], %s, %s" % (ob, ob + 7, sp(S_CODE), s(S_IP)))
+    a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
+
+
+def dispatch(a: Asm, next_bank: int):
+    nb = BANK[next_bank]
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_add_u32 %s, %s, %s" % (s(S_JMP), s(S_BASE), s(nb + F_OFF)))
+    a("s_addc_u32 %s, %s, 0" % (s(S_JMP + 1), s(S_BASE + 1)))
+    a("s_setpc_b64 %s" % sp(S_JMP))
+
+
+def load_masks(a: Asm, moff_sgpr: int, dst: int = S_M):
+    a("s_load_dwordx8 s[%d:%d], %s, %s" % (dst, dst + 7, sp(S_CONST), s(moff_sgpr)))
+
+
+def finish(a: Asm, bank: int, res: List[int], root: bool, mask: bool):
+    if mask:
+        a("s_waitcnt lgkmcnt(0)")
+    a.write_slot(res, fld(bank, F_D), S_M if mask else None)
+    if root:
+        a.root_and(v(res[0]))
+    dispatch(a, 1 - bank)
+
+
+def sext(a: Asm, regs: List[int], wsgpr: int, masks: int, tmp: int, st: int):
+    """Sign-extend regs (canonical at the width in s[wsgpr]) to 256 bits in
+    place.  masks: 8 SGPRs with the bits < width; st: 2 scratch SGPRs.
+    Preserves vcc."""
+    a("s_sub_u32 %s, %s, 1" % (s(st), s(wsgpr)))
+    a("s_lshr_b32 %s, %s, 5" % (s(st + 1), s(st)))
+    a("s_and_b32 %s, %s, 31" % (s(st), s(st)))
+    a("s_set_gpr_idx_on %s, gpr_idx(SRC0)" % s(st + 1))
+    a("v_mov_b32 %s, %s" % (v(tmp), v(regs[0])))
+    a.idx_off()
+    a("v_bfe_u32 %s, %s, %s, 1" % (v(tmp), v(tmp), s(st)))
+    a("v_sub_u32 %s, 0, %s" % (v(tmp), v(tmp)))
+    for j in range(8):
+        a("v_bfi_b32 %s, %s, %s, %s" % (v(regs[j]), s(masks + j), v(regs[j]), v(tmp)))
+
+
+def or_reduce(a: Asm, regs: List[int], out: int):
+    a("v_or3_b32 %s, %s, %s, %s" % (v(out), v(regs[0]), v(regs[1]), v(regs[2])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(out), v(out), v(regs[3]), v(regs[4])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(out), v(out), v(regs[5]), v(regs[6])))
+    a("v_or_b32 %s, %s, %s" % (v(out), v(out), v(regs[7])))
+
+
+# ---------------------------------------------------------------------------
+# cheap handlers (a, bank, root, mask)
+# ---------------------------------------------------------------------------
+
+def h_nop(a, bank, root, mask):
+    prologue(a, bank)
+    dispatch(a, 1 - bank)
+
+
+def h_halt(a, bank, root, mask):
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_branch .Lexit_%=")
+
+
+def h_const(a, bank, root, mask):
+    prologue(a, bank)
+    load_masks(a, fld(bank, F_IMM))                # the constant itself
+    a("s_waitcnt lgkmcnt(0)")
+    a.idx_on(fld(bank, F_D), "DST")
+    for j in range(8):
+        a("v_mov_b32 %s, %s" % (v(F[j]), s(S_M + j)))
+    a.idx_off()
+    if root:
+        a.root_and(s(S_M))
+    dispatch(a, 1 - bank)
+
+
+def _binop(a, bank, root, mask, emit):
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), "SRC0")
+    emit()
+    a.idx_off()
+    finish(a, bank, R, root, mask)
+
+
+def h_add(a, bank, root, mask):
+    def emit():
+        a("v_add_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(F[0]), v(Y[0])))
+        for j in range(1, 8):
+            a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(R[j]), v(F[j]), v(Y[j])))
+    _binop(a, bank, root, mask, emit)
+
+
+def h_sub(a, bank, root, mask):
+    def emit():
+        a("v_sub_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(F[0]), v(Y[0])))
+        for j in range(1, 8):
+            a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(R[j]), v(F[j]), v(Y[j])))
+    _binop(a, bank, root, mask, emit)
+
+
+def _logic(opname):
+    def h(a, bank, root, mask):
+        def emit():
+            for j in range(8):
+                a("%s %s, %s, %s" % (opname, v(R[j]), v(F[j]), v(Y[j])))
+        _binop(a, bank, root, False, emit)       # canonical in -> canonical out
+    return h
+
+
+h_and = _logic("v_and_b32")
+h_or = _logic("v_or_b32")
+h_xor = _logic("v_xor_b32")
+
+
+def h_not(a, bank, root, mask):
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.idx_on(fld(bank, F_A), "SRC0")
+    for j in range(8):
+        a("v_not_b32 %s, %s" % (v(R[j]), v(F[j])))
+    a.idx_off()
+    finish(a, bank, R, root, mask)
+
+
+def h_neg(a, bank, root, mask):
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.idx_on(fld(bank, F_A), "SRC1")
+    a("v_sub_co_u32 %s, vcc, 0, %s" % (v(R[0]), v(F[0])))
+    for j in range(1, 8):
+        a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(R[j]), v(F[j])))
+    a.idx_off()
+    finish(a, bank, R, root, mask)
+
+
+def h_mov(a, bank, root, mask):
+    prologue(a, bank)
+    a.read_slot(R, fld(bank, F_A))
+    finish(a, bank, R, root, False)
+
+
+def h_root(a, bank, root, mask):
+    prologue(a, bank)
+    a.idx_on(fld(bank, F_A), "SRC0")
+    a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+    a.idx_off()
+    dispatch(a, 1 - bank)
+
+
+def _bool_result(a, bank, root, true_if_vcc=True):
+    a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[0]), "0" if true_if_vcc else "1",
+                                         "1" if true_if_vcc else "0"))
+    a.idx_on(fld(bank, F_D), "DST")
+    a("v_mov_b32 %s, %s" % (v(F[0]), v(R[0])))
+    for j in range(1, 8):
+        a("v_mov_b32 %s, 0" % v(F[j]))
+    a.idx_off()
+    if root:
+        a.root_and(v(R[0]))
+    dispatch(a, 1 - bank)
+
+
+def h_eq(a, bank, root, mask):
+    prologue(a, bank)
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), "SRC0")
+    for j in range(8):
+        a("v_xor_b32 %s, %s, %s" % (v(Y[j]), v(F[j]), v(Y[j])))
+    a.idx_off()
+    or_reduce(a, Y, T[0])
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(T[0]))
+    _bool_result(a, bank, root)
+
+
+def _borrow(a, bank, lhs_field, rhs_field):
+    """vcc = borrow of F[lhs] - F[rhs] (unsigned lhs < rhs)."""
+    a.read_slot(Y, fld(bank, rhs_field))
+    a.idx_on(fld(bank, lhs_field), "SRC0")
+    a("v_sub_co_u32 %s, vcc, %s, %s" % (v(Y[0]), v(F[0]), v(Y[0])))
+    for j in range(1, 8):
+        a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(Y[j]), v(F[j]), v(Y[j])))
+    a.idx_off()
+
+
+def h_ult(a, bank, root, mask):
+    prologue(a, bank)
+    _borrow(a, bank, F_A, F_B)
+    _bool_result(a, bank, root)
+
+
+def h_ule(a, bank, root, mask):
+    prologue(a, bank)
+    _borrow(a, bank, F_B, F_A)            # b < a  ->  not (a <= b)
+    _bool_result(a, bank, root, true_if_vcc=False)
+
+
+def _scmp(a, bank, root, mask, le: bool):
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.read_slot(X, fld(bank, F_A))
+    a.read_slot(Y, fld(bank, F_B))
+    if mask:
+        a("s_waitcnt lgkmcnt(0)")
+        sext(a, X, fld(bank, F_W), S_M, T[0], S_T)
+        sext(a, Y, fld(bank, F_W), S_M, T[0], S_T)
+    a("v_xor_b32 %s, 0x80000000, %s" % (v(X[7]), v(X[7])))
+    a("v_xor_b32 %s, 0x80000000, %s" % (v(Y[7]), v(Y[7])))
+    lhs, rhs = (Y, X) if le else (X, Y)
+    a("v_sub_co_u32 %s, vcc, %s, %s" % (v(T[0]), v(lhs[0]), v(rhs[0])))
+    for j in range(1, 8):
+        a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(T[0]), v(lhs[j]), v(rhs[j])))
+    _bool_result(a, bank, root, true_if_vcc=not le)
+
+
+def h_slt(a, bank, root, mask):
+    _scmp(a, bank, root, mask, False)
+
+
+def h_sle(a, bank, root, mask):
+    _scmp(a, bank, root, mask, True)
+
+
+def h_ite(a, bank, root, mask):
+    prologue(a, bank)
+    a.idx_on(fld(bank, F_C), "SRC0")
+    a("v_and_b32_e64 %s, %s, 1" % (v(T[0]), v(F[0])))
+    a.idx_off()
+    a("v_cmp_ne_u32 vcc, 0, %s" % v(T[0]))
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), "SRC1")
+    for j in range(8):
+        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[j]), v(Y[j]), v(F[j])))
+    a.idx_off()
+    finish(a, bank, R, root, False)
+
+
+def h_extract(a, bank, root, mask):
+    """R = (F[a] >> lo) & mask(W).  C = 8a + (lo >> 5) + 8, IMM = lo & 31."""
+    prologue(a, bank)
+    load_masks(a, fld(bank, F_MOFF))
+    a.idx_on(fld(bank, F_C), "SRC0,SRC1")
+    for j in range(8):
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(R[j]), v(G[j + 1]), v(G[j]), s(fld(bank, F_IMM))))
+    a.idx_off()
+    finish(a, bank, R, root, True)
+
+
+def h_concat(a, bank, root, mask):
+    """R = F[a] << sb | F[b] (sb = width of b).  C = funnel index, IMM =
+    funnel shift; MOFF -> 8 masks of the bits >= sb."""
+    prologue(a, bank)
+    load_masks(a, fld(bank, F_MOFF))
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_C), "SRC0,SRC1")
+    for j in range(8):
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(R[j]), v(G[j + 1]), v(G[j]), s(fld(bank, F_IMM))))
+    a.idx_off()
+    a("s_waitcnt lgkmcnt(0)")
+    for j in range(8):
+        a("v_bfi_b32 %s, %s, %s, %s" % (v(R[j]), s(S_M + j), v(R[j]), v(Y[j])))
+    finish(a, bank, R, root, False)
+
+
+def h_sext(a, bank, root, mask):
+    """sign_extend from IMM bits to W bits.  MOFF -> 16 masks: bits < IMM,
+    then bits < W."""
+    prologue(a, bank)
+    load_masks(a, fld(bank, F_MOFF))
+    a("s_add_u32 %s, %s, 32" % (s(S_T), s(fld(bank, F_MOFF))))
+    a("s_load_dwordx8 s[%d:%d], %s, %s" % (S_CUR, S_CUR + 7, sp(S_CONST), s(S_T)))
+    a.read_slot(R, fld(bank, F_A))
+    a("s_waitcnt lgkmcnt(0)")
+    sext(a, R, fld(bank, F_IMM), S_M, T[0], S_T)
+    a.write_slot(R, fld(bank, F_D), S_CUR)
+    if root:
+        a.root_and(v(R[0]))
+    dispatch(a, 1 - bank)
+
+
+def h_spill_lds(a, bank, root, mask):
+    prologue(a, bank)
+    a.read_slot(Y, fld(bank, F_A))
+    a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
+    a("ds_write_b128 %s, v[%d:%d]" % (v(T[0]), Y[0], Y[3]))
+    a("ds_write_b128 %s, v[%d:%d] offset:4096" % (v(T[0]), Y[4], Y[7]))
+    dispatch(a, 1 - bank)
+
+
+def h_reload_lds(a, bank, root, mask):
+    prologue(a, bank)
+    a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
+    a("ds_read_b128 v[%d:%d], %s" % (R[0], R[3], v(T[0])))
+    a("ds_read_b128 v[%d:%d], %s offset:4096" % (R[4], R[7], v(T[0])))
+    a("s_waitcnt lgkmcnt(0)")
+    finish(a, bank, R, root, False)
+
+
+def h_spill_scr(a, bank, root, mask):
+    prologue(a, bank)
+    a.read_slot(Y, fld(bank, F_A))
+    a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
+    a("scratch_store_dwordx4 off, v[%d:%d], %s" % (Y[0], Y[3], s(S_T)))
+    a("scratch_store_dwordx4 off, v[%d:%d], %s offset:16" % (Y[4], Y[7], s(S_T)))
+    dispatch(a, 1 - bank)
+
+
+def h_reload_scr(a, bank, root, mask):
+    prologue(a, bank)
+    a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
+    a("scratch_load_dwordx4 v[%d:%d], off, %s" % (R[0], R[3], s(S_T)))
+    a("scratch_load_dwordx4 v[%d:%d], off, %s offset:16" % (R[4], R[7], s(S_T)))
+    a("s_waitcnt vmcnt(0)")
+    finish(a, bank, R, root, False)
+
+
+def _soa_base(a: Asm, ptr_op: str, row_sgpr: int):
+    """s[S_T:S_T+1] = ptr + (8*index) * stride*4 ; s[S_T+4:S_T+5] = stride*4.
+    Clobbers S_T..S_T+5."""
+    a("s_lshl_b64 %s, %s, 2" % (sp(S_T + 4), IN["stride"]))
+    a("s_lshl_b32 %s, %s, 3" % (s(S_T + 1), s(row_sgpr)))
+    a("s_mul_i32 %s, %s, %s" % (s(S_T), s(S_T + 1), s(S_T + 4)))
+    a("s_mul_hi_u32 %s, %s, %s" % (s(S_T + 2), s(S_T + 1), s(S_T + 4)))
+    a("s_mul_i32 %s, %s, %s" % (s(S_T + 3), s(S_T + 1), s(S_T + 5)))
+    a("s_add_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 2), s(S_T + 3)))
+    a("s_mov_b64 %s, %s" % (sp(S_T + 2), ptr_op))
+    a("s_add_u32 %s, %s, %s" % (s(S_T), s(S_T), s(S_T + 2)))
+    a("s_addc_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 1), s(S_T + 3)))
+
+
+def _soa_step(a: Asm):
+    a("s_add_u32 %s, %s, %s" % (s(S_T), s(S_T), s(S_T + 4)))
+    a("s_addc_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 1), s(S_T + 5)))
+
+
+def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int):
+    """regs -> SoA buffer ptr[(8*row + j) * stride + lane], active lanes only,
+    when ptr != 0.  Clobbers S_T..S_T+7, T[0]."""
+    skip = a.uniq("nost")
+    a("s_cmp_lg_u64 %s, 0" % ptr_op)
+    a("s_cbranch_scc0 %s" % skip)
+    _soa_base(a, ptr_op, row_sgpr)
+    a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
+    a("s_mov_b64 %s, exec" % sp(S_T + 6))
+    a("s_mov_b64 exec, %s" % IN["active"])
+    for j in range(8):
+        a("global_store_dword %s, %s, %s" % (v(T[0]), v(regs[j]), sp(S_T)))
+        if j < 7:
+            _soa_step(a)
+    a("s_mov_b64 exec, %s" % sp(S_T + 6))
+    a.label(skip)
+
+
+def h_out(a, bank, root, mask):
+    """probe[C] = F[a] (active lanes, when a probe buffer is bound)."""
+    prologue(a, bank)
+    a.read_slot(Y, fld(bank, F_A))
+    _store_soa(a, Y, IN["probes"], fld(bank, F_C))
+    dispatch(a, 1 - bank)
+
+
+# ---------------------------------------------------------------------------
+# LEAF: eval mode (SoA load) or the device candidate generator
+# ---------------------------------------------------------------------------
+
+GOLD = 0x9E3779B97F4A7C15
+
+
+def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
+    """SplitMix64 step on the per-lane state st=(lo,hi): st += GOLD;
+    z = mix(st).  t: 4 temps.  Uses vcc and s[S_T+6:S_T+7]."""
+    a("v_mov_b32 %s, 0x%x" % (v(t[0]), GOLD & 0xFFFFFFFF))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), v(t[0]), v(st[0])))
+    a("v_mov_b32 %s, 0x%x" % (v(t[0]), GOLD >> 32))
+    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[0]), v(st[1])))
+    a("v_mov_b32 %s, %s" % (v(z[0]), v(st[0])))
+    a("v_mov_b32 %s, %s" % (v(z[1]), v(st[1])))
+    for shift, mult in ((30, 0xBF58476D1CE4E5B9), (27, 0x94D049BB133111EB)):
+        a("v_lshrrev_b64 %s, %d, %s" % (vp(t[0]), shift, vp(z[0])))
+        a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
+        a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
+        a("v_mov_b32 %s, 0x%x" % (v(t[2]), mult & 0xFFFFFFFF))
+        a("v_mov_b32 %s, 0x%x" % (v(t[3]), mult >> 32))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(t[1]), v(z[0]), v(t[3])))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(t[3]), v(z[1]), v(t[2])))
+        a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(z[0]), sp(S_T + 6), v(z[0]), v(t[2])))
+        a("v_add3_u32 %s, %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1]), v(t[3])))
+    a("v_lshrrev_b64 %s, 31, %s" % (vp(t[0]), vp(z[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
+
+
+def _class_exec(a: Asm, lo_sgpr: Optional[int], hi_sgpr: Optional[int], cls: int, extra=None):
+    """exec = saved & (lo <= cls < hi) [& extra] (compares run on all lanes:
+    VALU compares write 0 for lanes outside exec)."""
+    a("s_mov_b64 exec, %s" % sp(S_T + 4))
+    m = sp(S_T)
+    if lo_sgpr is not None:
+        a("v_cmp_le_u32_e64 %s, %s, %s" % (m, s(lo_sgpr), v(cls)))
+    else:
+        a("s_mov_b64 %s, -1" % m)
+    if hi_sgpr is not None:
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_T + 2), s(hi_sgpr), v(cls)))
+        a("s_and_b64 %s, %s, %s" % (m, m, sp(S_T + 2)))
+    if extra:
+        extra()
+    a("s_and_b64 exec, %s, %s" % (m, sp(S_T + 4)))
+
+
+def _gen_leaf(a: Asm, bank: int):
+    """X[0..7] <- generator value of leaf C for candidate first + lane.
+    Mirrors oracle/gen_ref.py gen_leaf.  Device descriptor (8 words at
+    gen + 32*leaf): width, pool_off (x32 bytes: byte offset), pool_n,
+    pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
+    st, z, tt = [T[0], T[1]], [T[2], T[3]], [T[4], T[5], T[6], T[7]]
+    cls, lo = T[8], T[9]
+    g = S_CUR
+    a("s_load_dwordx2 %s, %s, 0x10" % (sp(S_T), IN["desc"]))       # gen table
+    a("s_lshl_b32 %s, %s, 5" % (s(S_T + 2), s(fld(bank, F_C))))
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
+    # idx = first + lane ; st = seed ^ salt ^ idx * GOLD
+    a("s_mov_b64 %s, %s" % (sp(S_T), IN["first"]))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(T[10]), s(S_T), OP_LANE_LO))
+    a("v_mov_b32 %s, %s" % (v(T[11]), s(S_T + 1)))
+    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(T[11]), v(T[11]), OP_LANE_HI))
+    a("v_mov_b32 %s, 0x%x" % (v(tt[0]), GOLD & 0xFFFFFFFF))
+    a("v_mov_b32 %s, 0x%x" % (v(tt[1]), GOLD >> 32))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(tt[2]), v(T[10]), v(tt[1])))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(tt[3]), v(T[11]), v(tt[0])))
+    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(st[0]), sp(S_T + 6), v(T[10]), v(tt[0])))
+    a("v_add3_u32 %s, %s, %s, %s" % (v(st[1]), v(st[1]), v(tt[2]), v(tt[3])))
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(g + 6)))
+    a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), v(st[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), v(st[1])))
+    sm64(a, st, z, tt)
+    a("v_mov_b32 %s, 100" % v(tt[0]))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), v(tt[0])))
+    a("v_mov_b32 %s, %s" % (v(lo), v(z[0])))
+    for j in range(8):
+        a("v_mov_b32 %s, 0" % v(X[j]))
+    a("s_mov_b64 %s, exec" % sp(S_T + 4))
+    # ---- small: pct_uniform <= cls < pct_small -> one sm64 (64 bits) -------
+    _class_exec(a, g + 3, g + 4, cls)
+    lab = a.uniq("gsm")
+    a("s_cbranch_execz %s" % lab)
+    a("v_mov_b32 %s, %s" % (v(T[10]), v(st[0])))
+    a("v_mov_b32 %s, %s" % (v(T[11]), v(st[1])))
+    sm64(a, [T[10], T[11]], [X[0], X[1]], tt)
+    a.label(lab)
+    # ---- boundary: pct_small <= cls < pct_boundary ------------------------
+    _class_exec(a, g + 4, g + 5, cls)
+    lab = a.uniq("gbd")
+    a("s_cbranch_execz %s" % lab)
+    kind, k, bit, hi = tt
+    a("v_mov_b32 %s, 6" % v(kind))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(kind), v(lo), v(kind)))
+    a("v_mov_b32 %s, 0x9e3779b1" % v(k))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(k), v(lo), v(k)))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(k), v(k), s(g + 0)))
+    # bit = kind==2 ? w-1 : (kind==1 ? 0 : k)
+    a("s_sub_u32 %s, %s, 1" % (s(S_T), s(g + 0)))
+    a("v_mov_b32 %s, %s" % (v(bit), s(S_T)))
+    a("v_cmp_eq_u32 vcc, 2, %s" % v(kind))
+    a("v_cndmask_b32 %s, %s, %s, vcc" % (v(k), v(k), v(bit)))
+    a("v_cmp_eq_u32 vcc, 1, %s" % v(kind))
+    a("v_cndmask_b32 %s, %s, 0, vcc" % (v(k), v(k)))
+    # one-hot for kind in {1,2,4,5}: limb (k>>5) = 1 << (k&31)
+    a("v_lshrrev_b32 %s, 5, %s" % (v(hi), v(k)))
+    a("v_lshlrev_b32 %s, %s, 1" % (v(bit), v(k)))
+    a("v_cmp_ne_u32 vcc, 0, %s" % v(kind))
+    a("v_cmp_ne_u32_e64 %s, 3, %s" % (sp(S_T), v(kind)))
+    a("s_and_b64 vcc, vcc, %s" % sp(S_T))
+    a("v_cndmask_b32 %s, -1, %s, vcc" % (v(hi), v(hi)))
+    for j in range(8):
+        a("v_cmp_eq_u32 vcc, %d, %s" % (j, v(hi)))
+        a("v_cndmask_b32 %s, 0, %s, vcc" % (v(X[j]), v(bit)))
+    # addend: +1 (kind 4), -1 (kinds 3, 5), else 0
+    a("v_cmp_eq_u32 vcc, 4, %s" % v(kind))
+    a("v_cndmask_b32 %s, 0, 1, vcc" % v(k))
+    a("v_cmp_eq_u32 vcc, 3, %s" % v(kind))
+    a("v_cmp_eq_u32_e64 %s, 5, %s" % (sp(S_T), v(kind)))
+    a("s_or_b64 vcc, vcc, %s" % sp(S_T))
+    a("v_cndmask_b32 %s, 0, -1, vcc" % v(hi))
+    a("v_cndmask_b32 %s, %s, -1, vcc" % (v(k), v(k)))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(X[0]), v(X[0]), v(k)))
+    for j in range(1, 8):
+        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(X[j]), v(X[j]), v(hi)))
+    a.label(lab)
+    # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
+    def need_pool():
+        a("s_cmp_lg_u32 %s, 0" % s(g + 2))
+        a("s_cselect_b64 %s, -1, 0" % sp(S_T + 2))
+        a("s_and_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
+    _class_exec(a, g + 5, None, cls, need_pool)
+    lab = a.uniq("gpl")
+    a("s_cbranch_execz %s" % lab)
+    e, delta, t2, hi = tt
+    a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(g + 2)))
+    a("v_lshlrev_b32 %s, 5, %s" % (v(e), v(e)))
+    a("v_add_u32 %s, %s, %s" % (v(e), s(g + 1), v(e)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s" % (X[0], X[3], v(e), sp(S_CONST)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (X[4], X[7], v(e), sp(S_CONST)))
+    a("v_mov_b32 %s, 0x85ebca6b" % v(delta))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(delta), v(lo), v(delta)))
+    a("v_mov_b32 %s, 3" % v(t2))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(delta), v(delta), v(t2)))
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(delta))
+    a("v_cndmask_b32 %s, 0, -1, vcc" % v(hi))
+    a("v_add_u32 %s, -1, %s" % (v(e), v(delta)))
+    a("s_waitcnt vmcnt(0)")
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(X[0]), v(X[0]), v(e)))
+    for j in range(1, 8):
+        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(X[j]), v(X[j]), v(hi)))
+    a.label(lab)
+    # ---- uniform: cls < pct_uniform, or the pool class without a pool ------
+    def uni():
+        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T + 2), s(g + 5), v(cls)))
+        a("s_cmp_eq_u32 %s, 0" % s(g + 2))
+        a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(S_T + 2)))
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_T), s(g + 3), v(cls)))
+        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
+    a("s_mov_b64 exec, %s" % sp(S_T + 4))
+    uni()
+    a("s_and_b64 exec, %s, %s" % (sp(S_T), sp(S_T + 4)))
+    lab = a.uniq("gun")
+    a("s_cbranch_execz %s" % lab)
+    for j in range(0, 8, 2):
+        sm64(a, st, [X[j], X[j + 1]], tt)
+    a.label(lab)
+    a("s_mov_b64 exec, %s" % sp(S_T + 4))
+
+
+def h_leaf(a, bank, root, mask):
+    prologue(a, bank)
+    load_masks(a, fld(bank, F_MOFF))
+    lab_gen, lab_done = a.uniq("lgen"), a.uniq("ldone")
+    a("s_bitcmp1_b32 %s, 0" % IN["mode"])
+    a("s_cbranch_scc1 %s" % lab_gen)
+    _soa_base(a, IN["leaves"], fld(bank, F_C))
+    a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
+    for j in range(8):
+        a("global_load_dword %s, %s, %s" % (v(X[j]), v(T[0]), sp(S_T)))
+        if j < 7:
+            _soa_step(a)
+    a("s_waitcnt vmcnt(0)")
+    a("s_branch %s" % lab_done)
+    a.label(lab_gen)
+    _gen_leaf(a, bank)
+    a("s_waitcnt lgkmcnt(0)")
+    for j in range(8):
+        a("v_and_b32 %s, %s, %s" % (v(X[j]), s(S_M + j), v(X[j])))
+    _store_soa(a, X, IN["lout"], fld(bank, F_C))
+    a.label(lab_done)
+    finish(a, bank, X, root, True)
+
+
+# ---------------------------------------------------------------------------
+# heavy ops: per-(bank, variant) stubs copy the record to S_CUR and branch to
+# a shared body; the body prefetches the next record into bank A
+# ---------------------------------------------------------------------------
+
+def heavy_stub(a: Asm, bank: int, varbits: int, body: str):
+    b = BANK[bank]
+    for k in range(0, 8, 2):
+        a("s_mov_b64 %s, %s" % (sp(S_CUR + k), sp(b + k)))
+    a("s_mov_b32 %s, %d" % (s(S_VAR), varbits))
+    a("s_branch %s" % body)
+
+
+def heavy_prologue(a: Asm):
+    a("s_load_dwordx8 s[%d:%d], %s, %s" % (BANK[0], BANK[0] + 7, sp(S_CODE), s(S_IP)))
+    a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
+    load_masks(a, cur(F_MOFF))     # MOFF always names a valid 8-word entry
+
+
+def heavy_finish(a: Asm, res: List[int]):
+    """Write (masked when variant bit1), fold ROOT when bit0, dispatch (A)."""
+    lab_nm, lab_done, lab_nr = a.uniq("hnm"), a.uniq("hwd"), a.uniq("hnr")
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
+    a("s_cbranch_scc0 %s" % lab_nm)
+    a.write_slot(res, cur(F_D), S_M)
+    a("s_branch %s" % lab_done)
+    a.label(lab_nm)
+    a.write_slot(res, cur(F_D), None)
+    a.label(lab_done)
+    a("s_bitcmp1_b32 %s, 0" % s(S_VAR))
+    a("s_cbranch_scc0 %s" % lab_nr)
+    a.root_and(v(res[0]))
+    a.label(lab_nr)
+    dispatch(a, 0)
+
+
+def col_product(a: Asm, x: List[int], y: List[int], ncols: int, out: Optional[List[int]] = None,
+                hi_or: Optional[int] = None):
+    """Product scanning of x*y over columns 0..ncols-1 with a 96-bit column
+    accumulator: the aligned pair (A0:A1) takes every 64-bit product
+    (v_mad_u64_u32), its carry-out goes to A2; the column digit is then A0
+    and the accumulator shifts down one word.  Column c < 8 goes to out[c]
+    (if given); with hi_or, columns >= 8 and the bits of columns < 8 outside
+    the masks s[S_M+c] (loaded and waited for) are OR-ed into v[hi_or].
+    Uses T4..T6, TMP, vcc, s[S_T+6:S_T+7]."""
+    A0, A1, A2 = T[4], T[5], T[6]
+    for r in (A0, A1, A2):
+        a("v_mov_b32 %s, 0" % v(r))
+    if hi_or is not None:
+        a("v_mov_b32 %s, 0" % v(hi_or))
+    for c in range(ncols):
+        last = c == ncols - 1
+        for i in range(max(0, c - 7), min(c, 7) + 1):
+            j = c - i
+            a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (
+                A0, A1, sp(S_T + 6), v(x[i]), v(y[j]), A0, A1))
+            if not last:
+                a("v_addc_co_u32 %s, vcc, 0, %s, %s" % (v(A2), v(A2), sp(S_T + 6)))
+        if out is not None and c < 8:
+            a("v_mov_b32 %s, %s" % (v(out[c]), v(A0)))
+        if hi_or is not None:
+            if c >= 8:
+                a("v_or_b32 %s, %s, %s" % (v(hi_or), v(hi_or), v(A0)))
+            else:
+                a("v_bfi_b32 %s, %s, 0, %s" % (v(TMP), s(S_M + c), v(A0)))
+                a("v_or_b32 %s, %s, %s" % (v(hi_or), v(hi_or), v(TMP)))
+        if not last:
+            a("v_mov_b32 %s, %s" % (v(A0), v(A1)))
+            a("v_mov_b32 %s, %s" % (v(A1), v(A2)))
+            a("v_mov_b32 %s, 0" % v(A2))
+
+
+def body_mul(a: Asm):
+    a.label(".Lbody_MUL_%=")
+    heavy_prologue(a)
+    a.read_slot(X, cur(F_A))
+    a.read_slot(Y, cur(F_B))
+    col_product(a, X, Y, 8, out=R)
+    heavy_finish(a, R)
+
+
+def body_umulno(a: Asm):
+    """R0 = (x*y < 2^W): the 512-bit product has no bit at or above W (the
+    width masks are all-ones for W = 256, so the low columns add nothing)."""
+    a.label(".Lbody_UMULNO_%=")
+    heavy_prologue(a)
+    a.read_slot(X, cur(F_A))
+    a.read_slot(Y, cur(F_B))
+    a("s_waitcnt lgkmcnt(0)")
+    col_product(a, X, Y, 16, hi_or=T[7])
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(T[7]))
+    a("v_cndmask_b32 %s, 0, 1, vcc" % v(R[0]))
+    for j in range(1, 8):
+        a("v_mov_b32 %s, 0" % v(R[j]))
+    a("s_and_b32 %s, %s, 1" % (s(S_VAR), s(S_VAR)))      # Bool result: never masked
+    heavy_finish(a, R)
+
+
+# ---- per-lane shifts ------------------------------------------------------
+
+def barrel_right(a: Asm, t: List[int], q: int, nl: int):
+    """t[0..nl-1] = t >> (32*q) limbs (q per lane in v[q] < 8), zero fill."""
+    for st in (1, 2, 4):
+        a("v_and_b32 %s, %d, %s" % (v(TMP), st, v(q)))
+        a("v_cmp_ne_u32 vcc, 0, %s" % v(TMP))
+        skip = a.uniq("brr")
+        a("s_cbranch_vccz %s" % skip)
+        for j in range(nl):
+            src = v(t[j + st]) if j + st < nl else "0"
+            a("v_cndmask_b32 %s, %s, %s, vcc" % (v(t[j]), v(t[j]), src))
+        a.label(skip)
+
+
+def barrel_left(a: Asm, t: List[int], q: int, nl: int, live: Optional[int] = None):
+    """t[0..nl-1] = t << (32*q) limbs (q < 8), zero fill; ``live`` = number
+    of possibly-nonzero low limbs on entry (known-zero moves are skipped)."""
+    hi = nl if live is None else live
+    for st in (1, 2, 4):
+        a("v_and_b32 %s, %d, %s" % (v(TMP), st, v(q)))
+        a("v_cmp_ne_u32 vcc, 0, %s" % v(TMP))
+        top = min(nl, hi + st)
+        skip = a.uniq("brl")
+        a("s_cbranch_vccz %s" % skip)
+        for j in reversed(range(top)):
+            src = v(t[j - st]) if j - st >= 0 else "0"
+            a("v_cndmask_b32 %s, %s, %s, vcc" % (v(t[j]), v(t[j]), src))
+        a.label(skip)
+        hi = top
+
+
+def bitshift_right(a: Asm, t: List[int], b: int, n_out: int):
+    """t[j] = (t[j+1]:t[j]) >> b for j < n_out (t[n_out] must exist)."""
+    for j in range(n_out):
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(t[j]), v(t[j + 1]), v(t[j]), v(b)))
+
+
+def bitshift_left(a: Asm, t: List[int], b: int, c: int, bz: int, nl: int):
+    """t[j] = t[j] << b | t[j-1] >> (32-b), j = nl-1..0 (t[-1] = 0);
+    c = (32 - b) & 31; s[bz:bz+1] = lanes with b == 0."""
+    for j in reversed(range(nl)):
+        lo = v(t[j - 1]) if j > 0 else "0"
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(TMP), v(t[j]), lo, v(c)))
+        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(t[j]), v(TMP), v(t[j]), sp(bz)))
+
+
+def body_shift(a: Asm, kind: str):
+    """SHL / LSHR / ASHR of F[a] by F[b] at width W."""
+    a.label(".Lbody_%s_%%=" % kind)
+    heavy_prologue(a)
+    a.read_slot(X, cur(F_A))
+    a.read_slot(Y, cur(F_B))
+    a("s_waitcnt lgkmcnt(0)")
+    over = S_X                     # s[88:89] lanes shifting by >= W
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(Y[1]), v(Y[2]), v(Y[3])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(T[0]), v(Y[4]), v(Y[5])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(T[0]), v(Y[6]), v(Y[7])))
+    a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(over), v(T[0])))
+    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), s(cur(F_W)), v(Y[0])))
+    a("s_or_b64 %s, %s, %s" % (sp(over), sp(over), sp(S_T)))
+    a("v_lshrrev_b32 %s, 5, %s" % (v(T[2]), v(Y[0])))
+    a("v_and_b32 %s, 7, %s" % (v(T[2]), v(T[2])))           # q (over lanes masked later)
+    a("v_and_b32 %s, 31, %s" % (v(T[3]), v(Y[0])))          # b
+    fill = None
+    if kind == "ASHR":
+        lab = a.uniq("asx")
+        a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
+        a("s_cbranch_scc0 %s" % lab)
+        sext(a, X, cur(F_W), S_M, T[4], S_T)
+        a.label(lab)
+        a("v_ashrrev_i32 %s, 31, %s" % (v(T[4]), v(X[7])))
+        for j in range(8):
+            a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[4])))
+        fill = T[4]
+    if kind == "SHL":
+        a("v_sub_u32 %s, 32, %s" % (v(T[5]), v(T[3])))
+        a("v_and_b32 %s, 31, %s" % (v(T[5]), v(T[5])))
+        a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_X + 2), v(T[3])))
+        barrel_left(a, X, T[2], 8)
+        bitshift_left(a, X, T[3], T[5], S_X + 2, 8)
+    else:
+        a("v_mov_b32 %s, 0" % v(R[0]))
+        t = X + [R[0]]
+        barrel_right(a, t, T[2], 8)
+        bitshift_right(a, t, T[3], 8)
+    for j in range(8):
+        if fill is None:
+            a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(R[j]), v(X[j]), sp(over)))
+        else:
+            a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(fill)))
+            a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(fill), sp(over)))
+    if kind == "LSHR":
+        a("s_and_b32 %s, %s, 1" % (s(S_VAR), s(S_VAR)))     # canonical: no mask needed
+    heavy_finish(a, R)
+
+
+# ---- division ---------------------------------------------------------------
+#
+# Unsigned 256/256 Knuth D on 32-bit digits, as udivrem256 in the C++
+# reference kernel: normalise by sh = clz(v) (limbs + bits) so vn's top digit
+# is vn[7]; un = u << sh (17 digits); quotient digit j (7..0) from un[j+8],
+# un[j+7], un[j+6] with the Moller-Granlund reciprocal of d = vn[7] and
+# Knuth's two-digit correction; multiply-subtract; add back if negative.
+# An iteration is skipped when no lane of the wave has un[j+8] != 0 or
+# un[j+7] >= d (its quotient digit is then 0 and nothing changes).
+# Registers: u = X, v = Y on entry; un = X ++ R ++ [T0]; vn = Y;
+# q/b/c = T2/T3/T4 (kept for the remainder); dinv = T1; digit temps T5..T11.
+
+def clz256(a: Asm, vals: List[int], out: int, t: int):
+    a("v_mov_b32 %s, 256" % v(out))
+    for j in range(8):
+        a("v_ffbh_u32 %s, %s" % (v(t), v(vals[j])))
+        a("v_add_u32 %s, %d, %s" % (v(t), (7 - j) * 32, v(t)))
+        a("v_cmp_ne_u32 vcc, 0, %s" % v(vals[j]))
+        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(out), v(out), v(t)))
+
+
+def udivrem(a: Asm, want_rem: bool):
+    """X / Y (Y != 0 in every lane): quotient -> R; remainder (want_rem) -> X.
+    Registers: un = X ++ R ++ [T0]; vn = Y; q/b/c = T1/T2/T3 (kept for the
+    remainder); pairs T4:T5, T6:T7, T8:T9 (64-bit tuples start even on
+    gfx950); dinv = T10.  Clobbers Y, T, vcc, s[S_T..S_T+7]."""
+    un = X + R + [T[0]]
+    vn = Y
+    sh, q, b, c, dinv = T[1], T[1], T[2], T[3], T[10]
+    bz = S_T + 4
+    for j in range(8):
+        a("v_mov_b32 %s, 0" % v(R[j]))
+    clz256(a, Y, sh, T[4])
+    a("v_and_b32 %s, 31, %s" % (v(b), v(sh)))
+    a("v_lshrrev_b32 %s, 5, %s" % (v(q), v(sh)))
+    a("v_sub_u32 %s, 32, %s" % (v(c), v(b)))
+    a("v_and_b32 %s, 31, %s" % (v(c), v(c)))
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(bz), v(b)))
+    barrel_left(a, vn, q, 8)
+    bitshift_left(a, vn, b, c, bz, 8)
+    barrel_left(a, un, q, 16, live=8)
+    a("v_alignbit_b32 %s, 0, %s, %s" % (v(T[0]), v(un[15]), v(c)))       # un[16]
+    a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(T[0]), v(T[0]), sp(bz)))
+    bitshift_left(a, un, b, c, bz, 16)
+    d, d6 = vn[7], vn[6]
+    # dinv = floor((2^64-1)/d) - 2^32 (d >= 2^31): f64 reciprocal, one
+    # Newton step, then exact integer correction (two rounds)
+    f0, f1, fe = T[4], T[6], T[8]
+    a("v_cvt_f64_u32_e32 %s, %s" % (vp(f0), v(d)))
+    a("v_rcp_f64_e32 %s, %s" % (vp(f1), vp(f0)))
+    a("s_nop 1")
+    a("v_fma_f64 %s, -%s, %s, 1.0" % (vp(fe), vp(f0), vp(f1)))            # e = 1 - d*r
+    a("v_fma_f64 %s, %s, %s, %s" % (vp(f1), vp(f1), vp(fe), vp(f1)))      # r += r*e
+    a("v_ldexp_f64 %s, %s, 64" % (vp(f1), vp(f1)))
+    a("s_mov_b32 %s, 0" % s(S_T + 6))
+    a("s_mov_b32 %s, 0xc1f00000" % s(S_T + 7))                          # -2^32
+    a("v_add_f64 %s, %s, %s" % (vp(f1), vp(f1), sp(S_T + 6)))
+    a("v_cvt_u32_f64_e32 %s, %s" % (v(dinv), vp(f1)))
+    a("s_nop 1")
+    p0, p1, tt = T[4], T[5], T[6]
+    for _ in range(2):
+        # p = dinv*d + (d << 32) = (2^32 + dinv) * d; carry -> too big
+        a("v_mov_b32 %s, 0" % v(p0))
+        a("v_mov_b32 %s, %s" % (v(p1), v(d)))
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (p0, p1, sp(S_T + 6), v(dinv), v(d), p0, p1))
+        a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(tt), sp(S_T + 6)))
+        a("v_sub_u32 %s, %s, %s" % (v(dinv), v(dinv), v(tt)))
+        # too small: (2^64-1) - p >= d  <=>  ~p_hi != 0 or ~p_lo >= d
+        a("v_not_b32 %s, %s" % (v(p0), v(p0)))
+        a("v_not_b32 %s, %s" % (v(p1), v(p1)))
+        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T + 2), v(p1)))
+        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), v(d), v(p0)))
+        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
+        a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 6)))
+        a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(tt), sp(S_T)))
+        a("v_add_u32 %s, %s, %s" % (v(dinv), v(dinv), v(tt)))
+    for j in reversed(range(8)):
+        u2, u1 = un[j + 8], un[j + 7]
+        skip = a.uniq("dvs")
+        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(u2)))
+        a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(u1), v(d)))
+        a("s_or_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 2)))
+        a("s_cbranch_vccz %s" % skip)
+        _div_digit(a, un, vn, j, d, d6, dinv)
+        a.label(skip)
+    if want_rem:
+        # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
+        a("v_mov_b32 %s, 0" % v(T[0]))
+        t = X + [T[0]]
+        barrel_right(a, t, q, 9)
+        bitshift_right(a, t, b, 8)
+
+
+def _div_digit(a: Asm, un, vn, j, d, d6, dinv):
+    u2, u1, u0 = un[j + 8], un[j + 7], un[j + 6]
+    A0, A1, P0, P1, CR, RH, QH = T[4], T[5], T[6], T[7], T[8], T[9], T[11]
+    RL = A1
+    st = S_T
+    lt = sp(st)                  # lanes with u2 < d
+    # qq = dinv * a2 + (a2:u1), a2 = u2 < d ? u2 : 0
+    a("v_cmp_lt_u32_e64 %s, %s, %s" % (lt, v(u2), v(d)))
+    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(A1), v(u2), lt))
+    a("v_mov_b32 %s, %s" % (v(A0), v(u1)))
+    a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (A0, A1, sp(st + 6), v(dinv), v(A1), A0, A1))
+    a("v_add_u32 %s, 1, %s" % (v(QH), v(A1)))                       # q1 (A0 = q0)
+    a("v_mul_lo_u32 %s, %s, %s" % (v(CR), v(QH), v(d)))
+    a("v_sub_u32 %s, %s, %s" % (v(CR), v(u1), v(CR)))                # r
+    a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(A0)))   # r > q0
+    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
+    a("v_sub_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
+    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
+    a("v_add_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
+    a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(d)))     # r >= d
+    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
+    a("v_add_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
+    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
+    a("v_sub_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
+    # u2 >= d (u2 == d): qhat = b-1, rhat = u1 + d (65 bits)
+    a("v_cndmask_b32_e64 %s, -1, %s, %s" % (v(QH), v(QH), lt))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(P0), v(u1), v(d)))
+    a("v_cndmask_b32 %s, 0, 1, vcc" % v(P1))
+    a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(RL), v(P0), v(CR), lt))
+    a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(RH), v(P1), lt))
+    # Knuth's test (twice): rh < 2^32 and qh*d6 > rh*2^32 + u0 -> qh--, rh += d
+    for _ in range(2):
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(d6)))
+        a("v_mov_b32 %s, %s" % (v(A0), v(u0)))                      # (A0, A1) = u0 : rh_lo
+        a("v_cmp_gt_u64_e64 %s, v[%d:%d], v[%d:%d]" % (sp(st + 2), P0, P1, A0, A1))
+        a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(st + 4), v(RH)))
+        a("s_and_b64 %s, %s, %s" % (sp(st + 2), sp(st + 2), sp(st + 4)))
+        a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
+        a("v_sub_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
+        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
+        a("v_add_co_u32 %s, vcc, %s, %s" % (v(RL), v(RL), v(P0)))
+        a("v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(RH), v(RH)))
+    # multiply-subtract un[j..j+8] -= qh * vn
+    a("v_mov_b32 %s, 0" % v(CR))
+    a("s_mov_b64 %s, 0" % sp(st + 4))
+    for i in range(8):
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(vn[i])))
+        a("v_add_co_u32 %s, vcc, %s, %s" % (v(P0), v(P0), v(CR)))
+        a("v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(CR), v(P1)))
+        a("v_sub_co_u32 %s, %s, %s, %s" % (v(un[j + i]), sp(st + 2), v(un[j + i]), v(P0)))
+        a("v_subb_co_u32 %s, vcc, %s, 0, %s" % (v(un[j + i]), v(un[j + i]), sp(st + 4)))
+        a("s_or_b64 %s, %s, vcc" % (sp(st + 4), sp(st + 2)))
+    a("v_sub_co_u32 %s, %s, %s, %s" % (v(u2), sp(st + 2), v(u2), v(CR)))
+    a("v_subb_co_u32 %s, vcc, %s, 0, %s" % (v(u2), v(u2), sp(st + 4)))
+    a("s_or_b64 %s, %s, vcc" % (sp(st + 4), sp(st + 2)))
+    lab = a.uniq("dab")
+    a("s_cmp_eq_u64 %s, 0" % sp(st + 4))
+    a("s_cbranch_scc1 %s" % lab)
+    a("v_cndmask_b32_e64 %s, 0, -1, %s" % (v(P1), sp(st + 4)))
+    a("v_and_b32 %s, %s, %s" % (v(P0), v(vn[0]), v(P1)))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(un[j]), v(un[j]), v(P0)))
+    for i in range(1, 8):
+        a("v_and_b32 %s, %s, %s" % (v(P0), v(vn[i]), v(P1)))
+        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
+    a.label(lab)
+    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 4)))
+    a("v_sub_u32 %s, %s, %s" % (v(u2), v(QH), v(P0)))
+
+
+def _cond_neg(a: Asm, regs: List[int], m: int):
+    a("v_sub_co_u32 %s, vcc, 0, %s" % (v(T[1]), v(regs[0])))
+    a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(regs[0]), v(regs[0]), v(T[1]), sp(m)))
+    for j in range(1, 8):
+        a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(T[1]), v(regs[j])))
+        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(regs[j]), v(regs[j]), v(T[1]), sp(m)))
+
+
+DIV_CODE = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
+
+
+def body_div(a: Asm):
+    """UDIV/UREM/SDIV/SREM/SMOD (op = S_VAR >> 4), SMT-LIB semantics."""
+    NS, NT, Z, OPR = S_X, S_X + 2, S_X + 4, S_X + 6
+    a.label(".Lbody_DIV_%=")
+    heavy_prologue(a)
+    a.read_slot(X, cur(F_A))
+    a.read_slot(Y, cur(F_B))
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_lshr_b32 %s, %s, 4" % (s(OPR), s(S_VAR)))
+    lab_u = a.uniq("du")
+    a("s_cmp_lt_u32 %s, 2" % s(OPR))
+    a("s_cbranch_scc1 %s" % lab_u)
+    lab_ns = a.uniq("dns")
+    a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
+    a("s_cbranch_scc0 %s" % lab_ns)
+    sext(a, X, cur(F_W), S_M, T[0], S_T)
+    sext(a, Y, cur(F_W), S_M, T[0], S_T)
+    a.label(lab_ns)
+    a("v_cmp_gt_i32_e64 %s, 0, %s" % (sp(NS), v(X[7])))
+    a("v_cmp_gt_i32_e64 %s, 0, %s" % (sp(NT), v(Y[7])))
+    _cond_neg(a, X, NS)
+    _cond_neg(a, Y, NT)
+    a.label(lab_u)
+    or_reduce(a, Y, T[0])
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(Z), v(T[0])))
+    a("v_cndmask_b32_e64 %s, %s, 1, %s" % (v(Y[0]), v(Y[0]), sp(Z)))
+    lab_q, lab_dd = a.uniq("dq"), a.uniq("ddd")
+    a("s_cmp_eq_u32 %s, 0" % s(OPR))
+    a("s_cbranch_scc1 %s" % lab_q)
+    a("s_cmp_eq_u32 %s, 2" % s(OPR))
+    a("s_cbranch_scc1 %s" % lab_q)
+    udivrem(a, want_rem=True)
+    a("s_branch %s" % lab_dd)
+    a.label(lab_q)
+    udivrem(a, want_rem=False)
+    a.label(lab_dd)
+    # R = q (== |u| where the divisor was forced to 1), X = remainder
+    labs = {k: a.uniq("dr%d" % k) for k in range(5)}
+    lab_end = a.uniq("dre")
+    for k in range(1, 5):
+        a("s_cmp_eq_u32 %s, %d" % (s(OPR), k))
+        a("s_cbranch_scc1 %s" % labs[k])
+    a.label(labs[0])                                   # udiv: z ? ~0 : q
+    for j in range(8):
+        a("v_cndmask_b32_e64 %s, %s, -1, %s" % (v(R[j]), v(R[j]), sp(Z)))
+    a("s_branch %s" % lab_end)
+    a.label(labs[1])                                   # urem: z ? q : rem
+    for j in range(8):
+        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j]), sp(Z)))
+    a("s_branch %s" % lab_end)
+    a.label(labs[2])                                   # sdiv
+    for j in range(8):
+        a("v_cndmask_b32_e64 %s, %s, -1, %s" % (v(R[j]), v(R[j]), sp(Z)))
+    a("s_xor_b64 %s, %s, %s" % (sp(NS), sp(NS), sp(NT)))
+    _cond_neg(a, R, NS)
+    a("s_branch %s" % lab_end)
+    a.label(labs[3])                                   # srem: sign of the dividend
+    for j in range(8):
+        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j]), sp(Z)))
+    _cond_neg(a, R, NS)
+    a("s_branch %s" % lab_end)
+    a.label(labs[4])                                   # smod
+    for j in range(8):                                 # m = z ? q : rem  -> X
+        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(X[j]), v(X[j]), v(R[j]), sp(Z)))
+    a.read_slot(Y, cur(F_B))                           # t again
+    lab_nx = a.uniq("dsx")
+    a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
+    a("s_cbranch_scc0 %s" % lab_nx)
+    sext(a, Y, cur(F_W), S_M, T[0], S_T)
+    a.label(lab_nx)
+    a("v_sub_co_u32 %s, vcc, 0, %s" % (v(R[0]), v(X[0])))             # R = -m
+    for j in range(1, 8):
+        a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(R[j]), v(X[j])))
+    for j in range(8):                                 # base = ns ? -m : m
+        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j]), sp(NS)))
+    a("s_xor_b64 %s, %s, %s" % (sp(NT), sp(NS), sp(NT)))               # ns != nt: + t
+    for j in range(8):
+        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(Y[j]), v(Y[j]), sp(NT)))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(R[0]), v(Y[0])))
+    for j in range(1, 8):
+        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(R[j]), v(R[j]), v(Y[j])))
+    or_reduce(a, X, T[0])                              # m == 0 -> 0
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(T[0]))
+    for j in range(8):
+        a("v_cndmask_b32 %s, %s, 0, vcc" % (v(R[j]), v(R[j])))
+    a.label(lab_end)
+    heavy_finish(a, R)
+
+
+# ---------------------------------------------------------------------------
+# the whole interpreter
+# ---------------------------------------------------------------------------
+
+CHEAP = {
+    "NOP": h_nop, "HALT": h_halt, "CONST": h_const, "LEAF": h_leaf,
+    "SPILL_LDS": h_spill_lds, "SPILL_SCR": h_spill_scr, "RELOAD_LDS": h_reload_lds,
+    "RELOAD_SCR": h_reload_scr, "ADD": h_add, "SUB": h_sub, "AND": h_and, "OR": h_or,
+    "XOR": h_xor, "NOT": h_not, "EQ": h_eq, "ULT": h_ult, "ULE": h_ule, "SLT": h_slt,
+    "SLE": h_sle, "ITE": h_ite, "CONCAT": h_concat, "EXTRACT": h_extract, "SEXT": h_sext,
+    "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov,
+}
+HEAVY = {"MUL": "MUL", "UMULNO": "UMULNO", "SHL": "SHL", "LSHR": "LSHR", "ASHR": "ASHR",
+         "UDIV": "DIV", "UREM": "DIV", "SDIV": "DIV", "SREM": "DIV", "SMOD": "DIV"}
+HEAVY_AOPS = sorted(AOP[n] for n in HEAVY)
+
+
+def generate() -> List[str]:
+    a = Asm()
+    a("s_mov_b32 %s, m0" % s(S_M0))
+    # mg_pdesc: code@0 consts@8 gen@16 ... xcode@48
+    a("s_load_dwordx2 %s, %s, 0x8" % (sp(S_CONST), IN["desc"]))
+    a("s_load_dwordx2 %s, %s, 0x30" % (sp(S_CODE), IN["desc"]))
+    a("v_mov_b32 %s, 1" % OP_ROOT)
+    a("s_getpc_b64 %s" % sp(S_BASE))
+    a.label(".Lbase_%=")
+    a("s_bitcmp1_b32 %s, 1" % IN["mode"])
+    a("s_cbranch_scc1 .Lquery_%=")
+    a("s_mov_b32 %s, 32" % s(S_IP))
+    a("s_waitcnt lgkmcnt(0)")
+    a("s_load_dwordx8 s[%d:%d], %s, 0x0" % (BANK[0], BANK[0] + 7, sp(S_CODE)))
+    dispatch(a, 0)
+    # query mode: table[h] = offset of handler h from .Lbase
+    a.label(".Lquery_%=")
+    a("v_mov_b32 %s, 0" % v(T[0]))
+    a("s_mov_b64 %s, %s" % (sp(S_T), IN["table"]))
+    for h in range(NUM_HANDLERS):
+        if h and h % 512 == 0:
+            a("s_add_u32 %s, %s, 2048" % (s(S_T), s(S_T)))
+            a("s_addc_u32 %s, %s, 0" % (s(S_T + 1), s(S_T + 1)))
+        a("v_mov_b32 %s, (.Lh%d_%%= - .Lbase_%%=)" % (v(T[1]), h))
+        a("global_store_dword %s, %s, %s offset:%d" % (v(T[0]), v(T[1]), sp(S_T), 4 * (h % 512)))
+    a("s_waitcnt vmcnt(0)")
+    a("s_branch .Lexit_%=")
+    for name in AOPS:
+        aop = AOP[name]
+        for var in range(NVAR):
+            root_v, mask_v = bool(var & V_ROOT), bool(var & V_MASK)
+            for bank in (0, 1):
+                a.label(".Lh%d_%%=" % hid(aop, var, bank))
+                if name in CHEAP:
+                    CHEAP[name](a, bank, root_v, mask_v)
+                else:
+                    bits = var | (DIV_CODE.get(name, 0) << 4)
+                    heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
+    body_mul(a)
+    body_umulno(a)
+    for k in ("SHL", "LSHR", "ASHR"):
+        body_shift(a, k)
+    body_div(a)
+    a.label(".Lexit_%=")
+    a("s_set_gpr_idx_off")
+    a("s_mov_b32 m0, %s" % s(S_M0))
+    return a.lines
+
+
+def clobbers() -> List[str]:
+    vs = ['"v%d"' % i for i in range(NVGPR_FIXED)]
+    ss = ['"s%d"' % i for i in range(BANK[0], S_LAST + 1)]
+    # m0 is saved/restored inside; exec is restored on every path
+    return vs + ss + ['"vcc"', '"scc"', '"memory"']
+
+
+def write_outputs(csrc: str) -> None:
+    lines = generate()
+    body = " \\\n".join('"%s\\n"' % l.replace('"', '\\"') for l in lines)
+    inc = ("// GENERATED by mythril_amd/asmgen.py -- do not edit.\n"
+           "// Inline-asm body of mg_interp_asm (gfx950), %d lines.\n"
+           "#define MG_ASM_BODY \\\n%s\n\n"
+           "#define MG_ASM_CLOBBERS %s\n") % (len(lines), body, ", ".join(clobbers()))
+    _write_if_changed(os.path.join(csrc, "mg_interp_gfx950.inc"), inc)
+    hdr = ["// GENERATED by mythril_amd/asmgen.py -- do not edit.",
+           "#ifndef MG_ASM_HANDLERS_H", "#define MG_ASM_HANDLERS_H",
+           "#define MGA_NUM_HANDLERS %d" % NUM_HANDLERS,
+           "#define MGA_NVAR %d" % NVAR,
+           "#define MGA_V_ROOT %d" % V_ROOT, "#define MGA_V_MASK %d" % V_MASK,
+           "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
+           "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,
+           "enum mga_op {"]
+    hdr += ["    MGA_%s = %d," % (n, i) for i, n in enumerate(AOPS)]
+    hdr += ["    MGA_NUM_OPS = %d" % len(AOPS), "};",
+            "/* heavy ops always prefetch the next record into bank A */",
+            "static inline int mga_is_heavy(int aop) {",
+            "    return " + " || ".join("aop == %d" % x for x in HEAVY_AOPS) + ";", "}",
+            "#endif", ""]
+    _write_if_changed(os.path.join(csrc, "mg_asm_handlers.h"), "\n".join(hdr))
+
+
+def _write_if_changed(path: str, text: str) -> None:
+    if os.path.exists(path):
+        with open(path) as fh:
+            if fh.read() == text:
+                return
+    with open(path, "w") as fh:
+        fh.write(text)
+
+
+if __name__ == "__main__":
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    write_outputs(here)
+    print("wrote", here)

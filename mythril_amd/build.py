@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "mythril_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "mythril_amd", "lib")
 LIB = os.path.join(LIBDIR, "libmythgpu.so")
-SOURCES = ["mg_kernels.hip", "mg_keccak.hip", "mg_api.cpp"]
+SOURCES = ["mg_interp_asm.hip", "mg_kernels.hip", "mg_keccak.hip", "mg_api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
 
@@ -17,7 +17,8 @@ ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
 def _deps():
     files = [os.path.join(CSRC, s) for s in SOURCES]
     files += [os.path.join(CSRC, "mg_device.h"), os.path.join(ROOT, "include", "mythgpu.h"),
-              os.path.join(ROOT, "include", "mythgpu_ir.h")]
+              os.path.join(ROOT, "include", "mythgpu_ir.h"),
+              os.path.join(ROOT, "mythril_amd", "asmgen.py")]
     return files
 
 
@@ -39,6 +40,9 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     if not force and out == LIB and up_to_date():
         return LIB
     os.makedirs(os.path.dirname(out), exist_ok=True)
+    # the assembly interpreter's body and handler numbering are generated
+    from mythril_amd import asmgen
+    asmgen.write_outputs(CSRC)
     objs = []
     for src in SOURCES:
         obj = out + "." + src + ".o"

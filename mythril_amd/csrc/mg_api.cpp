@@ -11,10 +11,16 @@
 #include <string>
 #include <vector>
 
+#include <cstdlib>
+#include <map>
+
 #include "mythgpu.h"
 #include "mythgpu_ir.h"
 #include "mg_device.h"
+#include "mg_asm_handlers.h"
 
+hipError_t mg_launch_asm(const mg_pdesc* d_descs, uint32_t n_progs, const mg_run& run,
+                         uint32_t mode, uint32_t lds_slots, uint32_t* table, hipStream_t stream);
 hipError_t mg_launch_interp(int gen, const mg_pdesc* d_descs, uint32_t n_progs, const mg_run& run,
                             uint32_t lds_slots, hipStream_t stream);
 hipError_t mg_launch_keccak(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
@@ -28,6 +34,11 @@ struct mg_ctx {
     std::string err;
     char name[256] = {0};
     int cus = 0;
+    // assembly interpreter: handler byte offsets (query launch at init),
+    // LDS spill slots per 256-lane block, and the kernel choice
+    uint32_t hoff[MGA_NUM_HANDLERS] = {0};
+    uint32_t lds_slots = 6;
+    bool use_asm = true;
     // grow-only device workspace for synchronous calls
     void* ws = nullptr;
     size_t ws_size = 0;
@@ -35,10 +46,24 @@ struct mg_ctx {
 
 struct mg_prog {
     mg_ctx* ctx = nullptr;
-    void* d_blob = nullptr;         // code | consts | gen | desc
+    void* d_blob = nullptr;         // code | consts | gen | desc | xcode
     mg_pdesc* d_desc = nullptr;
     uint32_t n_ins = 0, n_consts = 0, n_leaves = 0, n_lds = 0, n_probes = 0;
 };
+
+static uint32_t kernel_lds_slots(const mg_ctx* ctx, uint32_t n_lds) {
+    return ctx->use_asm ? (n_lds < ctx->lds_slots ? n_lds : ctx->lds_slots) : n_lds;
+}
+
+// one place that picks the kernel: the assembly interpreter (default) or the
+// compiled C++ interpreter kept for A/B (MYTHGPU_KERNEL=cxx)
+static hipError_t launch(const mg_ctx* ctx, int gen, const mg_pdesc* d_descs, uint32_t n_progs,
+                         const mg_run& run, uint32_t n_lds, hipStream_t stream) {
+    if (ctx->use_asm)
+        return mg_launch_asm(d_descs, n_progs, run, gen ? 1u : 0u, kernel_lds_slots(ctx, n_lds),
+                             nullptr, stream);
+    return mg_launch_interp(gen, d_descs, n_progs, run, n_lds, stream);
+}
 
 struct mg_batch {
     mg_ctx* ctx = nullptr;
@@ -78,9 +103,189 @@ static int workspace(mg_ctx* ctx, size_t bytes, void** out) {
     return MG_OK;
 }
 
+static int validate(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
+                    const mg_leafgen* leaves, uint32_t n_leaves, uint32_t n_lds,
+                    uint32_t n_spill, uint32_t n_probes);
+
+// One launch in query mode: the assembly interpreter writes the byte offset
+// of every handler (relative to its dispatch base) into a table.
+static int query_handlers(mg_ctx* ctx) {
+    void* d = nullptr;
+    const size_t tab_b = sizeof(uint32_t) * MGA_NUM_HANDLERS;
+    HIPCHECK(ctx, hipMalloc(&d, tab_b + 256));
+    mg_pdesc* d_desc = (mg_pdesc*)((uint8_t*)d + tab_b);
+    mg_pdesc zero;
+    memset(&zero, 0, sizeof zero);
+    zero.consts = (const uint32_t*)d;
+    zero.xcode = (const uint32_t*)d;
+    hipError_t e = hipMemcpy(d_desc, &zero, sizeof zero, hipMemcpyHostToDevice);
+    mg_run run;
+    memset(&run, 0, sizeof run);
+    run.n_assign = 1;
+    run.stride = 1;
+    if (e == hipSuccess) e = mg_launch_asm(d_desc, 1, run, 2u, 0, (uint32_t*)d, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(ctx->hoff, d, tab_b, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(ctx, MG_E_HIP, "handler query: %s", hipGetErrorString(e));
+    for (int h = 0; h < MGA_NUM_HANDLERS; ++h)
+        if (ctx->hoff[h] == 0 || ctx->hoff[h] > (1u << 24))
+            return fail(ctx, MG_E_HIP, "handler query: bad offset %u for %d", ctx->hoff[h], h);
+    return MG_OK;
+}
+
+// ---- IR -> assembly-interpreter records (8 words each) ----------------------
+//
+// w0 handler byte offset | w1 8*dst | w2 8*a | w3 8*b | w4 8*c / funnel index /
+// leaf or probe index | w5 immediate (const / spill byte offset, funnel shift,
+// source width) | w6 width | w7 byte offset of an 8- (SEXT: 16-) word mask
+// entry appended to the constant table.  The record after a heavy op lives in
+// bank A, otherwise banks alternate (asmgen.py: prefetch into the other bank).
+
+struct MaskPool {
+    uint32_t base;                                  // first entry index
+    std::vector<uint32_t> words;
+    std::map<std::vector<uint32_t>, uint32_t> where;
+    uint32_t add(const std::vector<uint32_t>& w) {  // returns a byte offset
+        auto it = where.find(w);
+        if (it != where.end()) return it->second;
+        const uint32_t off = (base + (uint32_t)(words.size() / 8)) * 32u;
+        words.insert(words.end(), w.begin(), w.end());
+        where[w] = off;
+        return off;
+    }
+};
+
+static std::vector<uint32_t> mask_lt(uint32_t w) {     // bits < w
+    std::vector<uint32_t> m(8);
+    for (uint32_t j = 0; j < 8; ++j)
+        m[j] = j < w / 32 ? 0xFFFFFFFFu : (j == w / 32 ? ((1u << (w % 32)) - 1u) : 0u);
+    return m;
+}
+
+static std::vector<uint32_t> mask_ge(uint32_t w) {     // bits >= w
+    std::vector<uint32_t> m = mask_lt(w);
+    for (auto& x : m) x = ~x;
+    return m;
+}
+
+static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
+                      uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
+    pool.base = n_consts;
+    const uint32_t ones = pool.add(mask_lt(256));
+    rec.assign((size_t)(n_ins + 2) * 8, 0);
+    int bank = 0;
+    for (uint32_t pc = 0; pc <= n_ins; ++pc) {
+        uint32_t* r = rec.data() + (size_t)pc * 8;
+        if (pc == n_ins) {          // HALT, then one zeroed record (prefetch pad)
+            r[0] = hoff[MGA_HID(MGA_HALT, 0, bank)];
+            break;
+        }
+        const uint32_t* in = code + 4 * pc;
+        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
+        const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
+                       c = (in[1] >> 24) & 0xFF;
+        uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
+        const uint32_t maskv = (w >= 1 && w < 256) ? MGA_V_MASK : 0;
+        r[1] = 8 * d; r[2] = 8 * a; r[3] = 8 * b; r[4] = 8 * c; r[5] = 0; r[6] = w; r[7] = ones;
+        int aop = MGA_NOP;
+        switch (op) {
+        case MG_NOP: aop = MGA_NOP; break;
+        case MG_CONST: aop = MGA_CONST; r[5] = imm * 32u; break;
+        case MG_LEAF:
+            aop = MGA_LEAF; r[4] = imm; r[7] = pool.add(mask_lt(w)); var |= MGA_V_MASK; break;
+        case MG_SPILL:
+            if (imm < n_lds) { aop = MGA_SPILL_LDS; r[5] = imm * 2u * 256u * 16u; }
+            else { aop = MGA_SPILL_SCR; r[5] = (imm - n_lds) * 32u; }
+            break;
+        case MG_RELOAD:
+            if (imm < n_lds) { aop = MGA_RELOAD_LDS; r[5] = imm * 2u * 256u * 16u; }
+            else { aop = MGA_RELOAD_SCR; r[5] = (imm - n_lds) * 32u; }
+            break;
+        case MG_ADD: aop = MGA_ADD; goto masked;
+        case MG_SUB: aop = MGA_SUB; goto masked;
+        case MG_MUL: aop = MGA_MUL; goto masked;
+        case MG_NEG: aop = MGA_NEG; goto masked;
+        case MG_NOT: aop = MGA_NOT; goto masked;
+        case MG_UDIV: aop = MGA_UDIV; goto masked;
+        case MG_UREM: aop = MGA_UREM; goto masked;
+        case MG_SDIV: aop = MGA_SDIV; goto masked;
+        case MG_SREM: aop = MGA_SREM; goto masked;
+        case MG_SMOD: aop = MGA_SMOD; goto masked;
+        case MG_SHL: aop = MGA_SHL; goto masked;
+        case MG_LSHR: aop = MGA_LSHR; goto masked;
+        case MG_ASHR: aop = MGA_ASHR; goto masked;
+        case MG_SLT: aop = MGA_SLT; goto masked;
+        case MG_SLE: aop = MGA_SLE; goto masked;
+        case MG_UMULNO: aop = MGA_UMULNO;
+        masked:
+            if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
+            break;
+        case MG_AND: aop = MGA_AND; break;
+        case MG_OR: aop = MGA_OR; break;
+        case MG_XOR: aop = MGA_XOR; break;
+        case MG_EQ: aop = MGA_EQ; break;
+        case MG_ULT: aop = MGA_ULT; break;
+        case MG_ULE: aop = MGA_ULE; break;
+        case MG_ITE: aop = MGA_ITE; break;
+        case MG_CONCAT: {           // R = a << imm | b
+            aop = MGA_CONCAT;
+            const uint32_t q = imm >> 5, bs = imm & 31;
+            r[4] = 8 * a + 8 - q - (bs ? 1 : 0);
+            r[5] = bs ? 32 - bs : 0;
+            r[7] = pool.add(mask_ge(imm));
+            break;
+        }
+        case MG_EXTRACT:            // R = (a >> imm) & mask(w)
+            aop = MGA_EXTRACT;
+            r[4] = 8 * a + (imm >> 5) + 8;
+            r[5] = imm & 31;
+            r[7] = pool.add(mask_lt(w));
+            break;
+        case MG_SEXT: {             // from imm bits to w bits: 16-word mask entry
+            aop = MGA_SEXT;
+            r[5] = imm;
+            std::vector<uint32_t> m = mask_lt(imm), m2 = mask_lt(w);
+            m.insert(m.end(), m2.begin(), m2.end());
+            r[7] = pool.add(m);
+            break;
+        }
+        case MG_OUT: aop = MGA_OUT; r[4] = imm; break;
+        case MG_ROOT: aop = MGA_ROOT; break;
+        case MG_MOV: aop = MGA_MOV; break;
+        default: aop = MGA_NOP; break;
+        }
+        r[0] = hoff[MGA_HID(aop, var, bank)];
+        bank = mga_is_heavy(aop) ? 0 : 1 - bank;
+    }
+}
+
 extern "C" {
 
 int mg_version(void) { return MG_VERSION; }
+
+int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32_t n_lds,
+                 const uint32_t* handler_off, uint32_t n_handlers, uint32_t* records,
+                 uint32_t max_record_words, uint32_t* n_record_words, uint32_t* masks,
+                 uint32_t max_mask_words, uint32_t* n_mask_words) {
+    if ((n_ins && !code) || !handler_off || n_handlers != MGA_NUM_HANDLERS || !n_record_words ||
+        !n_mask_words)
+        return MG_E_ARG;
+    // leaf and probe tables are not known here: only their indices' shape
+    int rc = validate(nullptr, code, n_ins, n_consts, nullptr, 0xFFFFFFFFu, MG_MAX_LDS,
+                      MG_MAX_LDS + MG_MAX_PSLOTS, 0xFFFFFFFFu);
+    if (rc) return rc;
+    if (n_lds > MG_MAX_LDS) return MG_E_ARG;
+    std::vector<uint32_t> rec;
+    MaskPool pool;
+    translate(handler_off, code, n_ins, n_consts, n_lds, rec, pool);
+    *n_record_words = (uint32_t)rec.size();
+    *n_mask_words = (uint32_t)pool.words.size();
+    if (rec.size() > max_record_words || pool.words.size() > max_mask_words) return MG_E_ARG;
+    if (records) memcpy(records, rec.data(), rec.size() * 4);
+    if (masks && !pool.words.empty()) memcpy(masks, pool.words.data(), pool.words.size() * 4);
+    return MG_OK;
+}
 
 int mg_config(uint32_t* out, uint32_t n) {
     const uint32_t cfg[4] = {MG_VERSION, MG_NREG, MG_MAX_LDS, MG_MAX_PSLOTS};
@@ -110,6 +315,15 @@ int mg_init(int device, mg_ctx** out) {
         delete ctx;
         return MG_E_HIP;
     }
+    if (const char* k = getenv("MYTHGPU_KERNEL")) ctx->use_asm = strcmp(k, "cxx") != 0;
+    if (const char* l = getenv("MYTHGPU_LDS_SLOTS")) {
+        const long v = strtol(l, nullptr, 10);
+        if (v >= 0 && v <= MG_MAX_LDS) ctx->lds_slots = (uint32_t)v;
+    }
+    if (query_handlers(ctx) != MG_OK) {
+        mg_free(ctx);
+        return MG_E_HIP;
+    }
     *out = ctx;
     return MG_OK;
 }
@@ -137,7 +351,7 @@ static int validate(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, uint32_t 
     if (n_lds > MG_MAX_LDS) return fail(ctx, MG_E_ARG, "too many LDS slots (%u)", n_lds);
     if (n_spill < n_lds || n_spill - n_lds > MG_MAX_PSLOTS)
         return fail(ctx, MG_E_ARG, "spill slots %u (LDS %u)", n_spill, n_lds);
-    for (uint32_t i = 0; i < n_leaves; ++i) {
+    for (uint32_t i = 0; leaves && i < n_leaves; ++i) {
         const mg_leafgen& g = leaves[i];
         if (g.width < 1 || g.width > MG_MAX_WIDTH)
             return fail(ctx, MG_E_ARG, "leaf %u: width %u", i, g.width);
@@ -201,28 +415,49 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
                       n_probes);
     if (rc) return rc;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
-    // 8 zeroed NOPs after the code: the interpreter prefetches up to 8 ahead
-    const size_t code_b = (size_t)(n_ins + 8) * 16, const_b = (size_t)n_consts * 32,
-                 gen_b = (size_t)n_leaves * sizeof(mg_leafgen);
+    // assembly records + translator masks (appended to the constant table)
+    std::vector<uint32_t> rec;
+    MaskPool pool;
+    translate(ctx->hoff, code, n_ins, n_consts, kernel_lds_slots(ctx, n_spill_slots), rec, pool);
+    const uint32_t n_const_all = n_consts + (uint32_t)(pool.words.size() / 8);
+    // device leaf descriptors: byte pool offsets and the per-leaf stream salt
+    std::vector<mg_leafgen_dev> gdev(n_leaves);
+    for (uint32_t i = 0; i < n_leaves; ++i) {
+        const uint64_t salt = (prog_seed * 0xD1B54A32D192ED03ull) ^
+                              ((uint64_t)(i + 1) * 0x8CB92BA72F3D8DD7ull);
+        gdev[i] = {leaves[i].width, leaves[i].pool_off * 32u, leaves[i].pool_n,
+                   leaves[i].pct_uniform, leaves[i].pct_small, leaves[i].pct_boundary,
+                   (uint32_t)salt, (uint32_t)(salt >> 32)};
+    }
+    // 8 zeroed NOPs after the IR code: the C++ interpreter prefetches ahead
+    const size_t code_b = (size_t)(n_ins + 8) * 16, const_b = (size_t)n_const_all * 32,
+                 gen_b = gdev.size() * sizeof(mg_leafgen_dev), rec_b = rec.size() * 4;
     auto align = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t off_const = align(code_b), off_gen = off_const + align(const_b),
-                 off_desc = off_gen + align(gen_b), total = off_desc + align(sizeof(mg_pdesc));
+                 off_desc = off_gen + align(gen_b), off_rec = off_desc + align(sizeof(mg_pdesc)),
+                 total = off_rec + align(rec_b);
     std::vector<uint8_t> blob(total, 0);
     if (n_ins) memcpy(blob.data(), code, (size_t)n_ins * 16);   // + zeroed NOP padding
-    if (const_b) memcpy(blob.data() + off_const, consts, const_b);
-    if (gen_b) memcpy(blob.data() + off_gen, leaves, gen_b);
+    if (n_consts) memcpy(blob.data() + off_const, consts, (size_t)n_consts * 32);
+    if (!pool.words.empty())
+        memcpy(blob.data() + off_const + (size_t)n_consts * 32, pool.words.data(),
+               pool.words.size() * 4);
+    if (gen_b) memcpy(blob.data() + off_gen, gdev.data(), gen_b);
+    memcpy(blob.data() + off_rec, rec.data(), rec_b);
     void* d = nullptr;
     HIPCHECK(ctx, hipMalloc(&d, total));
     uint8_t* db = (uint8_t*)d;
     mg_pdesc desc;
+    memset(&desc, 0, sizeof desc);
     desc.code = (const uint32_t*)db;
     desc.consts = (const uint32_t*)(db + off_const);
-    desc.gen = (const mg_leafgen*)(db + off_gen);
+    desc.gen = (const mg_leafgen_dev*)(db + off_gen);
     desc.n_ins = n_ins;
     desc.n_leaves = n_leaves;
     desc.n_lds = n_lds_slots;
     desc.n_probes = n_probes;
     desc.prog_seed = prog_seed;
+    desc.xcode = (const uint32_t*)(db + off_rec);
     memcpy(blob.data() + off_desc, &desc, sizeof desc);
     hipError_t e = hipMemcpy(d, blob.data(), total, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -278,7 +513,7 @@ int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, uint64
     run.words_per_prog = words;
     if (leaf_b)
         HIPCHECK(ctx, hipMemcpyAsync(base, leaves_soa, leaf_b, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHECK(ctx, mg_launch_interp(0, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
+    HIPCHECK(ctx, launch(ctx, 0, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
     HIPCHECK(ctx, hipMemcpyAsync(root_bits, run.root_bits, root_b, hipMemcpyDeviceToHost,
                                  ctx->stream));
     if (probes && probe_b)
@@ -311,7 +546,7 @@ int mg_eval_gen(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_
     run.seed = gen->seed;
     run.first_index = gen->first_index;
     if (leaf_b) HIPCHECK(ctx, hipMemsetAsync(run.leaves_out, 0, leaf_b, ctx->stream));
-    HIPCHECK(ctx, mg_launch_interp(1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
+    HIPCHECK(ctx, launch(ctx, 1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
     HIPCHECK(ctx, hipMemcpyAsync(root_bits, run.root_bits, root_b, hipMemcpyDeviceToHost,
                                  ctx->stream));
     if (probe_b)
@@ -345,7 +580,7 @@ int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_ca
         run.first_sat = d_first;
         run.seed = gen->seed;
         run.first_index = gen->first_index + done;
-        HIPCHECK(ctx, mg_launch_interp(1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
+        HIPCHECK(ctx, launch(ctx, 1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
         unsigned long long h = ~0ull;
         HIPCHECK(ctx, hipMemcpyAsync(&h, d_first, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -363,7 +598,7 @@ int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_ca
         run.first_index = (uint64_t)*first_sat;
         run.leaves_out = (uint32_t*)((uint8_t*)ws + 256);
         HIPCHECK(ctx, hipMemsetAsync(run.leaves_out, 0, leaf_b, ctx->stream));
-        HIPCHECK(ctx, mg_launch_interp(1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
+        HIPCHECK(ctx, launch(ctx, 1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
         HIPCHECK(ctx, hipMemcpyAsync(witness_leaves, run.leaves_out, leaf_b,
                                      hipMemcpyDeviceToHost, ctx->stream));
         HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -425,7 +660,7 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
         run.first_sat = d_first_sat ? (unsigned long long*)d_first_sat + p0 : nullptr;
         run.seed = seed;
         run.first_index = first_index;
-        HIPCHECK(ctx, mg_launch_interp(1, b->d_descs + p0, np, run, b->max_lds, s));
+        HIPCHECK(ctx, launch(ctx, 1, b->d_descs + p0, np, run, b->max_lds, s));
     }
     return MG_OK;
 }

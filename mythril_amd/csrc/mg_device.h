@@ -6,16 +6,27 @@
 #include <stdint.h>
 #include "mythgpu.h"
 
+/* Device form of a leaf generator descriptor (mg_leafgen + host-computed
+ * fields): 8 words, read by the kernels with one scalar load. */
+struct mg_leafgen_dev {
+    uint32_t width;
+    uint32_t pool_off_b;       /* byte offset of the pool in the const table  */
+    uint32_t pool_n;
+    uint32_t pct_uniform, pct_small, pct_boundary;
+    uint32_t salt_lo, salt_hi; /* prog_seed*C1 ^ (leaf+1)*C2 (oracle/gen_ref) */
+};
+
 /* One loaded program as the kernel sees it (read with scalar loads). */
 struct mg_pdesc {
-    const uint32_t* code;      /* n_ins x 4 words                          */
-    const uint32_t* consts;    /* n_consts x 8 words                       */
-    const mg_leafgen* gen;     /* n_leaves generator descriptors           */
+    const uint32_t* code;      /* n_ins x 4 words (IR)                      */
+    const uint32_t* consts;    /* n_consts x 8 words (+ translator masks)  */
+    const mg_leafgen_dev* gen; /* n_leaves generator descriptors           */
     uint32_t n_ins;
     uint32_t n_leaves;
     uint32_t n_lds;            /* LDS spill slots                          */
     uint32_t n_probes;
     uint64_t prog_seed;        /* per-program stream salt (generator mode) */
+    const uint32_t* xcode;     /* translated 8-word records (mg_interp_asm) */
 };
 
 /* Per-launch arguments (passed by value). */

@@ -30,7 +30,7 @@ typedef uint32_t vfile __attribute__((ext_vector_type(MG_NREG)));
 // constant address space: uniform loads through it become s_load (scalar
 // cache), which keeps opcodes and slot indices in SGPRs
 typedef __attribute__((address_space(4))) const uint32_t cu32;
-typedef __attribute__((address_space(4))) const mg_leafgen cgen;
+typedef __attribute__((address_space(4))) const mg_leafgen_dev cgen;
 
 #define DEV static __device__ __forceinline__
 
@@ -276,13 +276,16 @@ DEV uint64_t sm64(uint64_t& s) {
     return z ^ (z >> 31);
 }
 
-DEV void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t idx,
-                  cgen* g, cu32* consts, uint32_t* out) {
+DEV uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
+// candidate generator, v2 range reduction (multiply-high); mirrored by
+// oracle/gen_ref.py and the assembly interpreter (asmgen._gen_leaf)
+DEV void gen_leaf(uint64_t seed, uint32_t leaf, uint64_t idx, cgen* g, cu32* consts,
+                  uint32_t* out) {
     const uint32_t w = g->width;
-    uint64_t s = seed ^ (prog_seed * 0xD1B54A32D192ED03ull) ^
-                 ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull) ^ (idx * 0x9E3779B97F4A7C15ull);
+    uint64_t s = seed ^ (((uint64_t)g->salt_hi << 32) | g->salt_lo) ^ (idx * 0x9E3779B97F4A7C15ull);
     const uint64_t r0 = sm64(s);
-    const uint32_t cls = (uint32_t)(r0 >> 32) % 100u;
+    const uint32_t cls = mulhi32((uint32_t)(r0 >> 32), 100u);
     const uint32_t lo = (uint32_t)r0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) out[j] = 0;
@@ -292,36 +295,31 @@ DEV void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t idx
         out[0] = (uint32_t)r;
         out[1] = (uint32_t)(r >> 32);
     } else if (cls < g->pct_boundary && cls >= g->pct_small) {
-        const uint32_t kind = lo % 6u;
-        const uint32_t k = (lo >> 8) % w;
-        uint32_t bit = (kind == 2) ? w - 1 : k;
-        if (kind == 1) out[0] = 1;
-        if (kind == 2 || kind == 4 || kind == 5) {
+        const uint32_t kind = mulhi32(lo, 6u);
+        const uint32_t k = mulhi32(lo * 0x9E3779B1u, w);
+        const uint32_t bit = (kind == 2) ? w - 1 : (kind == 1 ? 0u : k);
+        if (kind != 0 && kind != 3) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) out[j] = (bit >> 5) == (uint32_t)j ? (1u << (bit & 31)) : 0u;
         }
-        if (kind == 3) {
+        uint32_t add[8];
+        const uint32_t up = (kind == 3 || kind == 5) ? 0xFFFFFFFFu : 0u;
+        add[0] = kind == 4 ? 1u : up;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) out[j] = 0xFFFFFFFFu;
-        }
-        if (kind == 4) {        // 2^k + 1 (k == 0 -> 2)
-            uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-            add256(out, one, out);
-        }
-        if (kind == 5) {        // 2^k - 1
-            uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-            sub256(out, one, out);
-        }
+        for (int j = 1; j < 8; ++j) add[j] = up;
+        add256(out, add, out);
     } else if (cls >= g->pct_boundary && pool_n > 0) {
-        const uint32_t e = (lo >> 3) % pool_n;
-        const uint32_t delta = (uint32_t)(r0 >> 16) % 3u;
-        cu32* p = consts + (size_t)(g->pool_off + e) * 8;
+        const uint32_t e = mulhi32(lo, pool_n);
+        const uint32_t delta = mulhi32(lo * 0x85EBCA6Bu, 3u);
+        cu32* p = consts + (size_t)g->pool_off_b / 4 + (size_t)e * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) out[j] = p[j];
-        uint32_t one[8] = {1, 0, 0, 0, 0, 0, 0, 0};
-        if (delta == 0) sub256(out, one, out);
-        if (delta == 2) add256(out, one, out);
-    } else {                    // uniform (also the pool fallback)
+        uint32_t add[8];
+        add[0] = delta - 1u;
+#pragma unroll
+        for (int j = 1; j < 8; ++j) add[j] = delta == 0 ? 0xFFFFFFFFu : 0u;
+        add256(out, add, out);
+    } else {                    // uniform (also the pool class without a pool)
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {
             const uint64_t r = sm64(s);
@@ -410,8 +408,8 @@ __global__ __launch_bounds__(BLOCK, MG_WAVES_PER_SIMD) void mg_interp(const mg_p
         }
         case MG_LEAF: {
             if (GEN) {
-                gen_leaf(run.seed, D->prog_seed, imm0, run.first_index + lane_idx,
-                         (cgen*)D->gen + imm0, consts, r);
+                gen_leaf(run.seed, imm0, run.first_index + lane_idx, (cgen*)D->gen + imm0,
+                         consts, r);
                 if (run.leaves_out && active) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j)

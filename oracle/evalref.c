@@ -422,6 +422,8 @@ static void eval_dag(const dag_t* g, const V* leaves, V* vals) {
 
 /* ---- device candidate generator (port of gen_leaf / oracle/gen_ref.py) ---- */
 
+static uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+
 static uint64_t sm64(uint64_t* s) {
     *s += 0x9E3779B97F4A7C15ull;
     uint64_t z = *s;
@@ -435,12 +437,13 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
     uint64_t s = seed ^ (prog_seed * 0xD1B54A32D192ED03ull) ^
                  ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull) ^ (idx * 0x9E3779B97F4A7C15ull);
     uint64_t r0 = sm64(&s);
-    uint32_t cls = (uint32_t)(r0 >> 32) % 100u, lo = (uint32_t)r0;
+    /* v2 range reduction: multiply-high (Lemire) instead of modulo */
+    uint32_t cls = mulhi32((uint32_t)(r0 >> 32), 100u), lo = (uint32_t)r0;
     vzero(out);
     if (cls >= pct[0] && cls < pct[1]) {
         out->w[0] = sm64(&s);
     } else if (cls >= pct[1] && cls < pct[2]) {
-        uint32_t kind = lo % 6u, k = (lo >> 8) % w;
+        uint32_t kind = mulhi32(lo, 6u), k = mulhi32(lo * 0x9E3779B1u, w);
         if (kind == 1) out->w[0] = 1;
         if (kind == 2) out->w[(w - 1) / 64] = 1ull << ((w - 1) % 64);
         if (kind == 3) for (int i = 0; i < 4; ++i) out->w[i] = ~0ull;
@@ -454,7 +457,7 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
             else vsub(&p, &one, out);
         }
     } else if (cls >= pct[2] && pool_n > 0) {
-        uint32_t e = (lo >> 3) % pool_n, delta = (uint32_t)(r0 >> 16) % 3u;
+        uint32_t e = mulhi32(lo, pool_n), delta = mulhi32(lo * 0x85EBCA6Bu, 3u);
         V one, p;
         vzero(&one);
         one.w[0] = 1;

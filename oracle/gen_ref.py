@@ -1,12 +1,16 @@
 """ORACLE — test infrastructure only.
 
-Host restatement of the device candidate generator (``gen_leaf`` in
-``mythril_amd/csrc/mg_kernels.hip``; contract in ``include/mythgpu.h``
+Host restatement of the device candidate generator (``_gen_leaf`` in
+``mythril_amd/asmgen.py``, ``gen_leaf`` in ``mythril_amd/csrc/mg_kernels.hip``; contract in ``include/mythgpu.h``
 ``mg_leafgen``), so tests can rebuild the exact assignment a GPU lane
 evaluated and check the lane against ``oracle/smtlib_ref.py``.
 """
 
 M64 = (1 << 64) - 1
+
+
+def _mulhi(a, b):
+    return (a * b) >> 32
 
 
 def _sm64(s):
@@ -22,20 +26,21 @@ def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
     s = (seed ^ ((prog_seed * 0xD1B54A32D192ED03) & M64) ^
          (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64) ^ ((idx * 0x9E3779B97F4A7C15) & M64)) & M64
     s, r0 = _sm64(s)
-    cls = (r0 >> 32) % 100
+    # v2 range reduction: multiply-high (Lemire), no modulo
+    cls = _mulhi(r0 >> 32, 100)
     lo = r0 & 0xFFFFFFFF
     mask = (1 << width) - 1
     if pct[0] <= cls < pct[1]:
         s, r = _sm64(s)
         v = r
     elif pct[1] <= cls < pct[2]:
-        kind = lo % 6
-        k = (lo >> 8) % width
+        kind = _mulhi(lo, 6)
+        k = _mulhi((lo * 0x9E3779B1) & 0xFFFFFFFF, width)
         v = {0: 0, 1: 1, 2: 1 << (width - 1), 3: (1 << 256) - 1,
              4: (1 << k) + 1, 5: (1 << k) - 1}[kind]
     elif cls >= pct[2] and len(pool) > 0:
-        e = (lo >> 3) % len(pool)
-        delta = ((r0 >> 16) & 0xFFFFFFFF) % 3
+        e = _mulhi(lo, len(pool))
+        delta = _mulhi((lo * 0x85EBCA6B) & 0xFFFFFFFF, 3)
         v = (pool[e] + delta - 1) % (1 << 256)
     else:
         v = 0

@@ -1,0 +1,129 @@
+"""CPU parity of the hand-written gfx950 assembly interpreter (the product's
+hot kernel) through an instruction-level simulator of its exact text
+(tests/asm_sim.py) and the library's own IR -> record translator
+(mg_translate, host-only).  Every probed node and root bit is compared with
+the oracle (oracle/smtlib_ref.py, oracle/gen_ref.py); the same cases run on
+the MI355X in test_gpu_parity.py."""
+
+import random
+
+import numpy as np
+import pytest
+
+import asm_sim
+import dag_cases
+from evm_mini import lower_program
+from mythril_amd import asmgen
+from mythril_amd.assign import Assignment as PA, pack, unpack
+from mythril_amd.corpus import make_dag
+from mythril_amd.engine import default_leafgen, limbs_to_int
+from mythril_amd.ir import compile_constraints
+from mythril_amd.smt import node as N
+from oracle import gen_ref
+from oracle import smtlib_ref as R
+from test_gpu_parity import flat_expected
+from test_oracle_golden import load, oracle_eval
+
+CASES = dag_cases.named_cases()
+SEED = 0x6D797468
+
+
+def test_handler_table_is_complete():
+    _, table = asm_sim.body_and_table()
+    assert len(table) == asmgen.NUM_HANDLERS
+    assert len(set(table)) == len(table) and min(table) > 0
+
+
+def test_generated_text_has_no_scalar_stores():
+    text = "\n".join(asmgen.generate())
+    for bad in ("s_store", "s_buffer_store", "s_scratch_store", "s_dcache", "s_atomic"):
+        assert bad not in text
+
+
+def _probe_check(prog, probes, asgs, pr, root, constraints):
+    for a, asg in enumerate(asgs):
+        want = flat_expected(probes, R.evaluate(list(probes), asg))
+        got = [limbs_to_int(pr[k, :, a]) for k in range(prog.n_probes)]
+        assert got == want, (a, [(i, hex(g), hex(w)) for i, (g, w) in
+                                 enumerate(zip(got, want)) if g != w][:4])
+        assert bool(root[a]) == bool(R.eval_constraints(constraints, asg)), a
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_case_parity_sim(name):
+    constraints, probes, gen, tables = CASES[name]
+    prog = compile_constraints(constraints, probes, table_sizes=tables)
+    rng = random.Random(2000 + len(name))
+    asgs = [gen(rng) for _ in range(64)]
+    soa = pack(prog, [PA(a.vars, a.arrays, a.funcs) for a in asgs])
+    root, pr, _, _ = asm_sim.simulate(prog, soa)
+    _probe_check(prog, probes, asgs, pr, root, constraints)
+
+
+def test_division_edges_with_reciprocal_noise():
+    """Every division operator on edge values, with v_rcp_f64 perturbed by
+    up to 1e-7 relative (the integer correction must absorb it)."""
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    probes = [N.bv_op(op, x, y) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    prog = compile_constraints([], probes)
+    rng = random.Random(3)
+    edges = [0, 1, 2, 3, (1 << 31), (1 << 32) - 1, 1 << 32, (1 << 64) - 1, 1 << 255,
+             (1 << 256) - 1, (1 << 255) - 1, (1 << 128) + 1, 0xFFFFFFFF00000000]
+    for rep in range(3):
+        asgs = [PA(vars={"x": rng.choice(edges + [rng.getrandbits(rng.choice((32, 64, 200, 256)))]),
+                         "y": rng.choice(edges + [rng.getrandbits(rng.choice((31, 33, 64, 130, 256)))])})
+                for _ in range(64)]
+        root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs), rcp_noise=1e-7)
+        for a, asg in enumerate(asgs):
+            want = R.evaluate(probes, R.Assignment(asg.vars))
+            got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+            assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
+
+
+@pytest.mark.parametrize("dag_id,n_lds", [(0, 6), (1, 0), (7, 2), (33, 6)])
+def test_corpus_constraints_as_probes_generated(dag_id, n_lds):
+    """A corpus DAG with every constraint probed (so each lane checks ~half
+    true bits), candidates from the device generator, spills split between
+    LDS and scratch as n_lds says."""
+    roots, _ = make_dag(dag_id, SEED)
+    prog = compile_constraints([], roots)
+    lg = default_leafgen(prog)
+    first = 777 * dag_id
+    _, pr, lout, _ = asm_sim.simulate(prog, gen=(SEED, dag_id, first, lg), n_lds=n_lds,
+                                      want_leaves=True)
+    pool = prog.const_values
+    for lane in range(64):
+        lv = [gen_ref.gen_leaf(SEED, dag_id, li, first + lane, l.width, pool)
+              for li, l in enumerate(prog.leaves)]
+        assert [limbs_to_int(lout[li, :, lane]) for li in range(len(prog.leaves))] == lv
+        asg = unpack(prog, lout[:, :, lane])
+        want = R.evaluate(list(roots), R.Assignment(asg.vars, asg.arrays, asg.funcs))
+        got = [int(pr[k, 0, lane]) for k in range(len(roots))]
+        assert got == [int(w) for w in want], lane
+
+
+def test_vmtests_sim():
+    checked = 0
+    for t in load("vmtests.json")[::3]:
+        vars_, stores, divergent = lower_program(t["code"], oracle_eval)
+        if divergent or not stores:
+            continue
+        probes = [v.raw for _, v in stores] + [k.raw for k, _ in stores]
+        prog = compile_constraints([], probes)
+        _, pr, _, _ = asm_sim.simulate(prog, pack(prog, [PA(vars=vars_)] * 64))
+        n = len(stores)
+        storage = {limbs_to_int(pr[n + i, :, 0]): limbs_to_int(pr[i, :, 0]) for i in range(n)}
+        storage = {k: v for k, v in storage.items() if v}
+        assert storage == {int(k, 16): int(v, 16) for k, v in t["storage"].items()}, t["name"]
+        checked += 1
+    assert checked >= 40
+
+
+def test_inactive_lanes_do_not_store():
+    x = N.bv_var("x", 256)
+    prog = compile_constraints([], [N.bv_op("bvadd", x, x)])
+    asgs = [PA(vars={"x": i + 1}) for i in range(64)]
+    active = (1 << 40) - 1
+    _, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs), active=active)
+    for a in range(64):
+        assert limbs_to_int(pr[0, :, a]) == (2 * (a + 1) if a < 40 else 0)
