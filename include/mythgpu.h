@@ -113,6 +113,9 @@ int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
 
 /* Library/ABI version (no GPU needed). */
 int mg_version(void);
+/* Digest of the generated gfx950 assembly the library was built from (no
+ * GPU needed; mythril_amd/asmgen.py digest()). */
+const char* mg_asm_digest(void);
 /* Host-only (no GPU): translate a validated IR program into the 8-word
  * records of the assembly interpreter, given its handler offset table
  * (mg_load_program does this with the table queried from the device).

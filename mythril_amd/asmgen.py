@@ -701,6 +701,7 @@ def _gen_leaf(a: Asm, bank: int):
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
 
 
+
 def h_leaf(a, bank, root, mask):
     prologue(a, bank)
     load_masks(a, fld(bank, F_MOFF))
@@ -1256,13 +1257,21 @@ def clobbers() -> List[str]:
     return vs + ss + ['"vcc"', '"scc"', '"memory"']
 
 
+def digest(lines: Optional[List[str]] = None) -> str:
+    """Short hash of the generated assembly (embedded in the library, so a
+    stale build is detected: engine.load_library, tests/test_abi.py)."""
+    import hashlib
+    return hashlib.sha256("\n".join(lines or generate()).encode()).hexdigest()[:16]
+
+
 def write_outputs(csrc: str) -> None:
     lines = generate()
     body = " \\\n".join('"%s\\n"' % l.replace('"', '\\"') for l in lines)
     inc = ("// GENERATED by mythril_amd/asmgen.py -- do not edit.\n"
            "// Inline-asm body of mg_interp_asm (gfx950), %d lines.\n"
            "#define MG_ASM_BODY \\\n%s\n\n"
-           "#define MG_ASM_CLOBBERS %s\n") % (len(lines), body, ", ".join(clobbers()))
+           "#define MG_ASM_CLOBBERS %s\n"
+           "#define MG_ASM_DIGEST \"%s\"\n") % (len(lines), body, ", ".join(clobbers()), digest(lines))
     _write_if_changed(os.path.join(csrc, "mg_interp_gfx950.inc"), inc)
     hdr = ["// GENERATED by mythril_amd/asmgen.py -- do not edit.",
            "#ifndef MG_ASM_HANDLERS_H", "#define MG_ASM_HANDLERS_H",

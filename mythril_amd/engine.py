@@ -22,7 +22,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
            "mg_batch_free", "mg_batch_eval_gen", "mg_keccak256", "mg_version", "mg_config",
-           "mg_translate")
+           "mg_translate", "mg_asm_digest")
 
 
 class EngineUnavailable(RuntimeError):
@@ -77,10 +77,18 @@ def load_library(path: str = _LIB_PATH):
         lib.mg_batch_eval_gen.argtypes = [p, p, u64, u64, u64, p, p, p]
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
         lib.mg_config.argtypes = [p, u32]
+        lib.mg_asm_digest.restype = C.c_char_p
         pu32 = C.POINTER(u32)
         lib.mg_translate.argtypes = [p, u32, u32, u32, p, u32, p, u32, pu32, p, u32, pu32]
         for name in EXPORTS:
             getattr(lib, name)
+        from . import asmgen
+        want = asmgen.digest()
+        got = lib.mg_asm_digest().decode()
+        if got != want:
+            raise EngineUnavailable("%s was built from a different assembly interpreter "
+                                    "(digest %s, generator %s); rebuild with "
+                                    "`python -m mythril_amd.build`" % (path, got, want))
         _libs[path] = lib
         return lib
 

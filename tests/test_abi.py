@@ -16,6 +16,11 @@ def declared():
     return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mg_\w+)\s*\(", text, re.M)))
 
 
+def test_library_built_from_current_generator():
+    from mythril_amd import asmgen
+    assert load_library().mg_asm_digest().decode() == asmgen.digest()
+
+
 def test_library_exports_every_declared_symbol():
     lib = load_library()
     names = declared()
