@@ -68,8 +68,32 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "NOT", "SHL", "LSHR", "ASHR", "EQ", "ULT", "ULE", "SLT", "SLE", "UMULNO", "ITE",
         "CONCAT", "EXTRACT", "SEXT", "NEG", "OUT", "ROOT", "MOV"]
 AOP = {n: i for i, n in enumerate(AOPS)}
-V_ROOT, V_MASK = 1, 2
-NVAR = 4
+V_ROOT, V_MASK, V_DC, V_W32 = 1, 2, 4, 8
+NVAR = 16
+# variant bits each handler family implements (the query maps the others to
+# the nearest implemented handler): DC = destination's upper limbs are known
+# zero (write limb 0 only), W32 = operands and result fit one limb
+_RM = V_ROOT | V_MASK
+SUPPORT = {n: _RM for n in AOPS}
+SUPPORT.update({n: _RM | V_DC | V_W32 for n in ("ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG",
+                                               "ITE", "EQ", "ULT", "ULE", "EXTRACT", "MOV",
+                                               "CONST")})
+SUPPORT.update({n: _RM | V_DC for n in ("SLT", "SLE")})
+# families whose result is never masked (canonical inputs give canonical
+# outputs) and families where DC only matters for one-limb results
+NO_MASK = {"AND", "OR", "XOR", "EQ", "ULT", "ULE", "ITE", "MOV", "CONST", "NOP", "HALT",
+           "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", "RELOAD_SCR", "OUT", "ROOT", "CONCAT",
+           "EXTRACT"}
+DC_NEEDS_W32 = {"ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "ITE", "EXTRACT", "MOV", "CONST"}
+
+
+def canon_var(name: str, var: int) -> int:
+    var &= SUPPORT[name]
+    if name in NO_MASK:
+        var &= ~V_MASK
+    if name in DC_NEEDS_W32 and not var & V_W32:
+        var &= ~V_DC
+    return var
 
 
 def hid(aop: int, variant: int, bank: int) -> int:
@@ -77,6 +101,13 @@ def hid(aop: int, variant: int, bank: int) -> int:
 
 
 NUM_HANDLERS = len(AOPS) * NVAR * 2
+
+
+def canonical(h: int) -> int:
+    """The implemented handler a handler id maps to (unsupported variant
+    bits dropped)."""
+    bank, var, aop = h % 2, (h // 2) % NVAR, h // (2 * NVAR)
+    return hid(aop, canon_var(AOPS[aop], var), bank)
 
 
 def v(n: int) -> str:
@@ -188,6 +219,40 @@ def finish(a: Asm, bank: int, res: List[int], root: bool, mask: bool):
     dispatch(a, 1 - bank)
 
 
+def write_narrow(a: Asm, bank: int, r0: str, dc: bool):
+    """F[D] = (r0, 0, ..., 0); with dc the upper limbs are already zero."""
+    a.idx_on(fld(bank, F_D), "DST")
+    a("v_mov_b32 %s, %s" % (v(F[0]), r0))
+    if not dc:
+        for j in range(1, 8):
+            a("v_mov_b32 %s, 0" % v(F[j]))
+    a.idx_off()
+
+
+def finish_narrow(a: Asm, bank: int, root: bool, mask: bool, dc: bool):
+    """R0 (one limb) -> F[D], masked to W bits if requested, ROOT, dispatch."""
+    if mask:
+        a("s_waitcnt lgkmcnt(0)")
+        a("v_and_b32 %s, %s, %s" % (v(R[0]), s(S_M), v(R[0])))
+    write_narrow(a, bank, v(R[0]), dc)
+    if root:
+        a.root_and(v(R[0]))
+    dispatch(a, 1 - bank)
+
+
+def narrow_binop(a: Asm, bank: int, root: bool, mask: bool, dc: bool, opname: str):
+    """R0 = op(F[a].limb0, F[b].limb0) for values of at most 32 bits."""
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.idx_on(fld(bank, F_B), "SRC0")
+    a("v_mov_b32 %s, %s" % (v(Y[0]), v(F[0])))
+    a("s_set_gpr_idx_idx %s" % s(fld(bank, F_A)))
+    a("%s %s, %s, %s" % (opname, v(R[0]), v(F[0]), v(Y[0])))
+    a.idx_off()
+    finish_narrow(a, bank, root, mask, dc)
+
+
 def sext(a: Asm, regs: List[int], wsgpr: int, masks: int, tmp: int, st: int):
     """Sign-extend regs (canonical at the width in s[wsgpr]) to 256 bits in
     place.  masks: 8 SGPRs with the bits < width; st: 2 scratch SGPRs.
@@ -215,20 +280,26 @@ def or_reduce(a: Asm, regs: List[int], out: int):
 # cheap handlers (a, bank, root, mask)
 # ---------------------------------------------------------------------------
 
-def h_nop(a, bank, root, mask):
+def h_nop(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     dispatch(a, 1 - bank)
 
 
-def h_halt(a, bank, root, mask):
+def h_halt(a, bank, root, mask, dc=False, w32=False):
     a("s_waitcnt lgkmcnt(0)")
     a("s_branch .Lexit_%=")
 
 
-def h_const(a, bank, root, mask):
+def h_const(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     load_masks(a, fld(bank, F_IMM))                # the constant itself
     a("s_waitcnt lgkmcnt(0)")
+    if w32:
+        write_narrow(a, bank, s(S_M), dc)
+        if root:
+            a.root_and(s(S_M))
+        dispatch(a, 1 - bank)
+        return
     a.idx_on(fld(bank, F_D), "DST")
     for j in range(8):
         a("v_mov_b32 %s, %s" % (v(F[j]), s(S_M + j)))
@@ -249,7 +320,9 @@ def _binop(a, bank, root, mask, emit):
     finish(a, bank, R, root, mask)
 
 
-def h_add(a, bank, root, mask):
+def h_add(a, bank, root, mask, dc=False, w32=False):
+    if w32:
+        return narrow_binop(a, bank, root, mask, dc, "v_add_u32")
     def emit():
         a("v_add_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(F[0]), v(Y[0])))
         for j in range(1, 8):
@@ -257,7 +330,9 @@ def h_add(a, bank, root, mask):
     _binop(a, bank, root, mask, emit)
 
 
-def h_sub(a, bank, root, mask):
+def h_sub(a, bank, root, mask, dc=False, w32=False):
+    if w32:
+        return narrow_binop(a, bank, root, mask, dc, "v_sub_u32")
     def emit():
         a("v_sub_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(F[0]), v(Y[0])))
         for j in range(1, 8):
@@ -266,7 +341,9 @@ def h_sub(a, bank, root, mask):
 
 
 def _logic(opname):
-    def h(a, bank, root, mask):
+    def h(a, bank, root, mask, dc=False, w32=False):
+        if w32:
+            return narrow_binop(a, bank, root, False, dc, opname)
         def emit():
             for j in range(8):
                 a("%s %s, %s, %s" % (opname, v(R[j]), v(F[j]), v(Y[j])))
@@ -279,10 +356,15 @@ h_or = _logic("v_or_b32")
 h_xor = _logic("v_xor_b32")
 
 
-def h_not(a, bank, root, mask):
+def h_not(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
+    if w32:
+        a.idx_on(fld(bank, F_A), "SRC0")
+        a("v_not_b32 %s, %s" % (v(R[0]), v(F[0])))
+        a.idx_off()
+        return finish_narrow(a, bank, root, mask, dc)
     a.idx_on(fld(bank, F_A), "SRC0")
     for j in range(8):
         a("v_not_b32 %s, %s" % (v(R[j]), v(F[j])))
@@ -290,10 +372,15 @@ def h_not(a, bank, root, mask):
     finish(a, bank, R, root, mask)
 
 
-def h_neg(a, bank, root, mask):
+def h_neg(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
+    if w32:
+        a.idx_on(fld(bank, F_A), "SRC1")
+        a("v_sub_u32 %s, 0, %s" % (v(R[0]), v(F[0])))
+        a.idx_off()
+        return finish_narrow(a, bank, root, mask, dc)
     a.idx_on(fld(bank, F_A), "SRC1")
     a("v_sub_co_u32 %s, vcc, 0, %s" % (v(R[0]), v(F[0])))
     for j in range(1, 8):
@@ -302,13 +389,18 @@ def h_neg(a, bank, root, mask):
     finish(a, bank, R, root, mask)
 
 
-def h_mov(a, bank, root, mask):
+def h_mov(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
+    if w32:
+        a.idx_on(fld(bank, F_A), "SRC0")
+        a("v_mov_b32 %s, %s" % (v(R[0]), v(F[0])))
+        a.idx_off()
+        return finish_narrow(a, bank, root, False, dc)
     a.read_slot(R, fld(bank, F_A))
     finish(a, bank, R, root, False)
 
 
-def h_root(a, bank, root, mask):
+def h_root(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     a.idx_on(fld(bank, F_A), "SRC0")
     a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
@@ -316,20 +408,29 @@ def h_root(a, bank, root, mask):
     dispatch(a, 1 - bank)
 
 
-def _bool_result(a, bank, root, true_if_vcc=True):
+def _bool_result(a, bank, root, true_if_vcc=True, dc=False):
     a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[0]), "0" if true_if_vcc else "1",
                                          "1" if true_if_vcc else "0"))
-    a.idx_on(fld(bank, F_D), "DST")
-    a("v_mov_b32 %s, %s" % (v(F[0]), v(R[0])))
-    for j in range(1, 8):
-        a("v_mov_b32 %s, 0" % v(F[j]))
-    a.idx_off()
+    write_narrow(a, bank, v(R[0]), dc)
     if root:
         a.root_and(v(R[0]))
     dispatch(a, 1 - bank)
 
 
-def h_eq(a, bank, root, mask):
+def _narrow_cmp(a, bank, root, dc, cmp):
+    """Bool = cmp(F[a].limb0, F[b].limb0) for operands of at most 32 bits."""
+    prologue(a, bank)
+    a.idx_on(fld(bank, F_B), "SRC0")
+    a("v_mov_b32 %s, %s" % (v(Y[0]), v(F[0])))
+    a("s_set_gpr_idx_idx %s" % s(fld(bank, F_A)))
+    a("%s vcc, %s, %s" % (cmp, v(F[0]), v(Y[0])))
+    a.idx_off()
+    _bool_result(a, bank, root, dc=dc)
+
+
+def h_eq(a, bank, root, mask, dc=False, w32=False):
+    if w32:
+        return _narrow_cmp(a, bank, root, dc, "v_cmp_eq_u32")
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_B))
     a.idx_on(fld(bank, F_A), "SRC0")
@@ -338,7 +439,7 @@ def h_eq(a, bank, root, mask):
     a.idx_off()
     or_reduce(a, Y, T[0])
     a("v_cmp_eq_u32 vcc, 0, %s" % v(T[0]))
-    _bool_result(a, bank, root)
+    _bool_result(a, bank, root, dc=dc)
 
 
 def _borrow(a, bank, lhs_field, rhs_field):
@@ -351,19 +452,23 @@ def _borrow(a, bank, lhs_field, rhs_field):
     a.idx_off()
 
 
-def h_ult(a, bank, root, mask):
+def h_ult(a, bank, root, mask, dc=False, w32=False):
+    if w32:
+        return _narrow_cmp(a, bank, root, dc, "v_cmp_lt_u32")
     prologue(a, bank)
     _borrow(a, bank, F_A, F_B)
-    _bool_result(a, bank, root)
+    _bool_result(a, bank, root, dc=dc)
 
 
-def h_ule(a, bank, root, mask):
+def h_ule(a, bank, root, mask, dc=False, w32=False):
+    if w32:
+        return _narrow_cmp(a, bank, root, dc, "v_cmp_le_u32")
     prologue(a, bank)
     _borrow(a, bank, F_B, F_A)            # b < a  ->  not (a <= b)
-    _bool_result(a, bank, root, true_if_vcc=False)
+    _bool_result(a, bank, root, true_if_vcc=False, dc=dc)
 
 
-def _scmp(a, bank, root, mask, le: bool):
+def _scmp(a, bank, root, mask, le: bool, dc: bool = False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
@@ -379,23 +484,31 @@ def _scmp(a, bank, root, mask, le: bool):
     a("v_sub_co_u32 %s, vcc, %s, %s" % (v(T[0]), v(lhs[0]), v(rhs[0])))
     for j in range(1, 8):
         a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(T[0]), v(lhs[j]), v(rhs[j])))
-    _bool_result(a, bank, root, true_if_vcc=not le)
+    _bool_result(a, bank, root, true_if_vcc=not le, dc=dc)
 
 
-def h_slt(a, bank, root, mask):
-    _scmp(a, bank, root, mask, False)
+def h_slt(a, bank, root, mask, dc=False, w32=False):
+    _scmp(a, bank, root, mask, False, dc)
 
 
-def h_sle(a, bank, root, mask):
-    _scmp(a, bank, root, mask, True)
+def h_sle(a, bank, root, mask, dc=False, w32=False):
+    _scmp(a, bank, root, mask, True, dc)
 
 
-def h_ite(a, bank, root, mask):
+def h_ite(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     a.idx_on(fld(bank, F_C), "SRC0")
     a("v_and_b32_e64 %s, %s, 1" % (v(T[0]), v(F[0])))
     a.idx_off()
     a("v_cmp_ne_u32 vcc, 0, %s" % v(T[0]))
+    if w32:
+        a.idx_on(fld(bank, F_B), "SRC0")
+        a("v_mov_b32 %s, %s" % (v(Y[0]), v(F[0])))
+        a("s_set_gpr_idx_idx %s" % s(fld(bank, F_A)))
+        a("s_set_gpr_idx_mode gpr_idx(SRC1)")
+        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[0]), v(Y[0]), v(F[0])))
+        a.idx_off()
+        return finish_narrow(a, bank, root, False, dc)
     a.read_slot(Y, fld(bank, F_B))
     a.idx_on(fld(bank, F_A), "SRC1")
     for j in range(8):
@@ -404,10 +517,15 @@ def h_ite(a, bank, root, mask):
     finish(a, bank, R, root, False)
 
 
-def h_extract(a, bank, root, mask):
+def h_extract(a, bank, root, mask, dc=False, w32=False):
     """R = (F[a] >> lo) & mask(W).  C = 8a + (lo >> 5) + 8, IMM = lo & 31."""
     prologue(a, bank)
     load_masks(a, fld(bank, F_MOFF))
+    if w32:
+        a.idx_on(fld(bank, F_C), "SRC0,SRC1")
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(R[0]), v(G[1]), v(G[0]), s(fld(bank, F_IMM))))
+        a.idx_off()
+        return finish_narrow(a, bank, root, True, dc)
     a.idx_on(fld(bank, F_C), "SRC0,SRC1")
     for j in range(8):
         a("v_alignbit_b32 %s, %s, %s, %s" % (v(R[j]), v(G[j + 1]), v(G[j]), s(fld(bank, F_IMM))))
@@ -415,7 +533,7 @@ def h_extract(a, bank, root, mask):
     finish(a, bank, R, root, True)
 
 
-def h_concat(a, bank, root, mask):
+def h_concat(a, bank, root, mask, dc=False, w32=False):
     """R = F[a] << sb | F[b] (sb = width of b).  C = funnel index, IMM =
     funnel shift; MOFF -> 8 masks of the bits >= sb."""
     prologue(a, bank)
@@ -431,7 +549,7 @@ def h_concat(a, bank, root, mask):
     finish(a, bank, R, root, False)
 
 
-def h_sext(a, bank, root, mask):
+def h_sext(a, bank, root, mask, dc=False, w32=False):
     """sign_extend from IMM bits to W bits.  MOFF -> 16 masks: bits < IMM,
     then bits < W."""
     prologue(a, bank)
@@ -447,7 +565,7 @@ def h_sext(a, bank, root, mask):
     dispatch(a, 1 - bank)
 
 
-def h_spill_lds(a, bank, root, mask):
+def h_spill_lds(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_A))
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
@@ -456,7 +574,7 @@ def h_spill_lds(a, bank, root, mask):
     dispatch(a, 1 - bank)
 
 
-def h_reload_lds(a, bank, root, mask):
+def h_reload_lds(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
     a("ds_read_b128 v[%d:%d], %s" % (R[0], R[3], v(T[0])))
@@ -465,7 +583,7 @@ def h_reload_lds(a, bank, root, mask):
     finish(a, bank, R, root, False)
 
 
-def h_spill_scr(a, bank, root, mask):
+def h_spill_scr(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_A))
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
@@ -474,7 +592,7 @@ def h_spill_scr(a, bank, root, mask):
     dispatch(a, 1 - bank)
 
 
-def h_reload_scr(a, bank, root, mask):
+def h_reload_scr(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
     a("scratch_load_dwordx4 v[%d:%d], off, %s" % (R[0], R[3], s(S_T)))
@@ -520,7 +638,7 @@ def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int):
     a.label(skip)
 
 
-def h_out(a, bank, root, mask):
+def h_out(a, bank, root, mask, dc=False, w32=False):
     """probe[C] = F[a] (active lanes, when a probe buffer is bound)."""
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_A))
@@ -535,70 +653,84 @@ def h_out(a, bank, root, mask):
 GOLD = 0x9E3779B97F4A7C15
 
 
+GOLD = 0x9E3779B97F4A7C15
+MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+# SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
+K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_X, S_X + 6)
+
+
+def load_sm64_consts(a: Asm):
+    for reg, val in ((K_GOLD_LO, GOLD), (K_GOLD_HI, GOLD >> 32), (K_M1_LO, MIX1),
+                     (K_M1_HI, MIX1 >> 32), (K_M2_LO, MIX2), (K_M2_HI, MIX2 >> 32)):
+        a("s_mov_b32 %s, 0x%x" % (s(reg), val & 0xFFFFFFFF))
+
+
+def mul64_const(a: Asm, z: List[int], klo: int, khi: int, t: List[int]):
+    """z *= K (mod 2^64), K in SGPRs; t: aligned pair t[0]:t[1] + t[2]."""
+    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(t[0]), sp(S_T + 6), v(z[1]), s(klo)))   # hi*klo
+    a("v_mov_b32 %s, %s" % (v(t[2]), v(t[0])))
+    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(t[0]), sp(S_T + 6), v(z[0]), s(khi)))   # lo*khi
+    a("v_add_u32 %s, %s, %s" % (v(t[2]), v(t[2]), v(t[0])))
+    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(z[0]), sp(S_T + 6), v(z[0]), s(klo)))   # lo*klo
+    a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[2])))
+
+
 def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
-    """SplitMix64 step on the per-lane state st=(lo,hi): st += GOLD;
-    z = mix(st).  t: 4 temps.  Uses vcc and s[S_T+6:S_T+7]."""
-    a("v_mov_b32 %s, 0x%x" % (v(t[0]), GOLD & 0xFFFFFFFF))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), v(t[0]), v(st[0])))
-    a("v_mov_b32 %s, 0x%x" % (v(t[0]), GOLD >> 32))
-    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[0]), v(st[1])))
-    a("v_mov_b32 %s, %s" % (v(z[0]), v(st[0])))
-    a("v_mov_b32 %s, %s" % (v(z[1]), v(st[1])))
-    for shift, mult in ((30, 0xBF58476D1CE4E5B9), (27, 0x94D049BB133111EB)):
-        a("v_lshrrev_b64 %s, %d, %s" % (vp(t[0]), shift, vp(z[0])))
-        a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
-        a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
-        a("v_mov_b32 %s, 0x%x" % (v(t[2]), mult & 0xFFFFFFFF))
-        a("v_mov_b32 %s, 0x%x" % (v(t[3]), mult >> 32))
-        a("v_mul_lo_u32 %s, %s, %s" % (v(t[1]), v(z[0]), v(t[3])))
-        a("v_mul_lo_u32 %s, %s, %s" % (v(t[3]), v(z[1]), v(t[2])))
-        a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(z[0]), sp(S_T + 6), v(z[0]), v(t[2])))
-        a("v_add3_u32 %s, %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1]), v(t[3])))
+    """SplitMix64 on the per-lane state st = (lo, hi): st += GOLD; z =
+    mix(st).  Constants in SGPRs (load_sm64_consts); t: 4 temps with
+    t[0]:t[1] aligned.  Full-rate v_mad_u64_u32 for every product.
+    Uses vcc and s[S_T+6:S_T+7]."""
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(K_GOLD_LO), v(st[0])))
+    a("v_mov_b32 %s, %s" % (v(t[3]), s(K_GOLD_HI)))
+    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[3]), v(st[1])))
+    a("v_lshrrev_b64 %s, 30, %s" % (vp(t[0]), vp(st[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(st[0]), v(t[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(st[1]), v(t[1])))
+    mul64_const(a, z, K_M1_LO, K_M1_HI, t)
+    a("v_lshrrev_b64 %s, 27, %s" % (vp(t[0]), vp(z[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
+    mul64_const(a, z, K_M2_LO, K_M2_HI, t)
     a("v_lshrrev_b64 %s, 31, %s" % (vp(t[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
     a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
 
 
-def _class_exec(a: Asm, lo_sgpr: Optional[int], hi_sgpr: Optional[int], cls: int, extra=None):
-    """exec = saved & (lo <= cls < hi) [& extra] (compares run on all lanes:
-    VALU compares write 0 for lanes outside exec)."""
-    a("s_mov_b64 exec, %s" % sp(S_T + 4))
-    m = sp(S_T)
-    if lo_sgpr is not None:
-        a("v_cmp_le_u32_e64 %s, %s, %s" % (m, s(lo_sgpr), v(cls)))
+def _class_mask(a: Asm, out: int, lo_sgpr: Optional[int], hi_sgpr: Optional[int], cls: int):
+    """s[out:out+1] = lanes with lo <= cls < hi (all lanes active)."""
+    if lo_sgpr is not None and hi_sgpr is not None:
+        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(out), s(lo_sgpr), v(cls)))
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_T), s(hi_sgpr), v(cls)))
+        a("s_and_b64 %s, %s, %s" % (sp(out), sp(out), sp(S_T)))
+    elif lo_sgpr is not None:
+        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(out), s(lo_sgpr), v(cls)))
     else:
-        a("s_mov_b64 %s, -1" % m)
-    if hi_sgpr is not None:
-        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_T + 2), s(hi_sgpr), v(cls)))
-        a("s_and_b64 %s, %s, %s" % (m, m, sp(S_T + 2)))
-    if extra:
-        extra()
-    a("s_and_b64 exec, %s, %s" % (m, sp(S_T + 4)))
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(out), s(hi_sgpr), v(cls)))
 
 
 def _gen_leaf(a: Asm, bank: int):
     """X[0..7] <- generator value of leaf C for candidate first + lane.
-    Mirrors oracle/gen_ref.py gen_leaf.  Device descriptor (8 words at
-    gen + 32*leaf): width, pool_off (x32 bytes: byte offset), pool_n,
-    pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
+    Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's four SplitMix64
+    words are computed for every lane (the small class is its first word);
+    the boundary and pool classes then overwrite their lanes under exec.
+    Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
+    pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
     st, z, tt = [T[0], T[1]], [T[2], T[3]], [T[4], T[5], T[6], T[7]]
     cls, lo = T[8], T[9]
     g = S_CUR
     a("s_load_dwordx2 %s, %s, 0x10" % (sp(S_T), IN["desc"]))       # gen table
     a("s_lshl_b32 %s, %s, 5" % (s(S_T + 2), s(fld(bank, F_C))))
+    load_sm64_consts(a)
     a("s_waitcnt lgkmcnt(0)")
     a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
     # idx = first + lane ; st = seed ^ salt ^ idx * GOLD
-    a("s_mov_b64 %s, %s" % (sp(S_T), IN["first"]))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(T[10]), s(S_T), OP_LANE_LO))
-    a("v_mov_b32 %s, %s" % (v(T[11]), s(S_T + 1)))
+    a("s_mov_b64 %s, %s" % (sp(S_T + 4), IN["first"]))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(T[10]), s(S_T + 4), OP_LANE_LO))
+    a("v_mov_b32 %s, %s" % (v(T[11]), s(S_T + 5)))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(T[11]), v(T[11]), OP_LANE_HI))
-    a("v_mov_b32 %s, 0x%x" % (v(tt[0]), GOLD & 0xFFFFFFFF))
-    a("v_mov_b32 %s, 0x%x" % (v(tt[1]), GOLD >> 32))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(tt[2]), v(T[10]), v(tt[1])))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(tt[3]), v(T[11]), v(tt[0])))
-    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(st[0]), sp(S_T + 6), v(T[10]), v(tt[0])))
-    a("v_add3_u32 %s, %s, %s, %s" % (v(st[1]), v(st[1]), v(tt[2]), v(tt[3])))
+    a("v_mov_b32 %s, %s" % (v(st[0]), v(T[10])))
+    a("v_mov_b32 %s, %s" % (v(st[1]), v(T[11])))
+    mul64_const(a, st, K_GOLD_LO, K_GOLD_HI, tt)
     a("s_waitcnt lgkmcnt(0)")
     a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(g + 6)))
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), v(st[0])))
@@ -607,19 +739,16 @@ def _gen_leaf(a: Asm, bank: int):
     a("v_mov_b32 %s, 100" % v(tt[0]))
     a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), v(tt[0])))
     a("v_mov_b32 %s, %s" % (v(lo), v(z[0])))
-    for j in range(8):
-        a("v_mov_b32 %s, 0" % v(X[j]))
+    # ---- uniform words for every lane; small lanes keep the first 64 bits
+    for j in range(0, 8, 2):
+        sm64(a, st, [X[j], X[j + 1]], tt)
+    _class_mask(a, S_T + 2, g + 3, g + 4, cls)                       # small
+    for j in range(2, 8):
+        a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(X[j]), v(X[j]), sp(S_T + 2)))
     a("s_mov_b64 %s, exec" % sp(S_T + 4))
-    # ---- small: pct_uniform <= cls < pct_small -> one sm64 (64 bits) -------
-    _class_exec(a, g + 3, g + 4, cls)
-    lab = a.uniq("gsm")
-    a("s_cbranch_execz %s" % lab)
-    a("v_mov_b32 %s, %s" % (v(T[10]), v(st[0])))
-    a("v_mov_b32 %s, %s" % (v(T[11]), v(st[1])))
-    sm64(a, [T[10], T[11]], [X[0], X[1]], tt)
-    a.label(lab)
-    # ---- boundary: pct_small <= cls < pct_boundary ------------------------
-    _class_exec(a, g + 4, g + 5, cls)
+    # ---- boundary: pct_small <= cls < pct_boundary -------------------------
+    _class_mask(a, S_T + 2, g + 4, g + 5, cls)
+    a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     lab = a.uniq("gbd")
     a("s_cbranch_execz %s" % lab)
     kind, k, bit, hi = tt
@@ -658,11 +787,11 @@ def _gen_leaf(a: Asm, bank: int):
         a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(X[j]), v(X[j]), v(hi)))
     a.label(lab)
     # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
-    def need_pool():
-        a("s_cmp_lg_u32 %s, 0" % s(g + 2))
-        a("s_cselect_b64 %s, -1, 0" % sp(S_T + 2))
-        a("s_and_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
-    _class_exec(a, g + 5, None, cls, need_pool)
+    a("s_mov_b64 exec, %s" % sp(S_T + 4))
+    _class_mask(a, S_T + 2, g + 5, None, cls)
+    a("s_cmp_lg_u32 %s, 0" % s(g + 2))
+    a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(S_T + 2)))
+    a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     lab = a.uniq("gpl")
     a("s_cbranch_execz %s" % lab)
     e, delta, t2, hi = tt
@@ -677,34 +806,19 @@ def _gen_leaf(a: Asm, bank: int):
     a("v_mul_hi_u32 %s, %s, %s" % (v(delta), v(delta), v(t2)))
     a("v_cmp_eq_u32 vcc, 0, %s" % v(delta))
     a("v_cndmask_b32 %s, 0, -1, vcc" % v(hi))
-    a("v_add_u32 %s, -1, %s" % (v(e), v(delta)))
+    a("v_add_u32 %s, -1, %s" % (v(t2), v(delta)))
     a("s_waitcnt vmcnt(0)")
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(X[0]), v(X[0]), v(e)))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(X[0]), v(X[0]), v(t2)))
     for j in range(1, 8):
         a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(X[j]), v(X[j]), v(hi)))
     a.label(lab)
-    # ---- uniform: cls < pct_uniform, or the pool class without a pool ------
-    def uni():
-        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T + 2), s(g + 5), v(cls)))
-        a("s_cmp_eq_u32 %s, 0" % s(g + 2))
-        a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(S_T + 2)))
-        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_T), s(g + 3), v(cls)))
-        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
-    a("s_mov_b64 exec, %s" % sp(S_T + 4))
-    uni()
-    a("s_and_b64 exec, %s, %s" % (sp(S_T), sp(S_T + 4)))
-    lab = a.uniq("gun")
-    a("s_cbranch_execz %s" % lab)
-    for j in range(0, 8, 2):
-        sm64(a, st, [X[j], X[j + 1]], tt)
-    a.label(lab)
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
 
 
-
-def h_leaf(a, bank, root, mask):
+def h_leaf(a, bank, root, mask, dc=False, w32=False):
     prologue(a, bank)
-    load_masks(a, fld(bank, F_MOFF))
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
     lab_gen, lab_done = a.uniq("lgen"), a.uniq("ldone")
     a("s_bitcmp1_b32 %s, 0" % IN["mode"])
     a("s_cbranch_scc1 %s" % lab_gen)
@@ -718,12 +832,13 @@ def h_leaf(a, bank, root, mask):
     a("s_branch %s" % lab_done)
     a.label(lab_gen)
     _gen_leaf(a, bank)
-    a("s_waitcnt lgkmcnt(0)")
-    for j in range(8):
-        a("v_and_b32 %s, %s, %s" % (v(X[j]), s(S_M + j), v(X[j])))
+    if mask:
+        a("s_waitcnt lgkmcnt(0)")
+        for j in range(8):
+            a("v_and_b32 %s, %s, %s" % (v(X[j]), s(S_M + j), v(X[j])))
     _store_soa(a, X, IN["lout"], fld(bank, F_C))
     a.label(lab_done)
-    finish(a, bank, X, root, True)
+    finish(a, bank, X, root, mask)
 
 
 # ---------------------------------------------------------------------------
@@ -1016,60 +1131,75 @@ def udivrem(a: Asm, want_rem: bool):
 
 
 def _div_digit(a: Asm, un, vn, j, d, d6, dinv):
+    """One quotient digit of Knuth D for every lane (see udivrem).
+    Registers: A = T4:T5, P = T6:T7 (64-bit pairs), CR/RH = T8:T9, QH = T11."""
     u2, u1, u0 = un[j + 8], un[j + 7], un[j + 6]
     A0, A1, P0, P1, CR, RH, QH = T[4], T[5], T[6], T[7], T[8], T[9], T[11]
     RL = A1
     st = S_T
-    lt = sp(st)                  # lanes with u2 < d
-    # qq = dinv * a2 + (a2:u1), a2 = u2 < d ? u2 : 0
+    lt = sp(st)                  # lanes with u2 < d (all but the u2 == d case)
+    # 2-by-1 quotient via the reciprocal: qq = dinv * a2 + (a2:u1), a2 = u2 < d ? u2 : 0
     a("v_cmp_lt_u32_e64 %s, %s, %s" % (lt, v(u2), v(d)))
     a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(A1), v(u2), lt))
     a("v_mov_b32 %s, %s" % (v(A0), v(u1)))
     a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (A0, A1, sp(st + 6), v(dinv), v(A1), A0, A1))
     a("v_add_u32 %s, 1, %s" % (v(QH), v(A1)))                       # q1 (A0 = q0)
-    a("v_mul_lo_u32 %s, %s, %s" % (v(CR), v(QH), v(d)))
-    a("v_sub_u32 %s, %s, %s" % (v(CR), v(u1), v(CR)))                # r
-    a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(A0)))   # r > q0
+    a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(d)))
+    a("v_sub_u32 %s, %s, %s" % (v(CR), v(u1), v(P0)))                # r = u1 - q1*d
+    a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(A0)))   # r > q0: q1--, r += d
     a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
     a("v_sub_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
     a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
     a("v_add_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
-    a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(d)))     # r >= d
+    a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(d)))     # r >= d: q1++, r -= d
     a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
     a("v_add_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
     a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
     a("v_sub_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
-    # u2 >= d (u2 == d): qhat = b-1, rhat = u1 + d (65 bits)
+    # rhat (65 bits) = r; lanes with u2 == d: qhat = b-1, rhat = u1 + d
+    a("v_mov_b32 %s, %s" % (v(RL), v(CR)))
+    a("v_mov_b32 %s, 0" % v(RH))
+    lab_nb = a.uniq("dnb")
+    a("s_cmp_eq_u64 %s, -1" % lt)
+    a("s_cbranch_scc1 %s" % lab_nb)
     a("v_cndmask_b32_e64 %s, -1, %s, %s" % (v(QH), v(QH), lt))
     a("v_add_co_u32 %s, vcc, %s, %s" % (v(P0), v(u1), v(d)))
     a("v_cndmask_b32 %s, 0, 1, vcc" % v(P1))
-    a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(RL), v(P0), v(CR), lt))
+    a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(RL), v(P0), v(RL), lt))
     a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(RH), v(P1), lt))
-    # Knuth's test (twice): rh < 2^32 and qh*d6 > rh*2^32 + u0 -> qh--, rh += d
-    for _ in range(2):
+    a.label(lab_nb)
+    # Knuth's test: rh < 2^32 and qh*d6 > rh*2^32 + u0 -> qh--, rh += d; a
+    # second round only if some lane of the wave corrected in the first
+    lab_k = a.uniq("dk")
+    for rnd in range(2):
         a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(d6)))
         a("v_mov_b32 %s, %s" % (v(A0), v(u0)))                      # (A0, A1) = u0 : rh_lo
         a("v_cmp_gt_u64_e64 %s, v[%d:%d], v[%d:%d]" % (sp(st + 2), P0, P1, A0, A1))
         a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(st + 4), v(RH)))
         a("s_and_b64 %s, %s, %s" % (sp(st + 2), sp(st + 2), sp(st + 4)))
+        a("s_cbranch_scc0 %s" % lab_k)                              # no lane to fix
         a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
         a("v_sub_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
-        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
-        a("v_add_co_u32 %s, vcc, %s, %s" % (v(RL), v(RL), v(P0)))
-        a("v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(RH), v(RH)))
-    # multiply-subtract un[j..j+8] -= qh * vn
+        if rnd == 0:
+            a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
+            a("v_add_co_u32 %s, vcc, %s, %s" % (v(RL), v(RL), v(P0)))
+            a("v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(RH), v(RH)))
+    a.label(lab_k)
+    # multiply-subtract un[j..j+8] -= qh * vn as one borrow chain in vcc:
+    # P = qh * vn[i] + carry (carry pair CR:RH with RH = 0), un[j+i] -= P.lo
     a("v_mov_b32 %s, 0" % v(CR))
-    a("s_mov_b64 %s, 0" % sp(st + 4))
+    a("v_mov_b32 %s, 0" % v(RH))
     for i in range(8):
-        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(vn[i])))
-        a("v_add_co_u32 %s, vcc, %s, %s" % (v(P0), v(P0), v(CR)))
-        a("v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(CR), v(P1)))
-        a("v_sub_co_u32 %s, %s, %s, %s" % (v(un[j + i]), sp(st + 2), v(un[j + i]), v(P0)))
-        a("v_subb_co_u32 %s, vcc, %s, 0, %s" % (v(un[j + i]), v(un[j + i]), sp(st + 4)))
-        a("s_or_b64 %s, %s, vcc" % (sp(st + 4), sp(st + 2)))
-    a("v_sub_co_u32 %s, %s, %s, %s" % (v(u2), sp(st + 2), v(u2), v(CR)))
-    a("v_subb_co_u32 %s, vcc, %s, 0, %s" % (v(u2), v(u2), sp(st + 4)))
-    a("s_or_b64 %s, %s, vcc" % (sp(st + 4), sp(st + 2)))
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (P0, P1, sp(st + 6), v(QH), v(vn[i]), CR, RH))
+        a("v_mov_b32 %s, %s" % (v(CR), v(P1)))
+        if i == 0:
+            a("v_sub_co_u32 %s, vcc, %s, %s" % (v(un[j]), v(un[j]), v(P0)))
+        else:
+            a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
+    a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(u2), v(u2), v(CR)))
+    # borrow lanes went negative: quotient digit qh - 1 and add vn back (rare)
+    a("s_mov_b64 %s, vcc" % sp(st + 4))
+    a("v_subb_co_u32 %s, vcc, %s, 0, vcc" % (v(u2), v(QH)))       # digit into the dead top
     lab = a.uniq("dab")
     a("s_cmp_eq_u64 %s, 0" % sp(st + 4))
     a("s_cbranch_scc1 %s" % lab)
@@ -1080,8 +1210,6 @@ def _div_digit(a: Asm, un, vn, j, d, d6, dinv):
         a("v_and_b32 %s, %s, %s" % (v(P0), v(vn[i]), v(P1)))
         a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
     a.label(lab)
-    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 4)))
-    a("v_sub_u32 %s, %s, %s" % (v(u2), v(QH), v(P0)))
 
 
 def _cond_neg(a: Asm, regs: List[int], m: int):
@@ -1224,18 +1352,21 @@ def generate() -> List[str]:
         if h and h % 512 == 0:
             a("s_add_u32 %s, %s, 2048" % (s(S_T), s(S_T)))
             a("s_addc_u32 %s, %s, 0" % (s(S_T + 1), s(S_T + 1)))
-        a("v_mov_b32 %s, (.Lh%d_%%= - .Lbase_%%=)" % (v(T[1]), h))
+        a("v_mov_b32 %s, (.Lh%d_%%= - .Lbase_%%=)" % (v(T[1]), canonical(h)))
         a("global_store_dword %s, %s, %s offset:%d" % (v(T[0]), v(T[1]), sp(S_T), 4 * (h % 512)))
     a("s_waitcnt vmcnt(0)")
     a("s_branch .Lexit_%=")
     for name in AOPS:
         aop = AOP[name]
         for var in range(NVAR):
+            if canon_var(name, var) != var:
+                continue
             root_v, mask_v = bool(var & V_ROOT), bool(var & V_MASK)
+            dc_v, w32_v = bool(var & V_DC), bool(var & V_W32)
             for bank in (0, 1):
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
                 if name in CHEAP:
-                    CHEAP[name](a, bank, root_v, mask_v)
+                    CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v)
                 else:
                     bits = var | (DIV_CODE.get(name, 0) << 4)
                     heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
@@ -1278,6 +1409,7 @@ def write_outputs(csrc: str) -> None:
            "#define MGA_NUM_HANDLERS %d" % NUM_HANDLERS,
            "#define MGA_NVAR %d" % NVAR,
            "#define MGA_V_ROOT %d" % V_ROOT, "#define MGA_V_MASK %d" % V_MASK,
+           "#define MGA_V_DC %d" % V_DC, "#define MGA_V_W32 %d" % V_W32,
            "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
            "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,
            "enum mga_op {"]

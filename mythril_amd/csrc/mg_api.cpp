@@ -169,11 +169,32 @@ static std::vector<uint32_t> mask_ge(uint32_t w) {     // bits >= w
     return m;
 }
 
+static bool is_compare(uint32_t op) {
+    return op == MG_EQ || op == MG_ULT || op == MG_ULE || op == MG_SLT || op == MG_SLE ||
+           op == MG_UMULNO;
+}
+
+// ops with a one-limb (W32) handler when operands and result fit 32 bits
+static bool has_w32(uint32_t op) {
+    switch (op) {
+    case MG_ADD: case MG_SUB: case MG_AND: case MG_OR: case MG_XOR: case MG_NOT: case MG_NEG:
+    case MG_ITE: case MG_EQ: case MG_ULT: case MG_ULE: case MG_EXTRACT: case MG_MOV:
+    case MG_CONST:
+        return true;
+    default:
+        return false;
+    }
+}
+
 static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
                       uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
     pool.base = n_consts;
     const uint32_t ones = pool.add(mask_lt(256));
     rec.assign((size_t)(n_ins + 2) * 8, 0);
+    // clean[s]: limbs 1..7 of slot s are known to be zero (its last value had
+    // at most 32 bits); registers start uninitialised
+    bool clean[MG_NREG];
+    for (int k = 0; k < MG_NREG; ++k) clean[k] = false;
     int bank = 0;
     for (uint32_t pc = 0; pc <= n_ins; ++pc) {
         uint32_t* r = rec.data() + (size_t)pc * 8;
@@ -186,14 +207,22 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
                        c = (in[1] >> 24) & 0xFF;
         uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
-        const uint32_t maskv = (w >= 1 && w < 256) ? MGA_V_MASK : 0;
+        const bool writes = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
+        // result fits one limb: Bool results, or values of at most 32 bits
+        const bool narrow = is_compare(op) || (writes && w <= 32);
+        const bool w32 = has_w32(op) && w <= 32;       // compares: w = operand width
+        if (w32) var |= MGA_V_W32;
+        if (writes && narrow && clean[d]) var |= MGA_V_DC;
+        const uint32_t maskv = w32 ? (w < 32 ? MGA_V_MASK : 0) : ((w >= 1 && w < 256) ? MGA_V_MASK : 0);
         r[1] = 8 * d; r[2] = 8 * a; r[3] = 8 * b; r[4] = 8 * c; r[5] = 0; r[6] = w; r[7] = ones;
         int aop = MGA_NOP;
         switch (op) {
         case MG_NOP: aop = MGA_NOP; break;
         case MG_CONST: aop = MGA_CONST; r[5] = imm * 32u; break;
         case MG_LEAF:
-            aop = MGA_LEAF; r[4] = imm; r[7] = pool.add(mask_lt(w)); var |= MGA_V_MASK; break;
+            aop = MGA_LEAF; r[4] = imm;
+            if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
+            break;
         case MG_SPILL:
             if (imm < n_lds) { aop = MGA_SPILL_LDS; r[5] = imm * 2u * 256u * 16u; }
             else { aop = MGA_SPILL_SCR; r[5] = (imm - n_lds) * 32u; }
@@ -256,6 +285,7 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         default: aop = MGA_NOP; break;
         }
         r[0] = hoff[MGA_HID(aop, var, bank)];
+        if (writes) clean[d] = narrow;
         bank = mga_is_heavy(aop) ? 0 : 1 - bank;
     }
 }

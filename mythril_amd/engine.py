@@ -47,7 +47,7 @@ _libs: Dict[str, object] = {}
 _lib_lock = threading.Lock()
 
 
-def load_library(path: str = _LIB_PATH):
+def load_library(path: str = _LIB_PATH, check_digest: bool = True):
     """Load libmythgpu.so (no GPU needed) and declare every export.  Other
     paths (A/B builds of the same ABI) load side by side."""
     with _lib_lock:
@@ -83,13 +83,14 @@ def load_library(path: str = _LIB_PATH):
         for name in EXPORTS:
             getattr(lib, name)
         from . import asmgen
-        want = asmgen.digest()
+        want = asmgen.digest() if check_digest else None
         got = lib.mg_asm_digest().decode()
-        if got != want:
+        if check_digest and got != want:
             raise EngineUnavailable("%s was built from a different assembly interpreter "
                                     "(digest %s, generator %s); rebuild with "
                                     "`python -m mythril_amd.build`" % (path, got, want))
-        _libs[path] = lib
+        if check_digest:
+            _libs[path] = lib
         return lib
 
 

@@ -416,6 +416,12 @@ class Wave:
         self.idx_mode = set(re.search(r"gpr_idx\(([^)]*)\)", a[1]).group(1).split(","))
         self.idx_on = True
 
+    def i_s_set_gpr_idx_idx(self, a, pc):
+        self.m0 = (self.m0 & ~0xFF) | (self.sread(a[0]) & 0xFF)
+
+    def i_s_set_gpr_idx_mode(self, a, pc):
+        self.idx_mode = set(re.search(r"gpr_idx\(([^)]*)\)", a[0]).group(1).split(","))
+
     def i_s_set_gpr_idx_off(self, a, pc):
         self.idx_on = False
 
@@ -762,7 +768,7 @@ def translate(prog, n_lds: int):
     import ctypes as C
     from mythril_amd.asmgen import NUM_HANDLERS
     from mythril_amd.engine import load_library
-    lib = load_library()
+    lib = load_library(check_digest=False)     # host-only translator
     _, table = body_and_table()
     code = np.ascontiguousarray(prog.code, dtype=np.uint32)
     tab = np.array(table, dtype=np.uint32)

@@ -30,8 +30,11 @@ SEED = 0x6D797468
 
 def test_handler_table_is_complete():
     _, table = asm_sim.body_and_table()
-    assert len(table) == asmgen.NUM_HANDLERS
-    assert len(set(table)) == len(table) and min(table) > 0
+    assert len(table) == asmgen.NUM_HANDLERS and min(table) > 0
+    canon = {asmgen.canonical(h) for h in range(asmgen.NUM_HANDLERS)}
+    assert len(set(table)) == len(canon)          # one body per implemented variant
+    for h in range(asmgen.NUM_HANDLERS):
+        assert table[h] == table[asmgen.canonical(h)]
 
 
 def test_generated_text_has_no_scalar_stores():
