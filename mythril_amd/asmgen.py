@@ -66,10 +66,12 @@ F_OFF, F_D, F_A, F_B, F_C, F_IMM, F_W, F_MOFF = range(8)
 AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", "RELOAD_SCR",
         "ADD", "SUB", "MUL", "UDIV", "UREM", "SDIV", "SREM", "SMOD", "AND", "OR", "XOR",
         "NOT", "SHL", "LSHR", "ASHR", "EQ", "ULT", "ULE", "SLT", "SLE", "UMULNO", "ITE",
-        "CONCAT", "EXTRACT", "SEXT", "NEG", "OUT", "ROOT", "MOV"]
+        "CONCAT", "EXTRACT", "SEXT", "NEG", "OUT", "ROOT", "MOV",
+        "SUBR",     # b - a   (SUB with the operands swapped: in place on a)
+        "ITEN"]     # c ? b : a (ITE with the operands swapped: in place on a)
 AOP = {n: i for i, n in enumerate(AOPS)}
-V_ROOT, V_MASK, V_DC, V_W32 = 1, 2, 4, 8
-NVAR = 16
+V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
+NVAR = 32
 # variant bits each handler family implements (the query maps the others to
 # the nearest implemented handler): DC = destination's upper limbs are known
 # zero (write limb 0 only), W32 = operands and result fit one limb
@@ -79,9 +81,14 @@ SUPPORT.update({n: _RM | V_DC | V_W32 for n in ("ADD", "SUB", "AND", "OR", "XOR"
                                                "ITE", "EQ", "ULT", "ULE", "EXTRACT", "MOV",
                                                "CONST")})
 SUPPORT.update({n: _RM | V_DC for n in ("SLT", "SLE")})
+# IP = the destination is operand a's slot: the ALU op writes the file in place
+SUPPORT.update({n: SUPPORT[n] | V_IP for n in ("ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG",
+                                               "ITE")})
+SUPPORT["SUBR"] = _RM | V_IP
+SUPPORT["ITEN"] = V_ROOT | V_IP
 # families whose result is never masked (canonical inputs give canonical
 # outputs) and families where DC only matters for one-limb results
-NO_MASK = {"AND", "OR", "XOR", "EQ", "ULT", "ULE", "ITE", "MOV", "CONST", "NOP", "HALT",
+NO_MASK = {"AND", "OR", "XOR", "EQ", "ULT", "ULE", "ITE", "ITEN", "MOV", "CONST", "NOP", "HALT",
            "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", "RELOAD_SCR", "OUT", "ROOT", "CONCAT",
            "EXTRACT"}
 DC_NEEDS_W32 = {"ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "ITE", "EXTRACT", "MOV", "CONST"}
@@ -93,6 +100,8 @@ def canon_var(name: str, var: int) -> int:
         var &= ~V_MASK
     if name in DC_NEEDS_W32 and not var & V_W32:
         var &= ~V_DC
+    if var & V_W32:
+        var &= ~V_IP                 # one limb: nothing to save
     return var
 
 
@@ -280,17 +289,17 @@ def or_reduce(a: Asm, regs: List[int], out: int):
 # cheap handlers (a, bank, root, mask)
 # ---------------------------------------------------------------------------
 
-def h_nop(a, bank, root, mask, dc=False, w32=False):
+def h_nop(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     dispatch(a, 1 - bank)
 
 
-def h_halt(a, bank, root, mask, dc=False, w32=False):
+def h_halt(a, bank, root, mask, dc=False, w32=False, ip=False):
     a("s_waitcnt lgkmcnt(0)")
     a("s_branch .Lexit_%=")
 
 
-def h_const(a, bank, root, mask, dc=False, w32=False):
+def h_const(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     load_masks(a, fld(bank, F_IMM))                # the constant itself
     a("s_waitcnt lgkmcnt(0)")
@@ -320,7 +329,35 @@ def _binop(a, bank, root, mask, emit):
     finish(a, bank, R, root, mask)
 
 
-def h_add(a, bank, root, mask, dc=False, w32=False):
+def inplace_op(a: Asm, bank: int, root: bool, mask: bool, mode: str, emit):
+    """F[a] = op(F[a], Y) in place (dest == a): Y <- F[b]; one pass with
+    the file both read and written through GPR indexing (mode: which
+    source position reads F[a]); mask and ROOT applied afterwards."""
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), mode + ",DST")
+    emit()
+    if mask:
+        a("s_waitcnt lgkmcnt(0)")
+        a("s_set_gpr_idx_mode gpr_idx(SRC0,DST)")
+        for j in range(8):
+            a("v_and_b32_e64 %s, %s, %s" % (v(F[j]), v(F[j]), s(S_M + j)))
+    if root:
+        a("s_set_gpr_idx_mode gpr_idx(SRC0)")
+        a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+    a.idx_off()
+    dispatch(a, 1 - bank)
+
+
+def h_add(a, bank, root, mask, dc=False, w32=False, ip=False):
+    if ip:
+        def emit():
+            a("v_add_co_u32 %s, vcc, %s, %s" % (v(F[0]), v(F[0]), v(Y[0])))
+            for j in range(1, 8):
+                a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(F[j]), v(F[j]), v(Y[j])))
+        return inplace_op(a, bank, root, mask, "SRC0", emit)
     if w32:
         return narrow_binop(a, bank, root, mask, dc, "v_add_u32")
     def emit():
@@ -330,7 +367,13 @@ def h_add(a, bank, root, mask, dc=False, w32=False):
     _binop(a, bank, root, mask, emit)
 
 
-def h_sub(a, bank, root, mask, dc=False, w32=False):
+def h_sub(a, bank, root, mask, dc=False, w32=False, ip=False):
+    if ip:
+        def emit():
+            a("v_sub_co_u32 %s, vcc, %s, %s" % (v(F[0]), v(F[0]), v(Y[0])))
+            for j in range(1, 8):
+                a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(F[j]), v(F[j]), v(Y[j])))
+        return inplace_op(a, bank, root, mask, "SRC0", emit)
     if w32:
         return narrow_binop(a, bank, root, mask, dc, "v_sub_u32")
     def emit():
@@ -341,9 +384,14 @@ def h_sub(a, bank, root, mask, dc=False, w32=False):
 
 
 def _logic(opname):
-    def h(a, bank, root, mask, dc=False, w32=False):
+    def h(a, bank, root, mask, dc=False, w32=False, ip=False):
         if w32:
             return narrow_binop(a, bank, root, False, dc, opname)
+        if ip:
+            def emit():
+                for j in range(8):
+                    a("%s %s, %s, %s" % (opname, v(F[j]), v(F[j]), v(Y[j])))
+            return inplace_op(a, bank, root, False, "SRC0", emit)
         def emit():
             for j in range(8):
                 a("%s %s, %s, %s" % (opname, v(R[j]), v(F[j]), v(Y[j])))
@@ -356,10 +404,25 @@ h_or = _logic("v_or_b32")
 h_xor = _logic("v_xor_b32")
 
 
-def h_not(a, bank, root, mask, dc=False, w32=False):
+def h_not(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
+    if ip:
+        a.idx_on(fld(bank, F_A), "SRC0,DST")
+        if mask:
+            a("s_waitcnt lgkmcnt(0)")
+            for j in range(8):
+                a("v_not_b32 %s, %s" % (v(F[j]), v(F[j])))
+                a("v_and_b32_e64 %s, %s, %s" % (v(F[j]), v(F[j]), s(S_M + j)))
+        else:
+            for j in range(8):
+                a("v_not_b32 %s, %s" % (v(F[j]), v(F[j])))
+        if root:
+            a("s_set_gpr_idx_mode gpr_idx(SRC0)")
+            a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+        a.idx_off()
+        return dispatch(a, 1 - bank)
     if w32:
         a.idx_on(fld(bank, F_A), "SRC0")
         a("v_not_b32 %s, %s" % (v(R[0]), v(F[0])))
@@ -372,10 +435,25 @@ def h_not(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, mask)
 
 
-def h_neg(a, bank, root, mask, dc=False, w32=False):
+def h_neg(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
+    if ip:
+        a.idx_on(fld(bank, F_A), "SRC1,DST")
+        a("v_sub_co_u32 %s, vcc, 0, %s" % (v(F[0]), v(F[0])))
+        for j in range(1, 8):
+            a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(F[j]), v(F[j])))
+        if mask:
+            a("s_waitcnt lgkmcnt(0)")
+            a("s_set_gpr_idx_mode gpr_idx(SRC0,DST)")
+            for j in range(8):
+                a("v_and_b32_e64 %s, %s, %s" % (v(F[j]), v(F[j]), s(S_M + j)))
+        if root:
+            a("s_set_gpr_idx_mode gpr_idx(SRC0)")
+            a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+        a.idx_off()
+        return dispatch(a, 1 - bank)
     if w32:
         a.idx_on(fld(bank, F_A), "SRC1")
         a("v_sub_u32 %s, 0, %s" % (v(R[0]), v(F[0])))
@@ -389,7 +467,7 @@ def h_neg(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, mask)
 
 
-def h_mov(a, bank, root, mask, dc=False, w32=False):
+def h_mov(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     if w32:
         a.idx_on(fld(bank, F_A), "SRC0")
@@ -400,7 +478,7 @@ def h_mov(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, False)
 
 
-def h_root(a, bank, root, mask, dc=False, w32=False):
+def h_root(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a.idx_on(fld(bank, F_A), "SRC0")
     a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
@@ -428,7 +506,7 @@ def _narrow_cmp(a, bank, root, dc, cmp):
     _bool_result(a, bank, root, dc=dc)
 
 
-def h_eq(a, bank, root, mask, dc=False, w32=False):
+def h_eq(a, bank, root, mask, dc=False, w32=False, ip=False):
     if w32:
         return _narrow_cmp(a, bank, root, dc, "v_cmp_eq_u32")
     prologue(a, bank)
@@ -452,7 +530,7 @@ def _borrow(a, bank, lhs_field, rhs_field):
     a.idx_off()
 
 
-def h_ult(a, bank, root, mask, dc=False, w32=False):
+def h_ult(a, bank, root, mask, dc=False, w32=False, ip=False):
     if w32:
         return _narrow_cmp(a, bank, root, dc, "v_cmp_lt_u32")
     prologue(a, bank)
@@ -460,7 +538,7 @@ def h_ult(a, bank, root, mask, dc=False, w32=False):
     _bool_result(a, bank, root, dc=dc)
 
 
-def h_ule(a, bank, root, mask, dc=False, w32=False):
+def h_ule(a, bank, root, mask, dc=False, w32=False, ip=False):
     if w32:
         return _narrow_cmp(a, bank, root, dc, "v_cmp_le_u32")
     prologue(a, bank)
@@ -487,15 +565,74 @@ def _scmp(a, bank, root, mask, le: bool, dc: bool = False):
     _bool_result(a, bank, root, true_if_vcc=not le, dc=dc)
 
 
-def h_slt(a, bank, root, mask, dc=False, w32=False):
+def h_slt(a, bank, root, mask, dc=False, w32=False, ip=False):
     _scmp(a, bank, root, mask, False, dc)
 
 
-def h_sle(a, bank, root, mask, dc=False, w32=False):
+def h_sle(a, bank, root, mask, dc=False, w32=False, ip=False):
     _scmp(a, bank, root, mask, True, dc)
 
 
-def h_ite(a, bank, root, mask, dc=False, w32=False):
+def h_subr(a, bank, root, mask, dc=False, w32=False, ip=False):
+    """b - a.  In place on a: F[a] = Y(b) - F[a] (v_subrev)."""
+    if ip:
+        def emit():
+            a("v_subrev_co_u32 %s, vcc, %s, %s" % (v(F[0]), v(F[0]), v(Y[0])))
+            for j in range(1, 8):
+                a("v_subbrev_co_u32 %s, vcc, %s, %s, vcc" % (v(F[j]), v(F[j]), v(Y[j])))
+        return inplace_op(a, bank, root, mask, "SRC0", emit)
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), "SRC0")
+    a("v_subrev_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(F[0]), v(Y[0])))
+    for j in range(1, 8):
+        a("v_subbrev_co_u32 %s, vcc, %s, %s, vcc" % (v(R[j]), v(F[j]), v(Y[j])))
+    a.idx_off()
+    finish(a, bank, R, root, mask)
+
+
+def _ite_cond(a: Asm, bank: int, negate: bool):
+    a.idx_on(fld(bank, F_C), "SRC0")
+    a("v_and_b32_e64 %s, %s, 1" % (v(T[0]), v(F[0])))
+    a.idx_off()
+    a("v_cmp_%s_u32 vcc, 0, %s" % ("eq" if negate else "ne", v(T[0])))
+
+
+def _ite_inplace(a: Asm, bank: int, root: bool, negate: bool):
+    """F[a] = cond ? F[a] : F[b]   (ITE, dest == a)
+       F[a] = cond ? F[b] : F[a]   (ITEN, dest == a): vcc = !cond."""
+    prologue(a, bank)
+    _ite_cond(a, bank, not negate)           # vcc set where F[b] is selected
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), "SRC0,DST")
+    for j in range(8):
+        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(F[j]), v(F[j]), v(Y[j])))
+    if root:
+        a("s_set_gpr_idx_mode gpr_idx(SRC0)")
+        a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+    a.idx_off()
+    dispatch(a, 1 - bank)
+
+
+def h_iten(a, bank, root, mask, dc=False, w32=False, ip=False):
+    """c ? b : a."""
+    if ip:
+        return _ite_inplace(a, bank, root, True)
+    prologue(a, bank)
+    _ite_cond(a, bank, False)
+    a.read_slot(Y, fld(bank, F_A))
+    a.idx_on(fld(bank, F_B), "SRC1")
+    for j in range(8):
+        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[j]), v(Y[j]), v(F[j])))
+    a.idx_off()
+    finish(a, bank, R, root, False)
+
+
+def h_ite(a, bank, root, mask, dc=False, w32=False, ip=False):
+    if ip:
+        return _ite_inplace(a, bank, root, False)
     prologue(a, bank)
     a.idx_on(fld(bank, F_C), "SRC0")
     a("v_and_b32_e64 %s, %s, 1" % (v(T[0]), v(F[0])))
@@ -517,7 +654,7 @@ def h_ite(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, False)
 
 
-def h_extract(a, bank, root, mask, dc=False, w32=False):
+def h_extract(a, bank, root, mask, dc=False, w32=False, ip=False):
     """R = (F[a] >> lo) & mask(W).  C = 8a + (lo >> 5) + 8, IMM = lo & 31."""
     prologue(a, bank)
     load_masks(a, fld(bank, F_MOFF))
@@ -533,7 +670,7 @@ def h_extract(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, True)
 
 
-def h_concat(a, bank, root, mask, dc=False, w32=False):
+def h_concat(a, bank, root, mask, dc=False, w32=False, ip=False):
     """R = F[a] << sb | F[b] (sb = width of b).  C = funnel index, IMM =
     funnel shift; MOFF -> 8 masks of the bits >= sb."""
     prologue(a, bank)
@@ -549,7 +686,7 @@ def h_concat(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, False)
 
 
-def h_sext(a, bank, root, mask, dc=False, w32=False):
+def h_sext(a, bank, root, mask, dc=False, w32=False, ip=False):
     """sign_extend from IMM bits to W bits.  MOFF -> 16 masks: bits < IMM,
     then bits < W."""
     prologue(a, bank)
@@ -565,7 +702,7 @@ def h_sext(a, bank, root, mask, dc=False, w32=False):
     dispatch(a, 1 - bank)
 
 
-def h_spill_lds(a, bank, root, mask, dc=False, w32=False):
+def h_spill_lds(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_A))
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
@@ -574,7 +711,7 @@ def h_spill_lds(a, bank, root, mask, dc=False, w32=False):
     dispatch(a, 1 - bank)
 
 
-def h_reload_lds(a, bank, root, mask, dc=False, w32=False):
+def h_reload_lds(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
     a("ds_read_b128 v[%d:%d], %s" % (R[0], R[3], v(T[0])))
@@ -583,7 +720,7 @@ def h_reload_lds(a, bank, root, mask, dc=False, w32=False):
     finish(a, bank, R, root, False)
 
 
-def h_spill_scr(a, bank, root, mask, dc=False, w32=False):
+def h_spill_scr(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_A))
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
@@ -592,7 +729,7 @@ def h_spill_scr(a, bank, root, mask, dc=False, w32=False):
     dispatch(a, 1 - bank)
 
 
-def h_reload_scr(a, bank, root, mask, dc=False, w32=False):
+def h_reload_scr(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
     a("scratch_load_dwordx4 v[%d:%d], off, %s" % (R[0], R[3], s(S_T)))
@@ -638,7 +775,7 @@ def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int):
     a.label(skip)
 
 
-def h_out(a, bank, root, mask, dc=False, w32=False):
+def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
     """probe[C] = F[a] (active lanes, when a probe buffer is bound)."""
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_A))
@@ -815,7 +952,7 @@ def _gen_leaf(a: Asm, bank: int):
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
 
 
-def h_leaf(a, bank, root, mask, dc=False, w32=False):
+def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
@@ -1322,7 +1459,7 @@ CHEAP = {
     "RELOAD_SCR": h_reload_scr, "ADD": h_add, "SUB": h_sub, "AND": h_and, "OR": h_or,
     "XOR": h_xor, "NOT": h_not, "EQ": h_eq, "ULT": h_ult, "ULE": h_ule, "SLT": h_slt,
     "SLE": h_sle, "ITE": h_ite, "CONCAT": h_concat, "EXTRACT": h_extract, "SEXT": h_sext,
-    "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov,
+    "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov, "SUBR": h_subr, "ITEN": h_iten,
 }
 HEAVY = {"MUL": "MUL", "UMULNO": "UMULNO", "SHL": "SHL", "LSHR": "LSHR", "ASHR": "ASHR",
          "UDIV": "DIV", "UREM": "DIV", "SDIV": "DIV", "SREM": "DIV", "SMOD": "DIV"}
@@ -1362,11 +1499,11 @@ def generate() -> List[str]:
             if canon_var(name, var) != var:
                 continue
             root_v, mask_v = bool(var & V_ROOT), bool(var & V_MASK)
-            dc_v, w32_v = bool(var & V_DC), bool(var & V_W32)
+            dc_v, w32_v, ip_v = bool(var & V_DC), bool(var & V_W32), bool(var & V_IP)
             for bank in (0, 1):
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
                 if name in CHEAP:
-                    CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v)
+                    CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
                 else:
                     bits = var | (DIV_CODE.get(name, 0) << 4)
                     heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
@@ -1410,6 +1547,7 @@ def write_outputs(csrc: str) -> None:
            "#define MGA_NVAR %d" % NVAR,
            "#define MGA_V_ROOT %d" % V_ROOT, "#define MGA_V_MASK %d" % V_MASK,
            "#define MGA_V_DC %d" % V_DC, "#define MGA_V_W32 %d" % V_W32,
+           "#define MGA_V_IP %d" % V_IP,
            "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
            "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,
            "enum mga_op {"]

@@ -284,6 +284,20 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         case MG_MOV: aop = MGA_MOV; break;
         default: aop = MGA_NOP; break;
         }
+        // in place: the destination is operand a's slot (swap operands of
+        // commutative ops, use the reversed forms SUBR / ITEN otherwise)
+        if (!(var & MGA_V_W32)) {
+            const bool comm = op == MG_ADD || op == MG_AND || op == MG_OR || op == MG_XOR;
+            if ((comm || op == MG_SUB || op == MG_ITE) && d == b && d != a) {
+                const uint32_t t = r[2]; r[2] = r[3]; r[3] = t;
+                if (op == MG_SUB) aop = MGA_SUBR;
+                if (op == MG_ITE) aop = MGA_ITEN;
+                var |= MGA_V_IP;
+            } else if ((comm || op == MG_SUB || op == MG_ITE || op == MG_NOT || op == MG_NEG) &&
+                       d == a) {
+                var |= MGA_V_IP;
+            }
+        }
         r[0] = hoff[MGA_HID(aop, var, bank)];
         if (writes) clean[d] = narrow;
         bank = mga_is_heavy(aop) ? 0 : 1 - bank;

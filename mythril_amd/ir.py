@@ -480,6 +480,9 @@ def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
     return out, fused
 
 
+_INPLACE = {I.ADD, I.SUB, I.AND, I.OR, I.XOR, I.NOT, I.NEG, I.ITE}
+
+
 def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = frozenset(),
               nreg: int = I.NREG):
     trash = nreg - 1
@@ -492,6 +495,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
     lds_of: Dict[int, int] = {}
     holder: Dict[int, LNode] = {}          # reg -> value
     free_regs = list(range(nreg - 1))[::-1]
+    reg_clean: Dict[int, bool] = {}        # register's last value had <= 32 bits
     free_lds: List[int] = []
     n_lds = 0
     ins: List[Tuple[int, int, int, int, int, int, int]] = []
@@ -535,6 +539,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
 
     def materialise(v: LNode, r: int):
         nonlocal n_reload
+        reg_clean[r] = v.width <= 32
         if v.op == I.CONST:
             ins.append((I.CONST, v.width, r, 0, 0, 0, const_index[v.imm]))
         else:
@@ -569,7 +574,26 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         if not uses.get(n.id):
             d = trash
         else:
-            d = alloc_reg(i, set())
+            d = None
+            # in place: reuse a dying operand's register (the engine then
+            # writes the result through the file directly)
+            if n.op in _INPLACE and n.width > 32:
+                cand = slots[1:3] if n.op == I.ITE else slots[:2]
+                for r in cand:
+                    if r in free_regs:
+                        free_regs.remove(r)
+                        d = r
+                        break
+            # one-limb results prefer a register whose upper limbs are zero
+            if d is None and n.width <= 32:
+                for r in reversed(free_regs):
+                    if reg_clean.get(r):
+                        free_regs.remove(r)
+                        d = r
+                        break
+            if d is None:
+                d = alloc_reg(i, set())
+            reg_clean[d] = n.width <= 32
             reg_of[n.id] = d
             holder[d] = n
         op = n.op

@@ -546,6 +546,17 @@ class Wave:
         self.wr_lanes(a[1], x < y + c)
         self.vwrite(a[0], (x - y - c) & np.uint64(M32))
 
+    def i_v_subrev_co_u32(self, a, pc):
+        x, y = self.vread(a[2], "SRC0"), self.vread(a[3], "SRC1")
+        self.wr_lanes(a[1], y < x)
+        self.vwrite(a[0], (y - x) & np.uint64(M32))
+
+    def i_v_subbrev_co_u32(self, a, pc):
+        x, y = self.vread(a[2], "SRC0"), self.vread(a[3], "SRC1")
+        c = self._carry_in(a[4])
+        self.wr_lanes(a[1], y < x + c)
+        self.vwrite(a[0], (y - x - c) & np.uint64(M32))
+
     def i_v_mad_u64_u32(self, a, pc):
         x, y = self.vread(a[2], "SRC0"), self.vread(a[3], "SRC1")
         c = self.vread(a[4], "SRC2", 64)
