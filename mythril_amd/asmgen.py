@@ -171,16 +171,18 @@ class Asm:
         self("s_set_gpr_idx_off")
 
     def read_slot(self, dst: List[int], fld_sgpr: int):
+        """dst[0..7] <- F[slot] with four 64-bit moves (full rate on gfx950,
+        profiles/r01/ubench2.log; slot indices keep pairs aligned)."""
         self.idx_on(fld_sgpr, "SRC0")
-        for j in range(8):
-            self("v_mov_b32 %s, %s" % (v(dst[j]), v(F[j])))
+        for j in range(0, 8, 2):
+            self("v_mov_b64 %s, %s" % (vp(dst[j]), vp(F[j])))
         self.idx_off()
 
     def write_slot(self, src: List[int], fld_sgpr: int, masks: Optional[int] = None):
         self.idx_on(fld_sgpr, "DST")
-        for j in range(8):
+        for j in range(0, 8, 2) if masks is None else range(8):
             if masks is None:
-                self("v_mov_b32 %s, %s" % (v(F[j]), v(src[j])))
+                self("v_mov_b64 %s, %s" % (vp(F[j]), vp(src[j])))
             else:
                 self("v_and_b32 %s, %s, %s" % (v(F[j]), s(masks + j), v(src[j])))
         self.idx_off()
@@ -229,12 +231,20 @@ def finish(a: Asm, bank: int, res: List[int], root: bool, mask: bool):
 
 
 def write_narrow(a: Asm, bank: int, r0: str, dc: bool):
-    """F[D] = (r0, 0, ..., 0); with dc the upper limbs are already zero."""
+    """F[D] = (r0, 0, ..., 0); with dc the upper limbs are already zero.
+    (R1 is used as the zero half of the first 64-bit move.)"""
+    if dc:
+        a.idx_on(fld(bank, F_D), "DST")
+        a("v_mov_b32 %s, %s" % (v(F[0]), r0))
+        a.idx_off()
+        return
+    if r0 != v(R[0]):
+        a("v_mov_b32 %s, %s" % (v(R[0]), r0))
+    a("v_mov_b32 %s, 0" % v(R[1]))
     a.idx_on(fld(bank, F_D), "DST")
-    a("v_mov_b32 %s, %s" % (v(F[0]), r0))
-    if not dc:
-        for j in range(1, 8):
-            a("v_mov_b32 %s, 0" % v(F[j]))
+    a("v_mov_b64 %s, %s" % (vp(F[0]), vp(R[0])))
+    for j in range(2, 8, 2):
+        a("v_mov_b64 %s, 0" % vp(F[j]))
     a.idx_off()
 
 
@@ -310,8 +320,8 @@ def h_const(a, bank, root, mask, dc=False, w32=False, ip=False):
         dispatch(a, 1 - bank)
         return
     a.idx_on(fld(bank, F_D), "DST")
-    for j in range(8):
-        a("v_mov_b32 %s, %s" % (v(F[j]), s(S_M + j)))
+    for j in range(0, 8, 2):
+        a("v_mov_b64 %s, %s" % (vp(F[j]), sp(S_M + j)))
     a.idx_off()
     if root:
         a.root_and(s(S_M))
@@ -512,11 +522,12 @@ def h_eq(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a.read_slot(Y, fld(bank, F_B))
     a.idx_on(fld(bank, F_A), "SRC0")
-    for j in range(8):
-        a("v_xor_b32 %s, %s, %s" % (v(Y[j]), v(F[j]), v(Y[j])))
+    for j in range(0, 8, 2):        # 64-bit compares (full rate), AND-ed in SALU
+        a("v_cmp_eq_u64_e64 %s, %s, %s" % (sp(S_T + j), vp(F[j]), vp(Y[j])))
     a.idx_off()
-    or_reduce(a, Y, T[0])
-    a("v_cmp_eq_u32 vcc, 0, %s" % v(T[0]))
+    a("s_and_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
+    a("s_and_b64 %s, %s, %s" % (sp(S_T + 4), sp(S_T + 4), sp(S_T + 6)))
+    a("s_and_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 4)))
     _bool_result(a, bank, root, dc=dc)
 
 
@@ -1186,13 +1197,19 @@ def body_shift(a: Asm, kind: str):
 # Registers: u = X, v = Y on entry; un = X ++ R ++ [T0]; vn = Y;
 # q/b/c = T2/T3/T4 (kept for the remainder); dinv = T1; digit temps T5..T11.
 
-def clz256(a: Asm, vals: List[int], out: int, t: int):
-    a("v_mov_b32 %s, 256" % v(out))
+def clz256(a: Asm, vals: List[int], out: int, t: List[int]):
+    """Leading zeros of a nonzero 256-bit value: min over limbs of
+    (7-j)*32 + ffbh(limb j), with ffbh(0) = ~0 kept saturated by a clamped
+    add.  t: 8 temps (may include out)."""
     for j in range(8):
-        a("v_ffbh_u32 %s, %s" % (v(t), v(vals[j])))
-        a("v_add_u32 %s, %d, %s" % (v(t), (7 - j) * 32, v(t)))
-        a("v_cmp_ne_u32 vcc, 0, %s" % v(vals[j]))
-        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(out), v(out), v(t)))
+        a("s_movk_i32 %s, 0x%x" % (s(S_T + j), (7 - j) * 32))
+    for j in range(8):
+        a("v_ffbh_u32 %s, %s" % (v(t[j]), v(vals[j])))
+        a("v_add_u32_e64 %s, %s, %s clamp" % (v(t[j]), v(t[j]), s(S_T + j)))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(t[0]), v(t[0]), v(t[1]), v(t[2])))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(t[3]), v(t[3]), v(t[4]), v(t[5])))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(out), v(t[0]), v(t[3]), v(t[6])))
+    a("v_min_u32 %s, %s, %s" % (v(out), v(out), v(t[7])))
 
 
 def udivrem(a: Asm, want_rem: bool):
@@ -1204,9 +1221,9 @@ def udivrem(a: Asm, want_rem: bool):
     vn = Y
     sh, q, b, c, dinv = T[1], T[1], T[2], T[3], T[10]
     bz = S_T + 4
-    for j in range(8):
-        a("v_mov_b32 %s, 0" % v(R[j]))
-    clz256(a, Y, sh, T[4])
+    clz256(a, Y, sh, [T[1]] + T[4:11])
+    for j in range(0, 8, 2):
+        a("v_mov_b64 %s, 0" % vp(R[j]))
     a("v_and_b32 %s, 31, %s" % (v(b), v(sh)))
     a("v_lshrrev_b32 %s, 5, %s" % (v(q), v(sh)))
     a("v_sub_u32 %s, 32, %s" % (v(c), v(b)))
@@ -1234,7 +1251,9 @@ def udivrem(a: Asm, want_rem: bool):
     a("v_cvt_u32_f64_e32 %s, %s" % (v(dinv), vp(f1)))
     a("s_nop 1")
     p0, p1, tt = T[4], T[5], T[6]
-    for _ in range(2):
+    # after the Newton step the estimate is within one of the exact value:
+    # one round of both corrections
+    for _ in range(1):
         # p = dinv*d + (d << 32) = (2^32 + dinv) * d; carry -> too big
         a("v_mov_b32 %s, 0" % v(p0))
         a("v_mov_b32 %s, %s" % (v(p1), v(d)))

@@ -89,7 +89,7 @@ def _split_ops(s: str) -> List[str]:
         if not m or m.end() == pos:
             break
         tok = m.group(1).strip()
-        mm = re.fullmatch(r"(.*\S)\s+(offset:\d+)", tok)
+        mm = re.fullmatch(r"(.*\S)\s+(offset:\d+|clamp)", tok)
         if mm:
             out.extend([mm.group(1), mm.group(2)])
         else:
@@ -449,6 +449,9 @@ class Wave:
     def i_v_mov_b32(self, a, pc):
         self.vwrite(a[0], self.vread(a[1], "SRC0"))
 
+    def i_v_mov_b64(self, a, pc):
+        self.vwrite(a[0], self.vread(a[1], "SRC0", 64))
+
     def _vop2(self, a, f):
         x = self.vread(a[1], "SRC0")
         y = self.vread(a[2], "SRC1")
@@ -464,6 +467,10 @@ class Wave:
         self._vop2(a, lambda x, y: x ^ y)
 
     def i_v_add_u32(self, a, pc):
+        if a and a[-1] == "clamp":
+            x, y = self.vread(a[1], "SRC0"), self.vread(a[2], "SRC1")
+            self.vwrite(a[0], np.minimum(x + y, np.uint64(M32)))
+            return
         self._vop2(a, lambda x, y: x + y)
 
     def i_v_sub_u32(self, a, pc):
@@ -498,6 +505,19 @@ class Wave:
     def _vop3(self, a, f, n):
         srcs = [self.vread(a[1 + i], "SRC%d" % i) for i in range(n)]
         self.vwrite(a[0], f(*srcs) & np.uint64(M32))
+
+    def i_v_add_u32_clamp(self, a, pc):
+        pass
+
+    def i_v_min3_u32(self, a, pc):
+        self._vop3(a, lambda x, y, z: np.minimum(np.minimum(x, y), z), 3)
+
+    def i_v_min_u32(self, a, pc):
+        self._vop2(a, lambda x, y: np.minimum(x, y))
+
+    def i_s_movk_i32(self, a, pc):
+        v = int(a[1], 0) & 0xFFFF
+        self.swrite(a[0], (v - 0x10000 if v & 0x8000 else v) & M32)
 
     def i_v_add3_u32(self, a, pc):
         self._vop3(a, lambda x, y, z: x + y + z, 3)
@@ -592,6 +612,9 @@ class Wave:
 
     def i_v_cmp_gt_i32(self, a, pc):
         self._cmp(a, lambda x, y: x > y, signed=True)
+
+    def i_v_cmp_eq_u64(self, a, pc):
+        self._cmp(a, lambda x, y: x == y, width=64)
 
     def i_v_cmp_gt_u64(self, a, pc):
         self._cmp(a, lambda x, y: x > y, width=64)
