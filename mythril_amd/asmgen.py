@@ -613,18 +613,30 @@ def _ite_cond(a: Asm, bank: int, negate: bool):
 
 def _ite_inplace(a: Asm, bank: int, root: bool, negate: bool):
     """F[a] = cond ? F[a] : F[b]   (ITE, dest == a)
-       F[a] = cond ? F[b] : F[a]   (ITEN, dest == a): vcc = !cond."""
+       F[a] = cond ? F[b] : F[a]   (ITEN, dest == a): vcc = !cond.
+    F[b] is copied in the lanes that select it (under exec)."""
     prologue(a, bank)
     _ite_cond(a, bank, not negate)           # vcc set where F[b] is selected
     a.read_slot(Y, fld(bank, F_B))
-    a.idx_on(fld(bank, F_A), "SRC0,DST")
-    for j in range(8):
-        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(F[j]), v(F[j]), v(Y[j])))
-    if root:
-        a("s_set_gpr_idx_mode gpr_idx(SRC0)")
-        a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+    lab = exec_begin(a, None, S_T)
+    a.idx_on(fld(bank, F_A), "DST")
+    moves(a, F, Y)
     a.idx_off()
+    exec_end(a, lab, S_T)
+    if root:
+        a.idx_on(fld(bank, F_A), "SRC0")
+        a("v_and_b32 %s, %s, %s" % (OP_ROOT, v(F[0]), OP_ROOT))
+        a.idx_off()
     dispatch(a, 1 - bank)
+
+
+def _ite_select(a: Asm, bank: int, first: int, other: int):
+    """R = F[first], then F[other] copied into R where vcc is set."""
+    a.read_slot(R, fld(bank, first))
+    a.read_slot(Y, fld(bank, other))
+    lab = exec_begin(a, None, S_T)
+    moves(a, R, Y)
+    exec_end(a, lab, S_T)
 
 
 def h_iten(a, bank, root, mask, dc=False, w32=False, ip=False):
@@ -632,12 +644,8 @@ def h_iten(a, bank, root, mask, dc=False, w32=False, ip=False):
     if ip:
         return _ite_inplace(a, bank, root, True)
     prologue(a, bank)
-    _ite_cond(a, bank, False)
-    a.read_slot(Y, fld(bank, F_A))
-    a.idx_on(fld(bank, F_B), "SRC1")
-    for j in range(8):
-        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[j]), v(Y[j]), v(F[j])))
-    a.idx_off()
+    _ite_cond(a, bank, False)                # vcc = c: take F[b]
+    _ite_select(a, bank, F_A, F_B)
     finish(a, bank, R, root, False)
 
 
@@ -645,11 +653,8 @@ def h_ite(a, bank, root, mask, dc=False, w32=False, ip=False):
     if ip:
         return _ite_inplace(a, bank, root, False)
     prologue(a, bank)
-    a.idx_on(fld(bank, F_C), "SRC0")
-    a("v_and_b32_e64 %s, %s, 1" % (v(T[0]), v(F[0])))
-    a.idx_off()
-    a("v_cmp_ne_u32 vcc, 0, %s" % v(T[0]))
     if w32:
+        _ite_cond(a, bank, False)
         a.idx_on(fld(bank, F_B), "SRC0")
         a("v_mov_b32 %s, %s" % (v(Y[0]), v(F[0])))
         a("s_set_gpr_idx_idx %s" % s(fld(bank, F_A)))
@@ -657,11 +662,8 @@ def h_ite(a, bank, root, mask, dc=False, w32=False, ip=False):
         a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[0]), v(Y[0]), v(F[0])))
         a.idx_off()
         return finish_narrow(a, bank, root, False, dc)
-    a.read_slot(Y, fld(bank, F_B))
-    a.idx_on(fld(bank, F_A), "SRC1")
-    for j in range(8):
-        a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[j]), v(Y[j]), v(F[j])))
-    a.idx_off()
+    _ite_cond(a, bank, True)                 # vcc = !c: take F[b]
+    _ite_select(a, bank, F_A, F_B)
     finish(a, bank, R, root, False)
 
 
@@ -814,22 +816,21 @@ def load_sm64_consts(a: Asm):
 
 
 def mul64_const(a: Asm, z: List[int], klo: int, khi: int, t: List[int]):
-    """z *= K (mod 2^64), K in SGPRs; t: aligned pair t[0]:t[1] + t[2]."""
-    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(t[0]), sp(S_T + 6), v(z[1]), s(klo)))   # hi*klo
-    a("v_mov_b32 %s, %s" % (v(t[2]), v(t[0])))
-    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(t[0]), sp(S_T + 6), v(z[0]), s(khi)))   # lo*khi
-    a("v_add_u32 %s, %s, %s" % (v(t[2]), v(t[2]), v(t[0])))
+    """z *= K (mod 2^64), K in SGPRs; t: aligned pairs t[0]:t[1], t[2]:t[3]
+    (t[3] is read as don't-care, never written).  hi cross terms with one
+    v_mul_lo and the low word of a mad; the full low product with a mad."""
+    a("v_mul_lo_u32 %s, %s, %s" % (v(t[2]), v(z[0]), s(khi)))                        # lo*khi
+    a("v_mad_u64_u32 %s, %s, %s, %s, %s" % (vp(t[0]), sp(S_T + 6), v(z[1]), s(klo), vp(t[2])))
     a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(z[0]), sp(S_T + 6), v(z[0]), s(klo)))   # lo*klo
-    a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[2])))
+    a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[0])))
 
 
 def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
     """SplitMix64 on the per-lane state st = (lo, hi): st += GOLD; z =
     mix(st).  Constants in SGPRs (load_sm64_consts); t: 4 temps with
-    t[0]:t[1] aligned.  Full-rate v_mad_u64_u32 for every product.
-    Uses vcc and s[S_T+6:S_T+7]."""
+    t[0]:t[1] and t[2]:t[3] aligned; t[3] holds GOLD_HI on entry (set once
+    per leaf, preserved).  Uses vcc and s[S_T+6:S_T+7]."""
     a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(K_GOLD_LO), v(st[0])))
-    a("v_mov_b32 %s, %s" % (v(t[3]), s(K_GOLD_HI)))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[3]), v(st[1])))
     a("v_lshrrev_b64 %s, 30, %s" % (vp(t[0]), vp(st[0])))
     a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(st[0]), v(t[0])))
@@ -873,12 +874,11 @@ def _gen_leaf(a: Asm, bank: int):
     a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
     # idx = first + lane ; st = seed ^ salt ^ idx * GOLD
     a("s_mov_b64 %s, %s" % (sp(S_T + 4), IN["first"]))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(T[10]), s(S_T + 4), OP_LANE_LO))
-    a("v_mov_b32 %s, %s" % (v(T[11]), s(S_T + 5)))
-    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(T[11]), v(T[11]), OP_LANE_HI))
-    a("v_mov_b32 %s, %s" % (v(st[0]), v(T[10])))
-    a("v_mov_b32 %s, %s" % (v(st[1]), v(T[11])))
+    a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(S_T + 4), OP_LANE_LO))
+    a("v_mov_b32 %s, %s" % (v(st[1]), s(S_T + 5)))
+    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(st[1]), OP_LANE_HI))
     mul64_const(a, st, K_GOLD_LO, K_GOLD_HI, tt)
+    a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
     a("s_waitcnt lgkmcnt(0)")
     a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(g + 6)))
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), v(st[0])))
@@ -891,9 +891,9 @@ def _gen_leaf(a: Asm, bank: int):
     for j in range(0, 8, 2):
         sm64(a, st, [X[j], X[j + 1]], tt)
     _class_mask(a, S_T + 2, g + 3, g + 4, cls)                       # small
-    for j in range(2, 8):
-        a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(X[j]), v(X[j]), sp(S_T + 2)))
-    a("s_mov_b64 %s, exec" % sp(S_T + 4))
+    lab = exec_begin(a, S_T + 2, S_T + 4)
+    moves(a, X[2:], [None] * 6)
+    exec_end(a, lab, S_T + 4)
     # ---- boundary: pct_small <= cls < pct_boundary -------------------------
     _class_mask(a, S_T + 2, g + 4, g + 5, cls)
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
@@ -1090,34 +1090,73 @@ def body_umulno(a: Asm):
 
 # ---- per-lane shifts ------------------------------------------------------
 
-def barrel_right(a: Asm, t: List[int], q: int, nl: int):
-    """t[0..nl-1] = t >> (32*q) limbs (q per lane in v[q] < 8), zero fill."""
-    for st in (1, 2, 4):
-        a("v_and_b32 %s, %d, %s" % (v(TMP), st, v(q)))
-        a("v_cmp_ne_u32 vcc, 0, %s" % v(TMP))
-        skip = a.uniq("brr")
-        a("s_cbranch_vccz %s" % skip)
-        for j in range(nl):
-            src = v(t[j + st]) if j + st < nl else "0"
-            a("v_cndmask_b32 %s, %s, %s, vcc" % (v(t[j]), v(t[j]), src))
-        a.label(skip)
+def exec_begin(a: Asm, mask: Optional[int], save: int, invert: bool = False) -> str:
+    """Narrow exec to the lanes of s[mask:mask+1] (vcc if None; or the
+    complement) and
+    branch over the block when none is left; returns the label that
+    exec_end places.  VALU under a narrowed exec writes only those lanes, so
+    a conditional update costs one plain instruction instead of a compute +
+    v_cndmask pair.  Clobbers s[save:save+1] and scc."""
+    lab = a.uniq("xm")
+    a("s_mov_b64 %s, exec" % sp(save))
+    a("s_%s_b64 exec, exec, %s" % ("andn2" if invert else "and", "vcc" if mask is None else sp(mask)))
+    a("s_cbranch_execz %s" % lab)
+    return lab
 
 
-def barrel_left(a: Asm, t: List[int], q: int, nl: int, live: Optional[int] = None):
-    """t[0..nl-1] = t << (32*q) limbs (q < 8), zero fill; ``live`` = number
-    of possibly-nonzero low limbs on entry (known-zero moves are skipped)."""
+def exec_end(a: Asm, lab: str, save: int):
+    a.label(lab)
+    a("s_mov_b64 exec, %s" % sp(save))
+
+
+def moves(a: Asm, dsts: List[int], srcs: List[Optional[int]]):
+    """dsts[i] <- srcs[i] (None = 0) in list order, two limbs per v_mov_b64
+    where both register pairs are even-aligned and consecutive.  The caller
+    orders the list so no source is overwritten before it is read."""
+    i = 0
+    while i < len(dsts):
+        if i + 1 < len(dsts):
+            d0, d1, s0, s1 = dsts[i], dsts[i + 1], srcs[i], srcs[i + 1]
+            lo, hi = (0, 1) if d1 == d0 + 1 else (1, 0)
+            dl, sl = (d0, s0) if lo == 0 else (d1, s1)
+            dh, sh = (d1, s1) if lo == 0 else (d0, s0)
+            if dh == dl + 1 and dl % 2 == 0 and (
+                    (sl is None and sh is None) or
+                    (sl is not None and sh == sl + 1 and sl % 2 == 0)):
+                a("v_mov_b64 %s, %s" % (vp(dl), "0" if sl is None else vp(sl)))
+                i += 2
+                continue
+        a("v_mov_b32 %s, %s" % (v(dsts[i]), "0" if srcs[i] is None else v(srcs[i])))
+        i += 1
+
+
+def _barrel(a: Asm, t: List[int], q: int, nl: int, left: bool, save: int,
+            live: Optional[int] = None):
     hi = nl if live is None else live
     for st in (1, 2, 4):
         a("v_and_b32 %s, %d, %s" % (v(TMP), st, v(q)))
         a("v_cmp_ne_u32 vcc, 0, %s" % v(TMP))
-        top = min(nl, hi + st)
-        skip = a.uniq("brl")
-        a("s_cbranch_vccz %s" % skip)
-        for j in reversed(range(top)):
-            src = v(t[j - st]) if j - st >= 0 else "0"
-            a("v_cndmask_b32 %s, %s, %s, vcc" % (v(t[j]), v(t[j]), src))
-        a.label(skip)
-        hi = top
+        lab = exec_begin(a, None, save)
+        if left:
+            top = min(nl, hi + st)
+            js = list(reversed(range(top)))
+            moves(a, [t[j] for j in js], [t[j - st] if j - st >= 0 else None for j in js])
+            hi = top
+        else:
+            moves(a, [t[j] for j in range(nl)], [t[j + st] if j + st < nl else None for j in range(nl)])
+        exec_end(a, lab, save)
+
+
+def barrel_right(a: Asm, t: List[int], q: int, nl: int, save: int):
+    """t[0..nl-1] = t >> (32*q) limbs (q per lane in v[q] < 8), zero fill;
+    each stage moves only the lanes that take it (under exec)."""
+    _barrel(a, t, q, nl, False, save)
+
+
+def barrel_left(a: Asm, t: List[int], q: int, nl: int, save: int, live: Optional[int] = None):
+    """t[0..nl-1] = t << (32*q) limbs (q < 8), zero fill; ``live`` = number
+    of possibly-nonzero low limbs on entry (known-zero moves are skipped)."""
+    _barrel(a, t, q, nl, True, save, live)
 
 
 def bitshift_right(a: Asm, t: List[int], b: int, n_out: int):
@@ -1126,13 +1165,15 @@ def bitshift_right(a: Asm, t: List[int], b: int, n_out: int):
         a("v_alignbit_b32 %s, %s, %s, %s" % (v(t[j]), v(t[j + 1]), v(t[j]), v(b)))
 
 
-def bitshift_left(a: Asm, t: List[int], b: int, c: int, bz: int, nl: int):
-    """t[j] = t[j] << b | t[j-1] >> (32-b), j = nl-1..0 (t[-1] = 0);
-    c = (32 - b) & 31; s[bz:bz+1] = lanes with b == 0."""
+def bitshift_left(a: Asm, t: List[int], c: int, bz: int, nl: int, save: int):
+    """t[j] = t[j] << b | t[j-1] >> (32-b), j = nl-1..0 (t[-1] = 0), for the
+    lanes with b != 0 (c = 32 - b; s[bz:bz+1] = lanes with b == 0, which keep
+    t unchanged: v_alignbit cannot shift by 32)."""
+    lab = exec_begin(a, bz, save, invert=True)
     for j in reversed(range(nl)):
         lo = v(t[j - 1]) if j > 0 else "0"
-        a("v_alignbit_b32 %s, %s, %s, %s" % (v(TMP), v(t[j]), lo, v(c)))
-        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(t[j]), v(TMP), v(t[j]), sp(bz)))
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(t[j]), v(t[j]), lo, v(c)))
+    exec_end(a, lab, save)
 
 
 def body_shift(a: Asm, kind: str):
@@ -1165,24 +1206,24 @@ def body_shift(a: Asm, kind: str):
         fill = T[4]
     if kind == "SHL":
         a("v_sub_u32 %s, 32, %s" % (v(T[5]), v(T[3])))
-        a("v_and_b32 %s, 31, %s" % (v(T[5]), v(T[5])))
         a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_X + 2), v(T[3])))
-        barrel_left(a, X, T[2], 8)
-        bitshift_left(a, X, T[3], T[5], S_X + 2, 8)
+        barrel_left(a, X, T[2], 8, S_T)
+        bitshift_left(a, X, T[5], S_X + 2, 8, S_T)
     else:
         a("v_mov_b32 %s, 0" % v(R[0]))
         t = X + [R[0]]
-        barrel_right(a, t, T[2], 8)
+        barrel_right(a, t, T[2], 8, S_T)
         bitshift_right(a, t, T[3], 8)
-    for j in range(8):
-        if fill is None:
-            a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(R[j]), v(X[j]), sp(over)))
-        else:
+    if fill is not None:
+        for j in range(8):
             a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(fill)))
-            a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(fill), sp(over)))
+        a("v_mov_b32 %s, %s" % (v(T[5]), v(fill)))
+    lab = exec_begin(a, over, S_T)                   # shift >= W: 0 or sign fill
+    moves(a, X, [None if fill is None else T[4 + (j & 1)] for j in range(8)])
+    exec_end(a, lab, S_T)
     if kind == "LSHR":
         a("s_and_b32 %s, %s, 1" % (s(S_VAR), s(S_VAR)))     # canonical: no mask needed
-    heavy_finish(a, R)
+    heavy_finish(a, X)
 
 
 # ---- division ---------------------------------------------------------------
@@ -1227,17 +1268,16 @@ def udivrem(a: Asm, want_rem: bool):
     a("v_and_b32 %s, 31, %s" % (v(b), v(sh)))
     a("v_lshrrev_b32 %s, 5, %s" % (v(q), v(sh)))
     a("v_sub_u32 %s, 32, %s" % (v(c), v(b)))
-    a("v_and_b32 %s, 31, %s" % (v(c), v(c)))
     a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(bz), v(b)))
-    barrel_left(a, vn, q, 8)
-    bitshift_left(a, vn, b, c, bz, 8)
-    barrel_left(a, un, q, 16, live=8)
-    a("v_alignbit_b32 %s, 0, %s, %s" % (v(T[0]), v(un[15]), v(c)))       # un[16]
-    a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(T[0]), v(T[0]), sp(bz)))
-    bitshift_left(a, un, b, c, bz, 16)
-    d, d6 = vn[7], vn[6]
+    a("v_mov_b32 %s, 0" % v(T[0]))                                       # un[16]
+    barrel_left(a, vn, q, 8, S_T)
+    bitshift_left(a, vn, c, bz, 8, S_T)
+    barrel_left(a, un, q, 16, S_T, live=8)
+    bitshift_left(a, un, c, bz, 17, S_T)
+    d = vn[7]
     # dinv = floor((2^64-1)/d) - 2^32 (d >= 2^31): f64 reciprocal, one
-    # Newton step, then exact integer correction (two rounds)
+    # Newton step (the estimate is then within one of the exact value), then
+    # one exact integer correction in each direction
     f0, f1, fe = T[4], T[6], T[8]
     a("v_cvt_f64_u32_e32 %s, %s" % (vp(f0), v(d)))
     a("v_rcp_f64_e32 %s, %s" % (vp(f1), vp(f0)))
@@ -1250,25 +1290,21 @@ def udivrem(a: Asm, want_rem: bool):
     a("v_add_f64 %s, %s, %s" % (vp(f1), vp(f1), sp(S_T + 6)))
     a("v_cvt_u32_f64_e32 %s, %s" % (v(dinv), vp(f1)))
     a("s_nop 1")
-    p0, p1, tt = T[4], T[5], T[6]
-    # after the Newton step the estimate is within one of the exact value:
-    # one round of both corrections
-    for _ in range(1):
-        # p = dinv*d + (d << 32) = (2^32 + dinv) * d; carry -> too big
-        a("v_mov_b32 %s, 0" % v(p0))
-        a("v_mov_b32 %s, %s" % (v(p1), v(d)))
-        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (p0, p1, sp(S_T + 6), v(dinv), v(d), p0, p1))
-        a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(tt), sp(S_T + 6)))
-        a("v_sub_u32 %s, %s, %s" % (v(dinv), v(dinv), v(tt)))
-        # too small: (2^64-1) - p >= d  <=>  ~p_hi != 0 or ~p_lo >= d
-        a("v_not_b32 %s, %s" % (v(p0), v(p0)))
-        a("v_not_b32 %s, %s" % (v(p1), v(p1)))
-        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T + 2), v(p1)))
-        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), v(d), v(p0)))
-        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
-        a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 6)))
-        a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(tt), sp(S_T)))
-        a("v_add_u32 %s, %s, %s" % (v(dinv), v(dinv), v(tt)))
+    p0, p1 = T[4], T[5]
+    # p = dinv*d + (d << 32) = (2^32 + dinv) * d; carry -> too big
+    a("v_mov_b32 %s, 0" % v(p0))
+    a("v_mov_b32 %s, %s" % (v(p1), v(d)))
+    a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (p0, p1, sp(S_T + 6), v(dinv), v(d), p0, p1))
+    a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), sp(S_T + 6)))
+    # too small: (2^64-1) - p >= d  <=>  ~p_hi != 0 or ~p_lo >= d
+    a("v_not_b32 %s, %s" % (v(p0), v(p0)))
+    a("v_not_b32 %s, %s" % (v(p1), v(p1)))
+    a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T + 2), v(p1)))
+    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), v(d), v(p0)))
+    a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
+    a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 6)))
+    a("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), sp(S_T)))
+    a("v_mov_b32 %s, 0" % v(T[9]))                                  # RH of the digit loop
     for j in reversed(range(8)):
         u2, u1 = un[j + 8], un[j + 7]
         skip = a.uniq("dvs")
@@ -1276,22 +1312,22 @@ def udivrem(a: Asm, want_rem: bool):
         a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(u1), v(d)))
         a("s_or_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 2)))
         a("s_cbranch_vccz %s" % skip)
-        _div_digit(a, un, vn, j, d, d6, dinv)
+        _div_digit(a, un, vn, j, d, dinv)
         a.label(skip)
     if want_rem:
         # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
         a("v_mov_b32 %s, 0" % v(T[0]))
         t = X + [T[0]]
-        barrel_right(a, t, q, 9)
+        barrel_right(a, t, q, 9, S_T)
         bitshift_right(a, t, b, 8)
 
 
-def _div_digit(a: Asm, un, vn, j, d, d6, dinv):
+def _div_digit(a: Asm, un, vn, j, d, dinv):
     """One quotient digit of Knuth D for every lane (see udivrem).
-    Registers: A = T4:T5, P = T6:T7 (64-bit pairs), CR/RH = T8:T9, QH = T11."""
-    u2, u1, u0 = un[j + 8], un[j + 7], un[j + 6]
+    Registers: A = T4:T5, P = T6:T7 (64-bit pairs), CR:RH = T8:T9 (RH = 0
+    for the whole loop), QH = T11."""
+    u2, u1 = un[j + 8], un[j + 7]
     A0, A1, P0, P1, CR, RH, QH = T[4], T[5], T[6], T[7], T[8], T[9], T[11]
-    RL = A1
     st = S_T
     lt = sp(st)                  # lanes with u2 < d (all but the u2 == d case)
     # 2-by-1 quotient via the reciprocal: qq = dinv * a2 + (a2:u1), a2 = u2 < d ? u2 : 0
@@ -1303,77 +1339,60 @@ def _div_digit(a: Asm, un, vn, j, d, d6, dinv):
     a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(d)))
     a("v_sub_u32 %s, %s, %s" % (v(CR), v(u1), v(P0)))                # r = u1 - q1*d
     a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(A0)))   # r > q0: q1--, r += d
-    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
-    a("v_sub_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
+    a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(QH), sp(st + 4), v(QH), sp(st + 2)))
     a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
     a("v_add_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
     a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(st + 2), v(CR), v(d)))     # r >= d: q1++, r -= d
-    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
-    a("v_add_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
-    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
-    a("v_sub_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
-    # rhat (65 bits) = r; lanes with u2 == d: qhat = b-1, rhat = u1 + d
-    a("v_mov_b32 %s, %s" % (v(RL), v(CR)))
-    a("v_mov_b32 %s, 0" % v(RH))
+    a("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (v(QH), sp(st + 4), v(QH), sp(st + 2)))
+    # lanes with u2 == d: qhat = b - 1.  qhat is now at most two above the
+    # true digit (Knuth's Theorem B, normalised divisor); the add-back below
+    # runs at most twice, and only for waves with a lane that needs it
     lab_nb = a.uniq("dnb")
     a("s_cmp_eq_u64 %s, -1" % lt)
     a("s_cbranch_scc1 %s" % lab_nb)
     a("v_cndmask_b32_e64 %s, -1, %s, %s" % (v(QH), v(QH), lt))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(P0), v(u1), v(d)))
-    a("v_cndmask_b32 %s, 0, 1, vcc" % v(P1))
-    a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(RL), v(P0), v(RL), lt))
-    a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(RH), v(P1), lt))
     a.label(lab_nb)
-    # Knuth's test: rh < 2^32 and qh*d6 > rh*2^32 + u0 -> qh--, rh += d; a
-    # second round only if some lane of the wave corrected in the first
-    lab_k = a.uniq("dk")
-    for rnd in range(2):
-        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(d6)))
-        a("v_mov_b32 %s, %s" % (v(A0), v(u0)))                      # (A0, A1) = u0 : rh_lo
-        a("v_cmp_gt_u64_e64 %s, v[%d:%d], v[%d:%d]" % (sp(st + 2), P0, P1, A0, A1))
-        a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(st + 4), v(RH)))
-        a("s_and_b64 %s, %s, %s" % (sp(st + 2), sp(st + 2), sp(st + 4)))
-        a("s_cbranch_scc0 %s" % lab_k)                              # no lane to fix
-        a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(P0), sp(st + 2)))
-        a("v_sub_u32 %s, %s, %s" % (v(QH), v(QH), v(P0)))
-        if rnd == 0:
-            a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), sp(st + 2)))
-            a("v_add_co_u32 %s, vcc, %s, %s" % (v(RL), v(RL), v(P0)))
-            a("v_addc_co_u32 %s, vcc, 0, %s, vcc" % (v(RH), v(RH)))
-    a.label(lab_k)
     # multiply-subtract un[j..j+8] -= qh * vn as one borrow chain in vcc:
     # P = qh * vn[i] + carry (carry pair CR:RH with RH = 0), un[j+i] -= P.lo
-    a("v_mov_b32 %s, 0" % v(CR))
-    a("v_mov_b32 %s, 0" % v(RH))
     for i in range(8):
-        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (P0, P1, sp(st + 6), v(QH), v(vn[i]), CR, RH))
+        add = "0" if i == 0 else "v[%d:%d]" % (CR, RH)
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (P0, P1, sp(st + 6), v(QH), v(vn[i]), add))
         a("v_mov_b32 %s, %s" % (v(CR), v(P1)))
         if i == 0:
             a("v_sub_co_u32 %s, vcc, %s, %s" % (v(un[j]), v(un[j]), v(P0)))
         else:
             a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
     a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(u2), v(u2), v(CR)))
-    # borrow lanes went negative: quotient digit qh - 1 and add vn back (rare)
+    # borrow lanes went negative: quotient digit qh - 1 and add vn back under
+    # exec (rare); without Knuth's test qh can be two too big: lanes with no
+    # carry out of the first add-back take a second one
     a("s_mov_b64 %s, vcc" % sp(st + 4))
     a("v_subb_co_u32 %s, vcc, %s, 0, vcc" % (v(u2), v(QH)))       # digit into the dead top
-    lab = a.uniq("dab")
+    lab, lab_x = a.uniq("dab"), a.uniq("dax")
     a("s_cmp_eq_u64 %s, 0" % sp(st + 4))
     a("s_cbranch_scc1 %s" % lab)
-    a("v_cndmask_b32_e64 %s, 0, -1, %s" % (v(P1), sp(st + 4)))
-    a("v_and_b32 %s, %s, %s" % (v(P0), v(vn[0]), v(P1)))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(un[j]), v(un[j]), v(P0)))
-    for i in range(1, 8):
-        a("v_and_b32 %s, %s, %s" % (v(P0), v(vn[i]), v(P1)))
-        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
+    a("s_mov_b64 %s, exec" % sp(st + 2))
+    a("s_mov_b64 exec, %s" % sp(st + 4))
+    for rnd in range(2):
+        a("v_add_co_u32 %s, vcc, %s, %s" % (v(un[j]), v(un[j]), v(vn[0])))
+        for i in range(1, 8):
+            a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(vn[i])))
+        if rnd == 0:
+            a("s_andn2_b64 exec, exec, vcc")                        # still negative
+            a("s_cbranch_execz %s" % lab_x)
+            a("v_add_u32 %s, -1, %s" % (v(u2), v(u2)))
+    a.label(lab_x)
+    a("s_mov_b64 exec, %s" % sp(st + 2))
     a.label(lab)
 
 
 def _cond_neg(a: Asm, regs: List[int], m: int):
-    a("v_sub_co_u32 %s, vcc, 0, %s" % (v(T[1]), v(regs[0])))
-    a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(regs[0]), v(regs[0]), v(T[1]), sp(m)))
+    """regs = -regs in the lanes of s[m:m+1] (under exec; uses s[S_T+2:+3])."""
+    lab = exec_begin(a, m, S_T + 2)
+    a("v_sub_co_u32 %s, vcc, 0, %s" % (v(regs[0]), v(regs[0])))
     for j in range(1, 8):
-        a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(T[1]), v(regs[j])))
-        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(regs[j]), v(regs[j]), v(T[1]), sp(m)))
+        a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(regs[j]), v(regs[j])))
+    exec_end(a, lab, S_T + 2)
 
 
 DIV_CODE = {"UDIV": 0, "UREM": 1, "SDIV": 2, "SREM": 3, "SMOD": 4}
@@ -1421,49 +1440,55 @@ def body_div(a: Asm):
     for k in range(1, 5):
         a("s_cmp_eq_u32 %s, %d" % (s(OPR), k))
         a("s_cbranch_scc1 %s" % labs[k])
+    def ones_where_zero():                             # R = z ? ~0 : R
+        lab = exec_begin(a, Z, S_T + 2)
+        for j in range(0, 8, 2):
+            a("v_mov_b64 %s, -1" % vp(R[j]))
+        exec_end(a, lab, S_T + 2)
+
+    def rem_unless_zero(dst, src):                     # dst = z ? dst : src
+        lab = exec_begin(a, Z, S_T + 2, invert=True)
+        moves(a, dst, src)
+        exec_end(a, lab, S_T + 2)
+
     a.label(labs[0])                                   # udiv: z ? ~0 : q
-    for j in range(8):
-        a("v_cndmask_b32_e64 %s, %s, -1, %s" % (v(R[j]), v(R[j]), sp(Z)))
+    ones_where_zero()
     a("s_branch %s" % lab_end)
     a.label(labs[1])                                   # urem: z ? q : rem
-    for j in range(8):
-        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j]), sp(Z)))
+    rem_unless_zero(R, X)
     a("s_branch %s" % lab_end)
     a.label(labs[2])                                   # sdiv
-    for j in range(8):
-        a("v_cndmask_b32_e64 %s, %s, -1, %s" % (v(R[j]), v(R[j]), sp(Z)))
+    ones_where_zero()
     a("s_xor_b64 %s, %s, %s" % (sp(NS), sp(NS), sp(NT)))
     _cond_neg(a, R, NS)
     a("s_branch %s" % lab_end)
     a.label(labs[3])                                   # srem: sign of the dividend
-    for j in range(8):
-        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j]), sp(Z)))
+    rem_unless_zero(R, X)
     _cond_neg(a, R, NS)
     a("s_branch %s" % lab_end)
     a.label(labs[4])                                   # smod
-    for j in range(8):                                 # m = z ? q : rem  -> X
-        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(X[j]), v(X[j]), v(R[j]), sp(Z)))
+    lab = exec_begin(a, Z, S_T + 2)                    # m = z ? q : rem  -> X
+    moves(a, X, R)
+    exec_end(a, lab, S_T + 2)
     a.read_slot(Y, cur(F_B))                           # t again
     lab_nx = a.uniq("dsx")
     a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
     a("s_cbranch_scc0 %s" % lab_nx)
     sext(a, Y, cur(F_W), S_M, T[0], S_T)
     a.label(lab_nx)
-    a("v_sub_co_u32 %s, vcc, 0, %s" % (v(R[0]), v(X[0])))             # R = -m
-    for j in range(1, 8):
-        a("v_subb_co_u32 %s, vcc, 0, %s, vcc" % (v(R[j]), v(X[j])))
-    for j in range(8):                                 # base = ns ? -m : m
-        a("v_cndmask_b32_e64 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j]), sp(NS)))
+    moves(a, R, X)                                     # base = ns ? -m : m
+    _cond_neg(a, R, NS)
     a("s_xor_b64 %s, %s, %s" % (sp(NT), sp(NS), sp(NT)))               # ns != nt: + t
-    for j in range(8):
-        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(Y[j]), v(Y[j]), sp(NT)))
+    lab = exec_begin(a, NT, S_T + 2)
     a("v_add_co_u32 %s, vcc, %s, %s" % (v(R[0]), v(R[0]), v(Y[0])))
     for j in range(1, 8):
         a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(R[j]), v(R[j]), v(Y[j])))
+    exec_end(a, lab, S_T + 2)
     or_reduce(a, X, T[0])                              # m == 0 -> 0
     a("v_cmp_eq_u32 vcc, 0, %s" % v(T[0]))
-    for j in range(8):
-        a("v_cndmask_b32 %s, %s, 0, vcc" % (v(R[j]), v(R[j])))
+    lab = exec_begin(a, None, S_T + 2)
+    moves(a, R, [None] * 8)
+    exec_end(a, lab, S_T + 2)
     a.label(lab_end)
     heavy_finish(a, R)
 

@@ -163,6 +163,35 @@ def overflow_case():
     return constraints, probes, gen
 
 
+def hard_division_pair(rng: random.Random):
+    """(x, y) where Knuth D's two-digit quotient estimate is often two too
+    big: y = a random top digit over all-ones lower digits (the shape of
+    2^k - 1 boundary values), x a near multiple of y."""
+    k = rng.randrange(2, 9)
+    y = (1 << (32 * k - 1)) | rng.getrandbits(32 * k - 1)
+    if rng.random() < 0.7:
+        y |= (1 << (32 * k - 33)) - 1
+    x = rng.getrandbits(256)
+    if rng.random() < 0.6:
+        x = (y * rng.getrandbits(32 * (8 - k) + 1) - rng.getrandbits(40)) % (1 << 256)
+    if rng.random() < 0.3:                       # negative operands for the signed ops
+        x = (1 << 256) - x if rng.random() < 0.5 else x
+        y = (1 << 256) - y if rng.random() < 0.5 else y
+    return x, y
+
+
+def division_case():
+    """All five division operators on hard_division_pair operands."""
+    x, y = N.bv_var("dx", 256), N.bv_var("dy", 256)
+    probes = [N.bv_op(op, x, y) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    constraints = [N.bv_cmp("bvult", probes[1], y)]
+
+    def gen(rng):
+        a, b = hard_division_pair(rng)
+        return Assignment(vars={"dx": a, "dy": b})
+    return constraints, probes, gen
+
+
 def named_cases():
     out = {}
     for w in WIDTHS:
@@ -174,4 +203,6 @@ def named_cases():
     out["keccak_uf"] = keccak_uf_case()
     c, p, g = overflow_case()
     out["overflow"] = (c, p, g, {})
+    c, p, g = division_case()
+    out["division_hard"] = (c, p, g, {})
     return out

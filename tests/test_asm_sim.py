@@ -83,6 +83,34 @@ def test_division_edges_with_reciprocal_noise():
             assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
 
 
+def _max_qhat_error(x: int, y: int) -> int:
+    """Largest (estimate - true digit) of Knuth D's two-digit quotient
+    estimate over the digits of x / y (32-bit digits, normalised)."""
+    B = 1 << 32
+    sh = 256 - y.bit_length()
+    un = [((x << sh) >> (32 * i)) & (B - 1) for i in range(17)]
+    V = y << sh
+    worst = 0
+    for j in range(7, -1, -1):
+        window = sum(un[j + i] << (32 * i) for i in range(9))
+        q = window // V
+        qh = min((un[j + 8] * B + un[j + 7]) // (V >> 224), B - 1)
+        worst = max(worst, qh - q)
+        r = window - q * V
+        for i in range(9):
+            un[j + i] = (r >> (32 * i)) & (B - 1)
+    return worst
+
+
+def test_hard_division_case_reaches_double_correction():
+    """The division_hard case (run by test_case_parity_sim here and by the
+    GPU parity suite) does exercise a quotient estimate two too big, the
+    path that takes the second add-back."""
+    rng = random.Random(2000 + len("division_hard"))
+    errs = [_max_qhat_error(*dag_cases.hard_division_pair(rng)) for _ in range(64)]
+    assert max(errs) == 2 and errs.count(2) >= 3
+
+
 @pytest.mark.parametrize("dag_id,n_lds", [(0, 6), (1, 0), (7, 2), (33, 6)])
 def test_corpus_constraints_as_probes_generated(dag_id, n_lds):
     """A corpus DAG with every constraint probed (so each lane checks ~half
