@@ -57,3 +57,21 @@ if sq:
     shutil.copy(sq, os.path.join(DST, "sq_counters.csv"))
 for log in glob.glob(os.path.join(SRC, "*.log")):
     shutil.copy(log, os.path.join(DST, os.path.basename(log)))
+if sq:
+    c = {}
+    for r in csv.DictReader(open(sq)):
+        if "mg_interp" in r["Kernel_Name"]:
+            c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    w = c.get("SQ_WAVES") or 1.0
+    summ = {k: c[k] for k in sorted(c)}
+    summ.update({"valu_per_wave": c.get("SQ_INSTS_VALU", 0) / w,
+                 "salu_per_wave": c.get("SQ_INSTS_SALU", 0) / w,
+                 "smem_per_wave": c.get("SQ_INSTS_SMEM", 0) / w,
+                 "note": "sums over the mg_interp dispatches of the --dags 512 pass; SQ cycle "
+                         "counters tick once per 4 shader cycles on CDNA"})
+    if c.get("SQ_WAVE_CYCLES"):
+        summ["valu_active_frac_of_wave_time"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"]
+        summ["salu_active_frac_of_wave_time"] = c.get("SQ_ACTIVE_INST_SALU", 0) / c["SQ_WAVE_CYCLES"]
+        summ["wait_inst_frac_of_wave_time"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+    json.dump(summ, open(os.path.join(DST, "sq_summary.json"), "w"), indent=1)
+    print("sq", json.dumps(summ))

@@ -9,5 +9,5 @@ ARGS="$@"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/kt -o kt -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS > gpurun_out/prof/kt.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof/fetch -o fetch -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > gpurun_out/prof/fetch.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof/write -o write -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > gpurun_out/prof/write.log 2>&1 || exit 1
-timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/prof/sq -o sq -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --dags 512 > gpurun_out/prof/sq.log 2>&1 || exit 1
+timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU --output-format csv -d gpurun_out/prof/sq -o sq -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --dags 512 > gpurun_out/prof/sq.log 2>&1 || exit 1
 echo profile-ok
