@@ -105,6 +105,16 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* batch, uint64_t seed, uint64_t firs
                       uint64_t n_assign, uint64_t* d_root_bits, uint64_t* d_first_sat,
                       void* stream);
 
+/* Batched witness search (replaces the per-state Constraints.is_possible ->
+ * get_model loop at mythril/laser/ethereum/svm.py:201-203 and :257-262):
+ * for every program of the batch, the smallest candidate index in
+ * [gen->first_index, gen->first_index + n_cand) that satisfies it, or -1, in
+ * first_sat[n_progs].  All programs share each launch; programs already
+ * solved stop consuming lanes.  Witness leaves: mg_search with n_cand = 1 at
+ * the returned index. */
+int mg_batch_search(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_cand,
+                    int64_t* first_sat);
+
 /* Keccak-256 (0x01 padding) of n messages, one GPU lane per message.
  *   data/offsets/lens describe the messages in one host byte buffer;
  *   out: n x 32 bytes. */

@@ -1228,51 +1228,71 @@ def body_shift(a: Asm, kind: str):
 
 # ---- division ---------------------------------------------------------------
 #
-# Unsigned 256/256 Knuth D on 32-bit digits, as udivrem256 in the C++
-# reference kernel: normalise by sh = clz(v) (limbs + bits) so vn's top digit
-# is vn[7]; un = u << sh (17 digits); quotient digit j (7..0) from un[j+8],
-# un[j+7], un[j+6] with the Moller-Granlund reciprocal of d = vn[7] and
-# Knuth's two-digit correction; multiply-subtract; add back if negative.
+# Unsigned 256/256 Knuth D on 32-bit digits: normalise by sh = clz(v) (limbs
+# + bits) so vn's top digit is vn[7]; un = u << sh (17 digits); quotient
+# digit j (7..0) from un[j+8], un[j+7] with the Moller-Granlund reciprocal of
+# d = vn[7] (two corrections give the exact 2-by-1 quotient, at most two above
+# the true digit); multiply-subtract; add back (at most twice) where negative.
 # An iteration is skipped when no lane of the wave has un[j+8] != 0 or
 # un[j+7] >= d (its quotient digit is then 0 and nothing changes).
 # Registers: u = X, v = Y on entry; un = X ++ R ++ [T0]; vn = Y;
-# q/b/c = T2/T3/T4 (kept for the remainder); dinv = T1; digit temps T5..T11.
+# b/c = T2/T3 (b kept for the remainder); digit temps T4..T11.
 
-def clz256(a: Asm, vals: List[int], out: int, t: List[int]):
-    """Leading zeros of a nonzero 256-bit value: min over limbs of
-    (7-j)*32 + ffbh(limb j), with ffbh(0) = ~0 kept saturated by a clamped
-    add.  t: 8 temps (may include out)."""
-    for j in range(8):
-        a("s_movk_i32 %s, 0x%x" % (s(S_T + j), (7 - j) * 32))
-    for j in range(8):
-        a("v_ffbh_u32 %s, %s" % (v(t[j]), v(vals[j])))
-        a("v_add_u32_e64 %s, %s, %s clamp" % (v(t[j]), v(t[j]), s(S_T + j)))
-    a("v_min3_u32 %s, %s, %s, %s" % (v(t[0]), v(t[0]), v(t[1]), v(t[2])))
-    a("v_min3_u32 %s, %s, %s, %s" % (v(t[3]), v(t[3]), v(t[4]), v(t[5])))
-    a("v_min3_u32 %s, %s, %s, %s" % (v(out), v(t[0]), v(t[3]), v(t[6])))
-    a("v_min_u32 %s, %s, %s" % (v(out), v(out), v(t[7])))
+DIV_M = {4: 48, 2: 50, 1: 52}   # limb-shift stage masks (bank B: free in heavy bodies)
 
 
-def udivrem(a: Asm, want_rem: bool):
-    """X / Y (Y != 0 in every lane): quotient -> R; remainder (want_rem) -> X.
-    Registers: un = X ++ R ++ [T0]; vn = Y; q/b/c = T1/T2/T3 (kept for the
-    remainder); pairs T4:T5, T6:T7, T8:T9 (64-bit tuples start even on
-    gfx950); dinv = T10.  Clobbers Y, T, vcc, s[S_T..S_T+7]."""
+def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
+           live: Optional[int] = None) -> int:
+    """One limb-barrel stage: shift t by st limbs in the lanes of s[mask]
+    (under exec; zero fill).  Returns the new number of live low limbs."""
+    lab = exec_begin(a, mask, S_T + 2)
+    if left:
+        hi = nl if live is None else live
+        top = min(nl, hi + st)
+        js = list(reversed(range(top)))
+        moves(a, [t[j] for j in js], [t[j - st] if j - st >= 0 else None for j in js])
+    else:
+        top = nl
+        moves(a, [t[j] for j in range(nl)], [t[j + st] if j + st < nl else None for j in range(nl)])
+    exec_end(a, lab, S_T + 2)
+    return top
+
+
+def udivrem(a: Asm, want_rem: bool, z: int):
+    """X / Y: quotient -> R; remainder (want_rem) -> X; s[z:z+1] <- lanes
+    with Y == 0, which divide by 1 instead (the caller applies SMT-LIB's
+    x/0 rules).  Normalisation shifts Y left until its top limb is nonzero,
+    4, 2 then 1 limbs at a time in the lanes whose top limbs are zero (the
+    stage masks stay in s[48:53] for the dividend and the remainder), then
+    by b = clz(top limb) bits.  Registers: un = X ++ R ++ [T0]; vn = Y;
+    b/c = T2/T3 (b kept for the remainder); pairs T4:T5, T6:T7, T8:T9
+    (64-bit tuples start even on gfx950); dinv = T10.  Clobbers Y, T, vcc,
+    s[S_T..S_T+7], s[48:53]."""
     un = X + R + [T[0]]
     vn = Y
-    sh, q, b, c, dinv = T[1], T[1], T[2], T[3], T[10]
+    b, c, dinv = T[2], T[3], T[10]
     bz = S_T + 4
-    clz256(a, Y, sh, [T[1]] + T[4:11])
     for j in range(0, 8, 2):
         a("v_mov_b64 %s, 0" % vp(R[j]))
-    a("v_and_b32 %s, 31, %s" % (v(b), v(sh)))
-    a("v_lshrrev_b32 %s, 5, %s" % (v(q), v(sh)))
+    a("v_mov_b32 %s, 0" % v(T[0]))                                       # un[16]
+    a("v_cmp_eq_u64_e64 %s, 0, %s" % (sp(DIV_M[4]), vp(Y[4])))
+    a("v_cmp_eq_u64_e64 %s, 0, %s" % (sp(S_T), vp(Y[6])))
+    a("s_and_b64 %s, %s, %s" % (sp(DIV_M[4]), sp(DIV_M[4]), sp(S_T)))
+    _stage(a, vn, 4, 8, True, DIV_M[4])
+    a("v_cmp_eq_u64_e64 %s, 0, %s" % (sp(DIV_M[2]), vp(Y[6])))
+    _stage(a, vn, 2, 8, True, DIV_M[2])
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(DIV_M[1]), v(Y[7])))
+    _stage(a, vn, 1, 8, True, DIV_M[1])
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(Y[7])))                  # Y == 0
+    a("v_ffbh_u32 %s, %s" % (v(b), v(Y[7])))
+    a("v_min_u32 %s, 31, %s" % (v(b), v(b)))                            # Y == 0: 1 << 255
+    a("v_cndmask_b32_e64 %s, %s, 1, %s" % (v(Y[7]), v(Y[7]), sp(z)))
     a("v_sub_u32 %s, 32, %s" % (v(c), v(b)))
     a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(bz), v(b)))
-    a("v_mov_b32 %s, 0" % v(T[0]))                                       # un[16]
-    barrel_left(a, vn, q, 8, S_T)
     bitshift_left(a, vn, c, bz, 8, S_T)
-    barrel_left(a, un, q, 16, S_T, live=8)
+    live = 8
+    for st in (4, 2, 1):
+        live = _stage(a, un, st, 16, True, DIV_M[st], live)
     bitshift_left(a, un, c, bz, 17, S_T)
     d = vn[7]
     # dinv = floor((2^64-1)/d) - 2^32 (d >= 2^31): f64 reciprocal, one
@@ -1318,7 +1338,8 @@ def udivrem(a: Asm, want_rem: bool):
         # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
         a("v_mov_b32 %s, 0" % v(T[0]))
         t = X + [T[0]]
-        barrel_right(a, t, q, 9, S_T)
+        for st in (1, 2, 4):
+            _stage(a, t, st, 9, False, DIV_M[st])
         bitshift_right(a, t, b, 8)
 
 
@@ -1421,18 +1442,15 @@ def body_div(a: Asm):
     _cond_neg(a, X, NS)
     _cond_neg(a, Y, NT)
     a.label(lab_u)
-    or_reduce(a, Y, T[0])
-    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(Z), v(T[0])))
-    a("v_cndmask_b32_e64 %s, %s, 1, %s" % (v(Y[0]), v(Y[0]), sp(Z)))
     lab_q, lab_dd = a.uniq("dq"), a.uniq("ddd")
     a("s_cmp_eq_u32 %s, 0" % s(OPR))
     a("s_cbranch_scc1 %s" % lab_q)
     a("s_cmp_eq_u32 %s, 2" % s(OPR))
     a("s_cbranch_scc1 %s" % lab_q)
-    udivrem(a, want_rem=True)
+    udivrem(a, want_rem=True, z=Z)
     a("s_branch %s" % lab_dd)
     a.label(lab_q)
-    udivrem(a, want_rem=False)
+    udivrem(a, want_rem=False, z=Z)
     a.label(lab_dd)
     # R = q (== |u| where the divisor was forced to 1), X = remainder
     labs = {k: a.uniq("dr%d" % k) for k in range(5)}

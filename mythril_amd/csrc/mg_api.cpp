@@ -709,6 +709,45 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
     return MG_OK;
 }
 
+int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand,
+                    int64_t* first_sat) {
+    if (!ctx || !b || !gen || (b->n && !first_sat)) return fail(ctx, MG_E_ARG, "null argument");
+    for (uint32_t i = 0; i < b->n; ++i) first_sat[i] = -1;
+    if (n_cand == 0 || b->n == 0) return MG_OK;
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    void* ws;
+    int rc = workspace(ctx, (size_t)b->n * 8, &ws);
+    if (rc) return rc;
+    unsigned long long* d_first = (unsigned long long*)ws;
+    HIPCHECK(ctx, hipMemsetAsync(d_first, 0xFF, (size_t)b->n * 8, ctx->stream));
+    std::vector<unsigned long long> h(b->n, ~0ull);
+    // ~2^24 lanes per launch over all programs (a launch stays well under a
+    // second); solved programs' blocks exit at once in later chunks
+    uint64_t chunk = (1ull << 24) / b->n;
+    chunk = chunk < 4096 ? 4096 : (chunk + 255) & ~255ull;
+    for (uint64_t done = 0; done < n_cand; done += chunk) {
+        for (uint32_t p0 = 0; p0 < b->n; p0 += 65535) {
+            const uint32_t np = b->n - p0 < 65535 ? b->n - p0 : 65535;
+            mg_run run = empty_run();
+            run.n_assign = n_cand - done < chunk ? n_cand - done : chunk;
+            run.stride = run.n_assign;
+            run.first_sat = d_first + p0;
+            run.seed = gen->seed;
+            run.first_index = gen->first_index + done;
+            run.skip_solved = 1;
+            HIPCHECK(ctx, launch(ctx, 1, b->d_descs + p0, np, run, b->max_lds, ctx->stream));
+        }
+        HIPCHECK(ctx, hipMemcpyAsync(h.data(), d_first, (size_t)b->n * 8, hipMemcpyDeviceToHost,
+                                     ctx->stream));
+        HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+        bool all = true;
+        for (uint32_t i = 0; i < b->n; ++i) all = all && h[i] != ~0ull;
+        if (all) break;
+    }
+    for (uint32_t i = 0; i < b->n; ++i) first_sat[i] = h[i] == ~0ull ? -1 : (int64_t)h[i];
+    return MG_OK;
+}
+
 int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lens,
                  uint32_t n, uint8_t* out) {
     if (!ctx || (n && (!offsets || !lens || !out))) return fail(ctx, MG_E_ARG, "null argument");

@@ -41,6 +41,9 @@ struct mg_run {
     uint32_t* leaves_out;      /* generator mode: dump generated leaves    */
     uint64_t seed;             /* generator seed                           */
     uint64_t first_index;      /* candidate index of lane 0                */
+    uint32_t skip_solved;      /* search: blocks of programs whose first_sat
+                                  is below first_index (solved by an earlier
+                                  chunk) return at once                    */
 };
 
 #endif

@@ -351,6 +351,7 @@ __global__ __launch_bounds__(BLOCK, MG_WAVES_PER_SIMD) void mg_interp(const mg_p
                                                       mg_run run) {
     extern __shared__ uint4 lds[];
     const uint32_t prog = blockIdx.y;
+    if (run.skip_solved && run.first_sat[prog] < run.first_index) return;
     const __attribute__((address_space(4))) mg_pdesc* D =
         (const __attribute__((address_space(4))) mg_pdesc*)(descs + prog);
     cu32* code = (cu32*)D->code;

@@ -21,7 +21,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
-           "mg_batch_free", "mg_batch_eval_gen", "mg_keccak256", "mg_version", "mg_config",
+           "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_keccak256", "mg_version", "mg_config",
            "mg_translate", "mg_asm_digest")
 
 
@@ -75,6 +75,7 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_batch_free.argtypes = [p]
         lib.mg_batch_free.restype = None
         lib.mg_batch_eval_gen.argtypes = [p, p, u64, u64, u64, p, p, p]
+        lib.mg_batch_search.argtypes = [p, p, C.POINTER(Gen), u64, p]
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
         lib.mg_config.argtypes = [p, u32]
         lib.mg_asm_digest.restype = C.c_char_p
@@ -232,6 +233,32 @@ class Engine:
                                         C.c_void_p(d_root_bits or None),
                                         C.c_void_p(d_first_sat or None), C.c_void_p(stream or None))
         self._check(rc, "mg_batch_eval_gen")
+
+
+    def batch_search(self, loaded: Sequence[LoadedProgram], seed: int, n_cand: int,
+                     first_index: int = 0) -> List[Tuple[int, Optional[np.ndarray]]]:
+        """Witness search over many programs in shared launches
+        (mg_batch_search); per program (index, leaves) or (-1, None)."""
+        if not loaded:
+            return []
+        h = self.batch_create(loaded)
+        try:
+            first = np.full(len(loaded), -1, dtype=np.int64)
+            g = Gen(seed & (2**64 - 1), first_index)
+            rc = self.lib.mg_batch_search(self._ctx, h, C.byref(g), n_cand, _ptr(first))
+            self._check(rc, "mg_batch_search")
+        finally:
+            self.batch_free(h)
+        out = []
+        for lp, f in zip(loaded, first.tolist()):
+            if f < 0:
+                out.append((-1, None))
+            else:
+                idx, wit = self.search(lp, seed, 1, first_index=f)   # regenerate the witness
+                if idx != f:
+                    raise EngineError("batch witness %d did not re-verify" % f)
+                out.append((f, wit))
+        return out
 
 
 def unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:

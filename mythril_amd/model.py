@@ -310,6 +310,85 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
     return _z3_check(constraints, minimize, maximize, timeout)
 
 
+def _witness_accepted(constraints, assignment, timeout) -> bool:
+    """get_model's rule for a GPU witness: re-verified by z3 when the
+    constraints are z3 ASTs and z3 is present, otherwise accepted (it was
+    evaluated bit-exactly on the device)."""
+    if z3bridge.available():
+        raws = [getattr(c, "raw", c) for c in constraints]
+        if all(not isinstance(r, N.Node) for r in raws):
+            return z3bridge.verify(raws, assignment, timeout) is not None
+    return True
+
+
+def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool]:
+    """``[c.is_possible for c in constraint_sets]`` with ONE batched GPU
+    witness search over all the sets.
+
+    Reference: ``Constraints.is_possible``
+    (``mythril/laser/ethereum/state/constraints.py:26-35``: possible iff
+    ``get_model(tuple(self))`` does not raise ``UnsatError``), called once per
+    state by LASER's state filters (``mythril/laser/ethereum/svm.py:201-203``
+    open states per transaction, ``:257-262`` new states per step).  A set
+    with a GPU witness (accepted by the same rule as ``get_model``) is
+    possible; every other set goes through ``get_model`` itself — its cache,
+    timeout arithmetic, Python-bool handling and z3 fallback — so the answers
+    are the ones the per-state loop gives, and UNSAT is only concluded by
+    z3."""
+    sets = [tuple(c) for c in constraint_sets]
+    results: List[Optional[bool]] = [None] * len(sets)
+    timeout = args.solver_timeout
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+    pending = []
+    if timeout > 0:
+        for i, cs in enumerate(sets):
+            if any(type(c) == bool and not c for c in cs):
+                continue                                   # get_model raises UnsatError
+            cs = [c for c in cs if type(c) != bool]
+            try:
+                nodes = _raw_nodes(cs)
+                prog = compile_constraints(nodes, extra_consts=harvest_hints(nodes))
+            except Unsupported as e:
+                stats.unsupported += 1
+                log.debug("GPU pre-filter: unsupported (%s)", e)
+                continue
+            pending.append((i, cs, prog))
+    if pending:
+        try:
+            eng = get_engine()
+            t0 = time.perf_counter()
+            loaded = [eng.load(prog, search_leafgen(prog), prog_seed=0) for _, _, prog in pending]
+            hits = eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES)
+            stats.gpu_time += time.perf_counter() - t0
+            for (i, cs, prog), (idx, wit) in zip(pending, hits):
+                stats.gpu_queries += 1
+                stats.gpu_candidates += SEARCH_CANDIDATES if idx < 0 else idx + 1
+                if idx >= 0 and _witness_accepted(cs, unpack(prog, wit), timeout):
+                    stats.gpu_hits += 1
+                    results[i] = True
+        except (EngineUnavailable, EngineError, z3bridge.Z3Unavailable) as e:
+            log.debug("GPU pre-filter unavailable: %s", e)
+    for i, cs in enumerate(sets):
+        if results[i] is None:
+            try:
+                get_model(cs, enforce_execution_time=enforce_execution_time)
+                results[i] = True
+            except UnsatError:
+                results[i] = False
+    return results
+
+
+def filter_possible(states, constraints_of=lambda s: s.world_state.constraints):
+    """Drop-in for LASER's state filters
+    ``[s for s in states if s.world_state.constraints.is_possible]``
+    (``svm.py:257-262``; ``svm.py:201-203`` passes
+    ``constraints_of=lambda s: s.constraints``), one batched search."""
+    states = list(states)
+    keep = batch_is_possible([constraints_of(s) for s in states])
+    return [s for s, k in zip(states, keep) if k]
+
+
 def install() -> None:
     """Rebind ``get_model`` in a Mythril installation: the three names bound
     by ``from ... import get_model``, and share Mythril's

@@ -91,3 +91,43 @@ def test_symbolic_calldata(engine):
     assert not check([load(BVV(51, 256)) == BVV(1, 8), size == BVV(50, 256)])
     # a byte inside the calldata can take a value
     assert check([load(BVV(3, 256)) == BVV(0xA9, 8), size == BVV(4, 256)])
+
+
+def test_batch_search_equals_per_program_search(engine):
+    """mg_batch_search returns, per program, the same first satisfying
+    candidate index as one mg_search per program (same counter-based
+    streams), -1 for an unsatisfiable program, and a witness that the oracle
+    accepts."""
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.assign import unpack
+    x, y = BVS("bx", 256), BVS("by", 256)
+    sets = [[x == BVV(3, 256)], [x + y == BVV(0, 256), x != BVV(0, 256)],
+            [(x & BVV(0xFF, 256)) == BVV(0x2A, 256)], [x != x], [y > x]]
+    progs = [compile_constraints([c.raw for c in s], extra_consts=M.harvest_hints([c.raw for c in s]))
+             for s in sets]
+    loaded = [engine.load(p, M.search_leafgen(p), prog_seed=0) for p in progs]
+    batch = engine.batch_search(loaded, M.SEARCH_SEED, 1 << 20)
+    for s, p, lp, (idx, wit) in zip(sets, progs, loaded, batch):
+        want, _ = engine.search(lp, M.SEARCH_SEED, 1 << 20)
+        assert idx == want
+        if idx >= 0:
+            a = unpack(p, wit)
+            assert R.eval_constraints([c.raw for c in s], R.Assignment(a.vars, a.arrays, a.funcs)) == 1
+    assert batch[3][0] == -1 and all(b[0] >= 0 for i, b in enumerate(batch) if i != 3)
+
+
+def test_batch_is_possible_on_reference_sat_queries(engine):
+    """The sat keccak / calldata / model_test queries as sibling states in
+    one batch: all possible, all found by the single batched search."""
+    x = BVS("x", 256)
+    cd = Array("1_calldata", 256, 8)
+    size = BVS("1_calldatasize", 256)
+    sets = [keccak_pair(engine, BVV(100, 8), BVV(100, 8)),
+            keccak_pair(engine, BVS("N1", 256), BVS("N2", 256)),
+            keccak_pair(engine, BVV(100, 256), BVS("N1", 256)),
+            [x == BVV(2, 256)],
+            [If(BVV(3, 256) < size, cd[BVV(3, 256)], BVV(0, 8)) == BVV(0xA9, 8),
+             size == BVV(4, 256)]]
+    hits0 = M.stats.gpu_hits
+    assert M.batch_is_possible(sets, enforce_execution_time=False) == [True] * len(sets)
+    assert M.stats.gpu_hits - hits0 == len(sets)

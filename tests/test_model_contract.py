@@ -84,3 +84,72 @@ def test_unsupported_falls_back(monkeypatch, fresh):
     with pytest.raises(M.SolverUnavailable):
         M.get_model((c_sat(),))
     assert M.stats.unsupported >= 1
+
+
+# ---- batched is_possible ---------------------------
+
+class FakeEngine:
+    """Stands in for the GPU: a set is 'found' unless its program has no
+    leaves (a constant query such as Bool false)."""
+
+    def __init__(self):
+        self.batches = []
+
+    def load(self, prog, leafgen, prog_seed=0):
+        return prog
+
+    def batch_search(self, loaded, seed, n_cand, first_index=0):
+        self.batches.append(len(loaded))
+        import numpy as np
+        out = []
+        for prog in loaded:
+            unsat = len(prog.leaves) == 0               # e.g. a constant-false query
+            out.append((-1, None) if unsat else (7, np.zeros((len(prog.leaves), 8), np.uint32)))
+        return out
+
+
+@pytest.fixture
+def batch_env(monkeypatch, fresh):
+    eng = FakeEngine()
+    monkeypatch.setattr(M, "get_engine", lambda: eng)
+    z3_calls = []
+
+    def fake_z3(constraints, minimize, maximize, timeout):
+        z3_calls.append(constraints)
+        raise M.UnsatError                         # z3 says unsat for every miss
+    monkeypatch.setattr(M, "_z3_check", fake_z3)
+    return eng, z3_calls
+
+
+def test_batch_is_possible_matches_the_per_state_loop(batch_env, monkeypatch):
+    eng, z3_calls = batch_env
+    x = symbol_factory.BitVecSym("x", 256)
+    unsat_like = symbol_factory.Bool(False).__class__(symbol_factory.Bool(False).raw)
+    sets = [(c_sat(),), (c_sat(), False), (unsat_like,), (True, c_sat()), (ULT(x, x),)]
+    got = M.batch_is_possible(sets)
+    assert eng.batches == [4]                        # one batched search, no per-set launches
+    want = []
+    for cs in sets:
+        try:
+            M.get_model(tuple(cs))
+            want.append(True)
+        except M.UnsatError:
+            want.append(False)
+    assert got == want
+    assert got[1] is False                           # Python False short-circuits
+
+
+def test_batch_is_possible_timeout_exhausted(batch_env):
+    eng, z3_calls = batch_env
+    M.time_handler.start_execution(0)
+    assert M.batch_is_possible([(c_sat(),), (c_sat(),)]) == [False, False]
+    assert eng.batches == [] and z3_calls == []
+
+
+def test_filter_possible_keeps_order_and_states(batch_env):
+    class S:
+        def __init__(self, c):
+            self.constraints = c
+    states = [S((c_sat(),)), S((c_sat(), False)), S((True, c_sat()))]
+    kept = M.filter_possible(states, constraints_of=lambda s: s.constraints)
+    assert kept == [states[0], states[2]]
