@@ -1,7 +1,9 @@
 /*
  * mythgpu IR — the compact postfix program the host compiler
- * (mythril_amd/ir.py) emits for one get_model constraint set and the HIP
- * interpreter (mythril_amd/csrc/mg_kernels.hip) executes per lane.
+ * (mythril_amd/ir.py) emits for one get_model constraint set.  The library
+ * validates it and translates it into the records of the gfx950 assembly
+ * interpreter (mythril_amd/asmgen.py, mg_interp_asm.hip), which executes it
+ * per lane (mg_kernels.hip holds the first C++ interpreter, kept for A/B).
  *
  * One lane evaluates one candidate assignment.  Values are bit-vectors of
  * width 1..256 held as 8 little-endian 32-bit limbs, always canonical (bits
@@ -37,8 +39,10 @@
 #define MG_TRASH (MG_NREG - 1) /* result sink                                 */
 #define MG_LIMBS 8           /* 8 x 32-bit limbs = 256 bits                   */
 #define MG_MAX_WIDTH 256
-#define MG_MAX_LDS 10        /* LDS spill slots: 10 x 8 KiB per 256-lane block
-                                keeps 2 blocks (8 waves) per CU               */
+#define MG_MAX_LDS 10        /* LDS spill slots addressable by the IR; the
+                                assembly kernel keeps the first 6 in LDS
+                                (6 x 8 KiB per 256-lane block, 3 blocks per
+                                CU) and the rest in per-lane scratch         */
 #define MG_MAX_PSLOTS 48     /* further spill slots in per-lane scratch      */
 
 enum mg_op {

@@ -116,10 +116,15 @@ class Model:
     witness itself (``assignment``)."""
 
     def __init__(self, models: Optional[List[object]] = None,
-                 assignment: Optional[Assignment] = None, program: Optional[Program] = None):
+                 assignment: Optional[Assignment] = None, programs=None):
         self.raw = models or []
         self.assignment = assignment
-        self.program = program
+        if isinstance(programs, Program):
+            programs = [programs]
+        self.programs = list(programs or [])
+        self.table_sizes: Dict[str, int] = {}
+        for p in self.programs:
+            self.table_sizes.update(p.table_sizes)
 
     def decls(self):
         out = []
@@ -149,8 +154,7 @@ class Model:
         if self.assignment is None:
             raise ValueError("no witness")
         from .assign import pack
-        prog = compile_constraints([], [node], table_sizes=dict(self.program.table_sizes)
-                                   if self.program else None)
+        prog = compile_constraints([], [node], table_sizes=dict(self.table_sizes) or None)
         eng = get_engine()
         lp = eng.load(prog)
         _, probes = eng.eval(lp, pack(prog, [self.assignment]), want_probes=True)
@@ -196,10 +200,66 @@ def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
     return sorted(out)
 
 
+def dependence_buckets(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
+    """Split constraints into groups that share no free symbol — the
+    ``DependenceMap`` of ``IndependenceSolver``
+    (``mythril/laser/smt/solver/independence_solver.py:38-84``), with free
+    arrays and uninterpreted functions counted as symbols too (the reference
+    only counts expression leaves; a GPU witness is a joint table per array /
+    UF, so two groups reading one table are not independent here).  Groups
+    keep the constraints' order; a symbol-free constraint is its own group."""
+    parent: Dict[object, object] = {}
+
+    def find(k):
+        while parent[k] != k:
+            parent[k] = parent[parent[k]]
+            k = parent[k]
+        return k
+
+    syms_of = []
+    for i, c in enumerate(nodes):
+        syms = set()
+        for n in N.topo_order([c]):
+            if n.op in ("var", "array", "apply"):
+                syms.add((n.op == "var", n.params[0]))
+        syms_of.append(syms)
+        parent.setdefault(("c", i), ("c", i))
+        for sym in syms:
+            parent.setdefault(sym, sym)
+            a, b = find(("c", i)), find(sym)
+            if a != b:
+                parent[b] = a
+    groups: Dict[object, List[N.Node]] = {}
+    for i, c in enumerate(nodes):
+        groups.setdefault(find(("c", i)), []).append(c)
+    return list(groups.values())
+
+
+def _merge(parts: Sequence[Assignment]) -> Assignment:
+    out = Assignment()
+    for a in parts:
+        out.vars.update(a.vars)
+        out.arrays.update(a.arrays)
+        out.funcs.update(a.funcs)
+    return out
+
+
 def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
-    """(assignment, program) of the first satisfying candidate, or None."""
-    prog = compile_constraints(nodes, extra_consts=harvest_hints(nodes))
+    """(assignment, programs) of a satisfying candidate, or None.  Queries
+    that split into independent groups (dependence_buckets) search every
+    group in one batched launch sequence and join the group witnesses, so the
+    hit probability is per group rather than their product."""
+    buckets = dependence_buckets(nodes)
     eng = get_engine()
+    if len(buckets) > 1:
+        progs = [compile_constraints(b, extra_consts=harvest_hints(b)) for b in buckets]
+        loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
+        hits = eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES)
+        stats.gpu_candidates += sum(SEARCH_CANDIDATES if i < 0 else i + 1 for i, _ in hits)
+        if any(i < 0 for i, _ in hits):
+            return None
+        return _merge([unpack(p, w) for p, (_, w) in zip(progs, hits)]), progs
+    prog = compile_constraints(nodes, extra_consts=harvest_hints(nodes))
     lp = eng.load(prog, search_leafgen(prog), prog_seed=0)
     t0 = time.perf_counter()
     chunk = 1 << 20
@@ -208,7 +268,7 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
         idx, wit = eng.search(lp, SEARCH_SEED, chunk, first_index=first)
         stats.gpu_candidates += chunk if idx < 0 else idx - first + 1
         if idx >= 0:
-            return unpack(prog, wit), prog
+            return unpack(prog, wit), [prog]
         first += chunk
         if (time.perf_counter() - t0) * 1000.0 > budget_ms:
             break
@@ -286,21 +346,21 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
             hit = gpu_search(nodes, budget_ms=min(timeout, 200))
             stats.gpu_time += time.perf_counter() - t0
             if hit is not None:
-                assignment, prog = hit
+                assignment, progs = hit
                 if z3bridge.available():
                     raws = [getattr(c, "raw", c) for c in constraints]
                     if all(not isinstance(r, N.Node) for r in raws):
                         m = z3bridge.verify(raws, assignment, timeout)
                         if m is not None:
                             stats.gpu_hits += 1
-                            return Model([m], assignment, prog)
+                            return Model([m], assignment, progs)
                         log.warning("GPU witness rejected by z3; falling back")
                     else:
                         stats.gpu_hits += 1
-                        return Model(None, assignment, prog)
+                        return Model(None, assignment, progs)
                 else:
                     stats.gpu_hits += 1
-                    return Model(None, assignment, prog)
+                    return Model(None, assignment, progs)
         except Unsupported as e:
             stats.unsupported += 1
             log.debug("GPU pre-filter: unsupported (%s)", e)
@@ -340,7 +400,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
     timeout = args.solver_timeout
     if enforce_execution_time:
         timeout = min(timeout, time_handler.time_remaining() - 500)
-    pending = []
+    pending = []                          # (set index, constraints, bucket programs)
     if timeout > 0:
         for i, cs in enumerate(sets):
             if any(type(c) == bool and not c for c in cs):
@@ -348,23 +408,29 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
             cs = [c for c in cs if type(c) != bool]
             try:
                 nodes = _raw_nodes(cs)
-                prog = compile_constraints(nodes, extra_consts=harvest_hints(nodes))
+                progs = [compile_constraints(b, extra_consts=harvest_hints(b))
+                         for b in dependence_buckets(nodes)]
             except Unsupported as e:
                 stats.unsupported += 1
                 log.debug("GPU pre-filter: unsupported (%s)", e)
                 continue
-            pending.append((i, cs, prog))
+            pending.append((i, cs, progs))
     if pending:
         try:
             eng = get_engine()
             t0 = time.perf_counter()
-            loaded = [eng.load(prog, search_leafgen(prog), prog_seed=0) for _, _, prog in pending]
-            hits = eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES)
+            flat = [p for _, _, progs in pending for p in progs]
+            loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in flat]
+            hits = iter(eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES))
             stats.gpu_time += time.perf_counter() - t0
-            for (i, cs, prog), (idx, wit) in zip(pending, hits):
+            for i, cs, progs in pending:
+                found = [next(hits) for _ in progs]
                 stats.gpu_queries += 1
-                stats.gpu_candidates += SEARCH_CANDIDATES if idx < 0 else idx + 1
-                if idx >= 0 and _witness_accepted(cs, unpack(prog, wit), timeout):
+                stats.gpu_candidates += sum(SEARCH_CANDIDATES if k < 0 else k + 1 for k, _ in found)
+                if any(k < 0 for k, _ in found):
+                    continue
+                a = _merge([unpack(p, w) for p, (_, w) in zip(progs, found)])
+                if _witness_accepted(cs, a, timeout):
                     stats.gpu_hits += 1
                     results[i] = True
         except (EngineUnavailable, EngineError, z3bridge.Z3Unavailable) as e:

@@ -7,6 +7,8 @@ import mythril_amd.model as M
 from mythril_amd.assign import Assignment
 from mythril_amd.smt import ULT, symbol_factory
 
+REAL_GPU_SEARCH = M.gpu_search          # the fixture below swaps in a fake
+
 
 @pytest.fixture(autouse=True)
 def fresh(monkeypatch):
@@ -153,3 +155,52 @@ def test_filter_possible_keeps_order_and_states(batch_env):
     states = [S((c_sat(),)), S((c_sat(), False)), S((True, c_sat()))]
     kept = M.filter_possible(states, constraints_of=lambda s: s.constraints)
     assert kept == [states[0], states[2]]
+
+
+# ---- independence splitting ------------------------
+
+def test_dependence_buckets_group_by_shared_symbols():
+    from mythril_amd.smt import Array, Function
+    bv = symbol_factory.BitVecSym
+    x, y, z, w = bv("x", 256), bv("y", 256), bv("z", 256), bv("w", 256)
+    a = Array("arr", 256, 256)
+    f = Function("keccak256_256", 256, 256)
+    cs = [x == symbol_factory.BitVecVal(1, 256),          # 0: {x}
+          y == symbol_factory.BitVecVal(2, 256),          # 1: {y}
+          (x + z) == symbol_factory.BitVecVal(3, 256),    # 2: {x, z} -> joins 0
+          a[y] == symbol_factory.BitVecVal(4, 256),       # 3: {arr, y} -> joins 1
+          f(w) == symbol_factory.BitVecVal(5, 256),       # 4: {f, w}
+          f(z) == symbol_factory.BitVecVal(6, 256),       # 5: {f, z} -> joins 0 and 4
+          symbol_factory.BitVecVal(1, 8) == symbol_factory.BitVecVal(1, 8)]   # 6: none
+    raws = [c.raw for c in cs]
+    groups = M.dependence_buckets(raws)
+    as_idx = sorted(sorted(raws.index(c) for c in g) for g in groups)
+    assert as_idx == [[0, 2, 4, 5], [1, 3], [6]]
+
+
+def test_bucketed_witness_joins_group_assignments(monkeypatch, fresh):
+    """gpu_search over independent groups: one batched search, the joint
+    witness is the union of the group witnesses."""
+    import numpy as np
+    bv = symbol_factory.BitVecSym
+    x, y = bv("x", 256), bv("y", 256)
+    nodes = [(x == symbol_factory.BitVecVal(9, 256)).raw, (y == symbol_factory.BitVecVal(4, 256)).raw]
+
+    class Eng:
+        calls = 0
+
+        def load(self, prog, leafgen, prog_seed=0):
+            return prog
+
+        def batch_search(self, loaded, seed, n_cand, first_index=0):
+            Eng.calls += 1
+            out = []
+            for p in loaded:
+                w = np.zeros((len(p.leaves), 8), np.uint32)
+                w[0, 0] = 9 if p.leaves[0].name == "x" else 4
+                out.append((3, w))
+            return out
+    monkeypatch.setattr(M, "get_engine", lambda: Eng())
+    a, progs = REAL_GPU_SEARCH(nodes, 200)
+    assert Eng.calls == 1 and len(progs) == 2
+    assert a.vars == {"x": 9, "y": 4}
