@@ -129,7 +129,8 @@ const char* mg_asm_digest(void);
 /* Host-only (no GPU): translate a validated IR program into the 8-word
  * records of the assembly interpreter, given its handler offset table
  * (mg_load_program does this with the table queried from the device).
- *   records: (n_ins + 2) x 8 words; masks: mask entries appended after the
+ *   records: up to (2 * n_ins + 3) x 8 words (a WAITVM record may precede
+ *   an instruction); masks: mask entries appended after the
  *   program's n_consts constants (8 words each).  Sizes are returned in
  *   *n_record_words / *n_mask_words; MG_E_ARG when a buffer is too small. */
 int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32_t n_lds,

@@ -68,7 +68,9 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "NOT", "SHL", "LSHR", "ASHR", "EQ", "ULT", "ULE", "SLT", "SLE", "UMULNO", "ITE",
         "CONCAT", "EXTRACT", "SEXT", "NEG", "OUT", "ROOT", "MOV",
         "SUBR",     # b - a   (SUB with the operands swapped: in place on a)
-        "ITEN"]     # c ? b : a (ITE with the operands swapped: in place on a)
+        "ITEN",     # c ? b : a (ITE with the operands swapped: in place on a)
+        "LEAFD",    # 256-bit LEAF straight into slot = variant, loads left in flight
+        "WAITVM"]   # wait for in-flight LEAFD loads (inserted by the translator)
 AOP = {n: i for i, n in enumerate(AOPS)}
 V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
 NVAR = 32
@@ -86,6 +88,7 @@ SUPPORT.update({n: SUPPORT[n] | V_IP for n in ("ADD", "SUB", "AND", "OR", "XOR",
                                                "ITE")})
 SUPPORT["SUBR"] = _RM | V_IP
 SUPPORT["ITEN"] = V_ROOT | V_IP
+SUPPORT["WAITVM"] = 0
 # families whose result is never masked (canonical inputs give canonical
 # outputs) and families where DC only matters for one-limb results
 NO_MASK = {"AND", "OR", "XOR", "EQ", "ULT", "ULE", "ITE", "ITEN", "MOV", "CONST", "NOP", "HALT",
@@ -95,6 +98,8 @@ DC_NEEDS_W32 = {"ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "ITE", "EXTRACT"
 
 
 def canon_var(name: str, var: int) -> int:
+    if name == "LEAFD":
+        return var & (NREG - 1)      # the variant is the destination slot
     var &= SUPPORT[name]
     if name in NO_MASK:
         var &= ~V_MASK
@@ -770,12 +775,15 @@ def _soa_step(a: Asm):
     a("s_addc_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 1), s(S_T + 5)))
 
 
-def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int):
+def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int, wait_vm: bool = False):
     """regs -> SoA buffer ptr[(8*row + j) * stride + lane], active lanes only,
-    when ptr != 0.  Clobbers S_T..S_T+7, T[0]."""
+    when ptr != 0 (after the in-flight loads into regs with wait_vm).
+    Clobbers S_T..S_T+7, T[0]."""
     skip = a.uniq("nost")
     a("s_cmp_lg_u64 %s, 0" % ptr_op)
     a("s_cbranch_scc0 %s" % skip)
+    if wait_vm:
+        a("s_waitcnt vmcnt(0)")
     _soa_base(a, ptr_op, row_sgpr)
     a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
     a("s_mov_b64 %s, exec" % sp(S_T + 6))
@@ -820,8 +828,8 @@ def mul64_const(a: Asm, z: List[int], klo: int, khi: int, t: List[int]):
     (t[3] is read as don't-care, never written).  hi cross terms with one
     v_mul_lo and the low word of a mad; the full low product with a mad."""
     a("v_mul_lo_u32 %s, %s, %s" % (v(t[2]), v(z[0]), s(khi)))                        # lo*khi
-    a("v_mad_u64_u32 %s, %s, %s, %s, %s" % (vp(t[0]), sp(S_T + 6), v(z[1]), s(klo), vp(t[2])))
-    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(z[0]), sp(S_T + 6), v(z[0]), s(klo)))   # lo*klo
+    a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(t[0]), v(z[1]), s(klo), vp(t[2])))
+    a("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (vp(z[0]), v(z[0]), s(klo)))   # lo*klo
     a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[0])))
 
 
@@ -829,7 +837,7 @@ def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
     """SplitMix64 on the per-lane state st = (lo, hi): st += GOLD; z =
     mix(st).  Constants in SGPRs (load_sm64_consts); t: 4 temps with
     t[0]:t[1] and t[2]:t[3] aligned; t[3] holds GOLD_HI on entry (set once
-    per leaf, preserved).  Uses vcc and s[S_T+6:S_T+7]."""
+    per leaf, preserved).  Uses vcc (also as the mads' junk carry-out)."""
     a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(K_GOLD_LO), v(st[0])))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[3]), v(st[1])))
     a("v_lshrrev_b64 %s, 30, %s" % (vp(t[0]), vp(st[0])))
@@ -857,17 +865,20 @@ def _class_mask(a: Asm, out: int, lo_sgpr: Optional[int], hi_sgpr: Optional[int]
         a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(out), s(hi_sgpr), v(cls)))
 
 
-def _gen_leaf(a: Asm, bank: int):
-    """X[0..7] <- generator value of leaf C for candidate first + lane.
+def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = True):
+    """dst[0..7] (default X) <- generator value of leaf C for candidate
+    first + lane; the boundary / pool lanes arrive by loads into dst, waited
+    for unless wait=False (LEAFD: the translator places the WAITVM).
     Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's four SplitMix64
     words are computed for every lane (the small class is its first word);
     the boundary and pool classes then overwrite their lanes under exec.
     Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
     pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
     st, z, tt = [T[0], T[1]], [T[2], T[3]], [T[4], T[5], T[6], T[7]]
-    cls, lo = T[8], T[9]
+    cls, lo = T[8], z[0]
     g = S_CUR
     a("s_load_dwordx2 %s, %s, 0x10" % (sp(S_T), IN["desc"]))       # gen table
+    a("s_load_dwordx2 %s, %s, 0x38" % (sp(S_T + 6), IN["desc"]))   # boundary table
     a("s_lshl_b32 %s, %s, 5" % (s(S_T + 2), s(fld(bank, F_C))))
     load_sm64_consts(a)
     a("s_waitcnt lgkmcnt(0)")
@@ -884,9 +895,8 @@ def _gen_leaf(a: Asm, bank: int):
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), v(st[0])))
     a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), v(st[1])))
     sm64(a, st, z, tt)
-    a("v_mov_b32 %s, 100" % v(tt[0]))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), v(tt[0])))
-    a("v_mov_b32 %s, %s" % (v(lo), v(z[0])))
+    a("s_movk_i32 %s, 100" % s(S_T))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), s(S_T)))
     # ---- uniform words for every lane; small lanes keep the first 64 bits
     for j in range(0, 8, 2):
         sm64(a, st, [X[j], X[j + 1]], tt)
@@ -894,47 +904,33 @@ def _gen_leaf(a: Asm, bank: int):
     lab = exec_begin(a, S_T + 2, S_T + 4)
     moves(a, X[2:], [None] * 6)
     exec_end(a, lab, S_T + 4)
+    dst = X if dst is None else dst
+    if dst != X:
+        moves(a, dst, X)
     # ---- boundary: pct_small <= cls < pct_boundary -------------------------
     _class_mask(a, S_T + 2, g + 4, g + 5, cls)
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     lab = a.uniq("gbd")
     a("s_cbranch_execz %s" % lab)
-    kind, k, bit, hi = tt
-    a("v_mov_b32 %s, 6" % v(kind))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(kind), v(lo), v(kind)))
-    a("v_mov_b32 %s, 0x9e3779b1" % v(k))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(k), v(lo), v(k)))
+    # one load from the context's boundary table (mg_api.cpp
+    # mg_boundary_table): entry kind * 256 + p, p = width - 1 for kind 2
+    # (1 << (w-1)) and k otherwise; masked to the width by the handler
+    kind, k, bit = tt[0], tt[1], tt[2]
+    a("v_mul_hi_u32 %s, %s, 6" % (v(kind), v(lo)))
+    a("s_mov_b32 %s, 0x9e3779b1" % s(S_T))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(k), v(lo), s(S_T)))
     a("v_mul_hi_u32 %s, %s, %s" % (v(k), v(k), s(g + 0)))
-    # bit = kind==2 ? w-1 : (kind==1 ? 0 : k)
-    a("s_sub_u32 %s, %s, 1" % (s(S_T), s(g + 0)))
-    a("v_mov_b32 %s, %s" % (v(bit), s(S_T)))
+    a("s_sub_u32 %s, %s, 1" % (s(S_T + 1), s(g + 0)))
+    a("v_mov_b32 %s, %s" % (v(bit), s(S_T + 1)))
     a("v_cmp_eq_u32 vcc, 2, %s" % v(kind))
     a("v_cndmask_b32 %s, %s, %s, vcc" % (v(k), v(k), v(bit)))
-    a("v_cmp_eq_u32 vcc, 1, %s" % v(kind))
-    a("v_cndmask_b32 %s, %s, 0, vcc" % (v(k), v(k)))
-    # one-hot for kind in {1,2,4,5}: limb (k>>5) = 1 << (k&31)
-    a("v_lshrrev_b32 %s, 5, %s" % (v(hi), v(k)))
-    a("v_lshlrev_b32 %s, %s, 1" % (v(bit), v(k)))
-    a("v_cmp_ne_u32 vcc, 0, %s" % v(kind))
-    a("v_cmp_ne_u32_e64 %s, 3, %s" % (sp(S_T), v(kind)))
-    a("s_and_b64 vcc, vcc, %s" % sp(S_T))
-    a("v_cndmask_b32 %s, -1, %s, vcc" % (v(hi), v(hi)))
-    for j in range(8):
-        a("v_cmp_eq_u32 vcc, %d, %s" % (j, v(hi)))
-        a("v_cndmask_b32 %s, 0, %s, vcc" % (v(X[j]), v(bit)))
-    # addend: +1 (kind 4), -1 (kinds 3, 5), else 0
-    a("v_cmp_eq_u32 vcc, 4, %s" % v(kind))
-    a("v_cndmask_b32 %s, 0, 1, vcc" % v(k))
-    a("v_cmp_eq_u32 vcc, 3, %s" % v(kind))
-    a("v_cmp_eq_u32_e64 %s, 5, %s" % (sp(S_T), v(kind)))
-    a("s_or_b64 vcc, vcc, %s" % sp(S_T))
-    a("v_cndmask_b32 %s, 0, -1, vcc" % v(hi))
-    a("v_cndmask_b32 %s, %s, -1, vcc" % (v(k), v(k)))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(X[0]), v(X[0]), v(k)))
-    for j in range(1, 8):
-        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(X[j]), v(X[j]), v(hi)))
+    a("v_lshl_add_u32 %s, %s, 8, %s" % (v(k), v(kind), v(k)))
+    a("v_lshlrev_b32 %s, 5, %s" % (v(k), v(k)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(k), sp(S_T + 6)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(k), sp(S_T + 6)))
     a.label(lab)
     # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
+    # the pool is stored as (v-1, v, v+1) triples: entry e * 3 + delta
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
     _class_mask(a, S_T + 2, g + 5, None, cls)
     a("s_cmp_lg_u32 %s, 0" % s(g + 2))
@@ -942,25 +938,19 @@ def _gen_leaf(a: Asm, bank: int):
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     lab = a.uniq("gpl")
     a("s_cbranch_execz %s" % lab)
-    e, delta, t2, hi = tt
+    e, delta = tt[0], tt[1]
     a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(g + 2)))
-    a("v_lshlrev_b32 %s, 5, %s" % (v(e), v(e)))
-    a("v_add_u32 %s, %s, %s" % (v(e), s(g + 1), v(e)))
-    a("global_load_dwordx4 v[%d:%d], %s, %s" % (X[0], X[3], v(e), sp(S_CONST)))
-    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (X[4], X[7], v(e), sp(S_CONST)))
-    a("v_mov_b32 %s, 0x85ebca6b" % v(delta))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(delta), v(lo), v(delta)))
-    a("v_mov_b32 %s, 3" % v(t2))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(delta), v(delta), v(t2)))
-    a("v_cmp_eq_u32 vcc, 0, %s" % v(delta))
-    a("v_cndmask_b32 %s, 0, -1, vcc" % v(hi))
-    a("v_add_u32 %s, -1, %s" % (v(t2), v(delta)))
-    a("s_waitcnt vmcnt(0)")
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(X[0]), v(X[0]), v(t2)))
-    for j in range(1, 8):
-        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(X[j]), v(X[j]), v(hi)))
+    a("s_mov_b32 %s, 0x85ebca6b" % s(S_T))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(delta), v(lo), s(S_T)))
+    a("v_mul_hi_u32 %s, %s, 3" % (v(delta), v(delta)))
+    a("v_mad_u32_u24 %s, %s, 3, %s" % (v(e), v(e), v(delta)))
+    a("v_lshl_add_u32 %s, %s, 5, %s" % (v(e), v(e), s(g + 1)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(e), sp(S_CONST)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(e), sp(S_CONST)))
     a.label(lab)
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
+    if wait:
+        a("s_waitcnt vmcnt(0)")                   # boundary and pool loads
 
 
 def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
@@ -987,6 +977,37 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     _store_soa(a, X, IN["lout"], fld(bank, F_C))
     a.label(lab_done)
     finish(a, bank, X, root, mask)
+
+
+def h_leafd(a: Asm, bank: int, slot: int):
+    """256-bit LEAF into slot ``slot`` (the variant): the value is built
+    straight in the slot's registers and its memory loads (input SoA, or the
+    generator's boundary / pool lanes) are left in flight, so a run of leaves
+    pays one memory latency at the WAITVM the translator puts before the
+    first instruction that touches a pending slot."""
+    fd = [FB + 8 * slot + j for j in range(8)]
+    prologue(a, bank)
+    lab_gen, lab_done = a.uniq("lgen"), a.uniq("ldone")
+    a("s_bitcmp1_b32 %s, 0" % IN["mode"])
+    a("s_cbranch_scc1 %s" % lab_gen)
+    _soa_base(a, IN["leaves"], fld(bank, F_C))
+    a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
+    for j in range(8):
+        a("global_load_dword %s, %s, %s" % (v(fd[j]), v(T[0]), sp(S_T)))
+        if j < 7:
+            _soa_step(a)
+    a("s_branch %s" % lab_done)
+    a.label(lab_gen)
+    _gen_leaf(a, bank, dst=fd, wait=False)
+    _store_soa(a, fd, IN["lout"], fld(bank, F_C), wait_vm=True)
+    a.label(lab_done)
+    dispatch(a, 1 - bank)
+
+
+def h_waitvm(a, bank, root, mask, dc=False, w32=False, ip=False):
+    prologue(a, bank)
+    a("s_waitcnt vmcnt(0)")
+    dispatch(a, 1 - bank)
 
 
 # ---------------------------------------------------------------------------
@@ -1522,6 +1543,7 @@ CHEAP = {
     "XOR": h_xor, "NOT": h_not, "EQ": h_eq, "ULT": h_ult, "ULE": h_ule, "SLT": h_slt,
     "SLE": h_sle, "ITE": h_ite, "CONCAT": h_concat, "EXTRACT": h_extract, "SEXT": h_sext,
     "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov, "SUBR": h_subr, "ITEN": h_iten,
+    "WAITVM": h_waitvm,
 }
 HEAVY = {"MUL": "MUL", "UMULNO": "UMULNO", "SHL": "SHL", "LSHR": "LSHR", "ASHR": "ASHR",
          "UDIV": "DIV", "UREM": "DIV", "SDIV": "DIV", "SREM": "DIV", "SMOD": "DIV"}
@@ -1564,7 +1586,9 @@ def generate() -> List[str]:
             dc_v, w32_v, ip_v = bool(var & V_DC), bool(var & V_W32), bool(var & V_IP)
             for bank in (0, 1):
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
-                if name in CHEAP:
+                if name == "LEAFD":
+                    h_leafd(a, bank, var)
+                elif name in CHEAP:
                     CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
                 else:
                     bits = var | (DIV_CODE.get(name, 0) << 4)

@@ -39,6 +39,8 @@ struct mg_ctx {
     uint32_t hoff[MGA_NUM_HANDLERS] = {0};
     uint32_t lds_slots = 6;
     bool use_asm = true;
+    // generator boundary-value table (device, 48 KiB; MG_BTAB_WORDS)
+    uint32_t* d_btab = nullptr;
     // grow-only device workspace for synchronous calls
     void* ws = nullptr;
     size_t ws_size = 0;
@@ -186,26 +188,59 @@ static bool has_w32(uint32_t op) {
     }
 }
 
+// register slots an IR instruction reads or writes (bit mask)
+static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
+    switch (op) {
+    case MG_NOP: return 0;
+    case MG_CONST: case MG_LEAF: case MG_RELOAD: return 1u << d;
+    case MG_SPILL: case MG_OUT: case MG_ROOT: return 1u << a;
+    case MG_NOT: case MG_NEG: case MG_MOV: case MG_EXTRACT: case MG_SEXT:
+        return (1u << d) | (1u << a);
+    case MG_ITE: return (1u << d) | (1u << a) | (1u << b) | (1u << c);
+    default: return (1u << d) | (1u << a) | (1u << b);
+    }
+}
+
 static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
                       uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
     pool.base = n_consts;
     const uint32_t ones = pool.add(mask_lt(256));
-    rec.assign((size_t)(n_ins + 2) * 8, 0);
+    rec.clear();
+    rec.reserve((size_t)(n_ins + 4) * 8);
     // clean[s]: limbs 1..7 of slot s are known to be zero (its last value had
     // at most 32 bits); registers start uninitialised
     bool clean[MG_NREG];
     for (int k = 0; k < MG_NREG; ++k) clean[k] = false;
+    // slots whose LEAFD loads may still be in flight: a WAITVM record goes
+    // before the first instruction that reads or writes one of them
+    uint32_t pending = 0;
     int bank = 0;
+    auto emit = [&rec]() {
+        rec.resize(rec.size() + 8, 0);
+        return rec.data() + rec.size() - 8;
+    };
     for (uint32_t pc = 0; pc <= n_ins; ++pc) {
-        uint32_t* r = rec.data() + (size_t)pc * 8;
         if (pc == n_ins) {          // HALT, then one zeroed record (prefetch pad)
-            r[0] = hoff[MGA_HID(MGA_HALT, 0, bank)];
+            if (pending) {
+                emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
+                bank = 1 - bank;
+            }
+            emit()[0] = hoff[MGA_HID(MGA_HALT, 0, bank)];
+            emit();
             break;
         }
         const uint32_t* in = code + 4 * pc;
         const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
         const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
                        c = (in[1] >> 24) & 0xFF;
+        const bool leafd = op == MG_LEAF && w == 256;
+        if (pending && (slots_touched(op, d, a, b, c) & pending)) {
+            emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
+            bank = 1 - bank;
+            pending = 0;
+        }
+        if (leafd) pending |= 1u << d;
+        uint32_t* r = emit();
         uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
         const bool writes = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
         // result fits one limb: Bool results, or values of at most 32 bits
@@ -221,7 +256,8 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         case MG_CONST: aop = MGA_CONST; r[5] = imm * 32u; break;
         case MG_LEAF:
             aop = MGA_LEAF; r[4] = imm;
-            if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
+            if (leafd) { aop = MGA_LEAFD; var = d; }
+            else if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
             break;
         case MG_SPILL:
             if (imm < n_lds) { aop = MGA_SPILL_LDS; r[5] = imm * 2u * 256u * 16u; }
@@ -338,6 +374,29 @@ int mg_config(uint32_t* out, uint32_t n) {
     return MG_OK;
 }
 
+// Boundary values of the candidate generator as a table the LEAF handler
+// indexes by kind * 256 + p (oracle/gen_ref.py gen_leaf, boundary class):
+// kind 0: 0, 1: 1, 2: 1 << p (p = width - 1), 3: 2^256 - 1, 4: (1 << p) + 1,
+// 5: (1 << p) - 1 (p = k); the handler masks to the width afterwards.
+#define MG_BTAB_WORDS (6 * 256 * 8)
+static void mg_boundary_table(uint32_t* t) {
+    memset(t, 0, MG_BTAB_WORDS * 4);
+    for (uint32_t p = 0; p < 256; ++p) {
+        uint32_t* e1 = t + (1 * 256 + p) * 8;
+        uint32_t* e2 = t + (2 * 256 + p) * 8;
+        uint32_t* e3 = t + (3 * 256 + p) * 8;
+        uint32_t* e4 = t + (4 * 256 + p) * 8;
+        uint32_t* e5 = t + (5 * 256 + p) * 8;
+        e1[0] = 1;
+        e2[p >> 5] = 1u << (p & 31);
+        for (int j = 0; j < 8; ++j) e3[j] = ~0u;
+        e4[p >> 5] = 1u << (p & 31);
+        e4[0] += 1;                              // p = 0: 1 + 1 = 2
+        for (uint32_t j = 0; j < (p >> 5); ++j) e5[j] = ~0u;
+        e5[p >> 5] = (1u << (p & 31)) - 1;
+    }
+}
+
 int mg_init(int device, mg_ctx** out) {
     if (!out) return MG_E_ARG;
     *out = nullptr;
@@ -368,6 +427,16 @@ int mg_init(int device, mg_ctx** out) {
         mg_free(ctx);
         return MG_E_HIP;
     }
+    {
+        std::vector<uint32_t> bt(MG_BTAB_WORDS);
+        mg_boundary_table(bt.data());
+        if (hipMalloc(&ctx->d_btab, MG_BTAB_WORDS * 4) != hipSuccess ||
+            hipMemcpy(ctx->d_btab, bt.data(), MG_BTAB_WORDS * 4, hipMemcpyHostToDevice) !=
+                hipSuccess) {
+            mg_free(ctx);
+            return MG_E_HIP;
+        }
+    }
     *out = ctx;
     return MG_OK;
 }
@@ -376,6 +445,7 @@ void mg_free(mg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
+    if (ctx->d_btab) (void)hipFree(ctx->d_btab);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -463,13 +533,30 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     std::vector<uint32_t> rec;
     MaskPool pool;
     translate(ctx->hoff, code, n_ins, n_consts, kernel_lds_slots(ctx, n_spill_slots), rec, pool);
-    const uint32_t n_const_all = n_consts + (uint32_t)(pool.words.size() / 8);
+    // generator pools expanded to (v - 1, v, v + 1) triples (mod 2^256), so
+    // the pool class is one indexed load (pool[e] + delta - 1, gen_ref.py)
+    const uint32_t n_masks = (uint32_t)(pool.words.size() / 8);
+    std::vector<uint32_t> pm(consts ? (size_t)n_consts * 24 : 0);
+    for (uint32_t c = 0; c < n_consts; ++c) {
+        const uint32_t* v = consts + (size_t)c * 8;
+        uint32_t* o = pm.data() + (size_t)c * 24;
+        uint64_t bm = 1, bp = 1;                 // borrow of v - 1, carry of v + 1
+        for (int j = 0; j < 8; ++j) {
+            o[j] = v[j] - (uint32_t)bm;
+            bm = bm && v[j] == 0;
+            o[8 + j] = v[j];
+            o[16 + j] = v[j] + (uint32_t)bp;
+            bp = bp && v[j] == 0xFFFFFFFFu;
+        }
+    }
+    const uint32_t n_const_all = n_consts + n_masks + n_consts * 3;
     // device leaf descriptors: byte pool offsets and the per-leaf stream salt
     std::vector<mg_leafgen_dev> gdev(n_leaves);
     for (uint32_t i = 0; i < n_leaves; ++i) {
         const uint64_t salt = (prog_seed * 0xD1B54A32D192ED03ull) ^
                               ((uint64_t)(i + 1) * 0x8CB92BA72F3D8DD7ull);
-        gdev[i] = {leaves[i].width, leaves[i].pool_off * 32u, leaves[i].pool_n,
+        gdev[i] = {leaves[i].width, (n_consts + n_masks + 3 * leaves[i].pool_off) * 32u,
+                   leaves[i].pool_n,
                    leaves[i].pct_uniform, leaves[i].pct_small, leaves[i].pct_boundary,
                    (uint32_t)salt, (uint32_t)(salt >> 32)};
     }
@@ -486,6 +573,9 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     if (!pool.words.empty())
         memcpy(blob.data() + off_const + (size_t)n_consts * 32, pool.words.data(),
                pool.words.size() * 4);
+    if (!pm.empty())
+        memcpy(blob.data() + off_const + (size_t)(n_consts + n_masks) * 32, pm.data(),
+               pm.size() * 4);
     if (gen_b) memcpy(blob.data() + off_gen, gdev.data(), gen_b);
     memcpy(blob.data() + off_rec, rec.data(), rec_b);
     void* d = nullptr;
@@ -502,6 +592,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     desc.n_probes = n_probes;
     desc.prog_seed = prog_seed;
     desc.xcode = (const uint32_t*)(db + off_rec);
+    desc.btab = ctx->d_btab;
     memcpy(blob.data() + off_desc, &desc, sizeof desc);
     hipError_t e = hipMemcpy(d, blob.data(), total, hipMemcpyHostToDevice);
     if (e != hipSuccess) {

@@ -10,7 +10,8 @@
  * fields): 8 words, read by the kernels with one scalar load. */
 struct mg_leafgen_dev {
     uint32_t width;
-    uint32_t pool_off_b;       /* byte offset of the pool in the const table  */
+    uint32_t pool_off_b;       /* byte offset (from the const table) of the
+                                  leaf's pool expanded to v-1, v, v+1 triples */
     uint32_t pool_n;
     uint32_t pct_uniform, pct_small, pct_boundary;
     uint32_t salt_lo, salt_hi; /* prog_seed*C1 ^ (leaf+1)*C2 (oracle/gen_ref) */
@@ -27,6 +28,9 @@ struct mg_pdesc {
     uint32_t n_probes;
     uint64_t prog_seed;        /* per-program stream salt (generator mode) */
     const uint32_t* xcode;     /* translated 8-word records (mg_interp_asm) */
+    const uint32_t* btab;      /* generator boundary table (context-wide):
+                                  [kind 0..5][p 0..255] x 8 words, see
+                                  mg_boundary_table in mg_api.cpp         */
 };
 
 /* Per-launch arguments (passed by value). */

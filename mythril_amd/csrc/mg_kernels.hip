@@ -311,14 +311,10 @@ DEV void gen_leaf(uint64_t seed, uint32_t leaf, uint64_t idx, cgen* g, cu32* con
     } else if (cls >= g->pct_boundary && pool_n > 0) {
         const uint32_t e = mulhi32(lo, pool_n);
         const uint32_t delta = mulhi32(lo * 0x85EBCA6Bu, 3u);
-        cu32* p = consts + (size_t)g->pool_off_b / 4 + (size_t)e * 8;
+        // pool expanded to (v - 1, v, v + 1) triples at load (mg_api.cpp)
+        cu32* p = consts + (size_t)g->pool_off_b / 4 + (size_t)(e * 3 + delta) * 8;
 #pragma unroll
         for (int j = 0; j < 8; ++j) out[j] = p[j];
-        uint32_t add[8];
-        add[0] = delta - 1u;
-#pragma unroll
-        for (int j = 1; j < 8; ++j) add[j] = delta == 0 ? 0xFFFFFFFFu : 0u;
-        add256(out, add, out);
     } else {                    // uniform (also the pool class without a pool)
 #pragma unroll
         for (int j = 0; j < 8; j += 2) {

@@ -244,14 +244,27 @@ class Wave:
         self.swrite(op, _bool_to_mask(b & _mask_to_bool(self.exec)))
 
     # ---- pending loads -----------------------------------------------------
-    def _defer(self, kind: str, key, apply):
+    def _defer(self, kind: str, key, apply, lanes=None):
+        """Queue a load's register write until its counter is waited for.
+        Two outstanding vector-memory loads may target one register only
+        with disjoint lane sets (VMEM returns in issue order, so the writes
+        then commute); anything else is an error."""
         if key in self.pending:
-            raise SimError("overlapping pending loads into %s%d" % key)
-        self.pending[key] = (kind, apply)
+            kd, prev, plan = self.pending[key]
+            if not (kind == kd == "vm" and lanes is not None and plan is not None
+                    and not np.any(lanes & plan)):
+                raise SimError("overlapping pending loads into %s%d" % key)
+
+            def both(prev=prev, apply=apply):
+                prev()
+                apply()
+            self.pending[key] = (kind, both, plan | lanes)
+            return
+        self.pending[key] = (kind, apply, lanes)
 
     def _wait(self, kind: str):
-        for key in [k for k, (kd, _) in self.pending.items() if kd == kind]:
-            _, apply = self.pending.pop(key)
+        for key in [k for k, (kd, _, _) in self.pending.items() if kd == kind]:
+            _, apply, _ = self.pending.pop(key)
             apply()
 
     # ---- execution -----------------------------------------------------------
@@ -506,8 +519,12 @@ class Wave:
         srcs = [self.vread(a[1 + i], "SRC%d" % i) for i in range(n)]
         self.vwrite(a[0], f(*srcs) & np.uint64(M32))
 
-    def i_v_add_u32_clamp(self, a, pc):
-        pass
+    def i_v_mad_u32_u24(self, a, pc):
+        m24 = np.uint64(0xFFFFFF)
+        self._vop3(a, lambda x, y, z: (x & m24) * (y & m24) + z, 3)
+
+    def i_v_lshl_add_u32(self, a, pc):
+        self._vop3(a, lambda x, y, z: (x << (y & np.uint64(31))) + z, 3)
 
     def i_v_min3_u32(self, a, pc):
         self._vop3(a, lambda x, y, z: np.minimum(np.minimum(x, y), z), 3)
@@ -697,7 +714,7 @@ class Wave:
         for i in range(n):
             def apply(i=i):
                 self.v[dst + i] = np.where(act, np.array(vals[i], dtype=np.uint64), self.v[dst + i])
-            self._defer("vm", ("v", dst + i), apply)
+            self._defer("vm", ("v", dst + i), apply, lanes=act.copy())
 
     def i_global_store_dword(self, a, pc):
         addrs = self._gaddr(a[0], a[2], a[3:])
@@ -806,7 +823,7 @@ def translate(prog, n_lds: int):
     _, table = body_and_table()
     code = np.ascontiguousarray(prog.code, dtype=np.uint32)
     tab = np.array(table, dtype=np.uint32)
-    rec = np.zeros((prog.n_ins + 2) * 8, dtype=np.uint32)
+    rec = np.zeros((2 * prog.n_ins + 3) * 8, dtype=np.uint32)
     masks = np.zeros(8 * 4096, dtype=np.uint32)
     nr, nm = C.c_uint32(0), C.c_uint32(0)
     rc = lib.mg_translate(code.ctypes.data_as(C.c_void_p), prog.n_ins, prog.consts.shape[0], n_lds,
@@ -821,6 +838,30 @@ def translate(prog, n_lds: int):
 GOLD = 0x9E3779B97F4A7C15
 
 
+def _limbs(v: int) -> list:
+    return [(v >> (32 * j)) & M32 for j in range(8)]
+
+
+def boundary_table() -> np.ndarray:
+    """The generator's boundary table as mg_api.cpp builds it: entry
+    kind * 256 + p = 0, 1, 1 << p, 2^256 - 1, (1 << p) + 1, (1 << p) - 1."""
+    t = np.zeros((6, 256, 8), dtype=np.uint32)
+    for p in range(256):
+        for kind, val in enumerate((0, 1, 1 << p, (1 << 256) - 1, (1 << p) + 1, (1 << p) - 1)):
+            t[kind, p] = _limbs(val)
+    return t
+
+
+def expanded_pool(consts: np.ndarray) -> np.ndarray:
+    """(v - 1, v, v + 1) mod 2^256 for every constant (mg_load_program)."""
+    out = np.zeros((consts.shape[0], 3, 8), dtype=np.uint32)
+    for c in range(consts.shape[0]):
+        v = sum(int(consts[c, j]) << (32 * j) for j in range(8))
+        for d in range(3):
+            out[c, d] = _limbs((v + d - 1) % (1 << 256))
+    return out
+
+
 def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
              active: int = (1 << NL) - 1, rcp_noise: float = 0.0, want_leaves: bool = False):
     """Run one 64-lane wave of the assembly interpreter on a compiled
@@ -831,8 +872,9 @@ def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
     lines, _ = body_and_table()
     rec, masks = translate(prog, n_lds)
     mem = Memory()
-    consts = np.concatenate([np.ascontiguousarray(prog.consts, dtype=np.uint32).reshape(-1),
-                             masks]).astype(np.uint32)
+    pc = np.ascontiguousarray(prog.consts, dtype=np.uint32).reshape(-1, 8)
+    consts = np.concatenate([pc.reshape(-1), masks, expanded_pool(pc).reshape(-1)]).astype(np.uint32)
+    pool_base = pc.shape[0] + len(masks) // 8         # expanded pool, in 32-byte entries
     c_base = mem.alloc(consts.tobytes(), "consts")
     x_base = mem.alloc(rec.astype(np.uint32).tobytes(), "records")
     n_leaves = len(prog.leaves)
@@ -842,11 +884,12 @@ def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
         seed, prog_seed, first, leafgens = gen
         for i, g in enumerate(leafgens):
             salt = ((prog_seed * 0xD1B54A32D192ED03) ^ ((i + 1) * 0x8CB92BA72F3D8DD7)) & M64
-            gdev[i] = [g.width, g.pool_off * 32, g.pool_n, g.pct_uniform, g.pct_small,
-                       g.pct_boundary, salt & M32, salt >> 32]
+            gdev[i] = [g.width, (pool_base + 3 * g.pool_off) * 32, g.pool_n, g.pct_uniform,
+                       g.pct_small, g.pct_boundary, salt & M32, salt >> 32]
     g_base = mem.alloc(gdev.tobytes(), "gen")
-    desc = struct.pack("<QQQIIIIQQ", 0, c_base, g_base, prog.n_ins, n_leaves, 0, 0,
-                       prog_seed & M64, x_base)
+    b_base = mem.alloc(boundary_table().tobytes(), "btab")
+    desc = struct.pack("<QQQIIIIQQQ", 0, c_base, g_base, prog.n_ins, n_leaves, 0, 0,
+                       prog_seed & M64, x_base, b_base)
     d_base = mem.alloc(desc, "desc")
     lv = soa if soa is not None else np.zeros((max(1, n_leaves), 8, NL), dtype=np.uint32)
     l_base = mem.alloc(np.ascontiguousarray(lv, dtype=np.uint32).tobytes(), "leaves")
