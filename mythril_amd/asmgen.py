@@ -1092,19 +1092,52 @@ def body_mul(a: Asm):
     heavy_finish(a, R)
 
 
+def clz256(a: Asm, vals: List[int], out: int, t: List[int]):
+    """Leading zeros of a 256-bit value (256 for zero): min over limbs of
+    (7-j)*32 + ffbh(limb j), ffbh(0) = ~0 kept saturated by a clamped add.
+    t: 8 temps (may include out).  Clobbers s[S_T..S_T+7]."""
+    for j in range(8):
+        a("s_movk_i32 %s, 0x%x" % (s(S_T + j), (7 - j) * 32))
+    for j in range(8):
+        a("v_ffbh_u32 %s, %s" % (v(t[j]), v(vals[j])))
+        a("v_add_u32_e64 %s, %s, %s clamp" % (v(t[j]), v(t[j]), s(S_T + j)))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(t[0]), v(t[0]), v(t[1]), v(t[2])))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(t[3]), v(t[3]), v(t[4]), v(t[5])))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(out), v(t[0]), v(t[3]), v(t[6])))
+    a("s_movk_i32 %s, 0x100" % s(S_T))
+    a("v_min3_u32 %s, %s, %s, %s" % (v(out), v(out), v(t[7]), s(S_T)))
+
+
 def body_umulno(a: Asm):
-    """R0 = (x*y < 2^W): the 512-bit product has no bit at or above W (the
-    width masks are all-ones for W = 256, so the low columns add nothing)."""
+    """R0 = (x*y < 2^W).  With p, q the bit lengths of x and y,
+    2^(p+q-2) <= x*y < 2^(p+q): no overflow when p + q <= W, overflow when
+    p + q >= W + 2.  Only the lanes with p + q == W + 1 need the product;
+    the 512-bit product (columns >= W OR-ed; the width masks are all-ones
+    for W = 256) runs only when some lane of the wave has one."""
     a.label(".Lbody_UMULNO_%=")
     heavy_prologue(a)
     a.read_slot(X, cur(F_A))
     a.read_slot(Y, cur(F_B))
     a("s_waitcnt lgkmcnt(0)")
+    sz = T[8]                                   # clz(x) + clz(y) = 512 - (p + q)
+    clz256(a, X, sz, [T[8], T[9], T[10], T[11], T[0], T[1], T[2], T[3]])
+    clz256(a, Y, T[4], [T[4], T[5], T[6], T[7], T[0], T[1], T[2], T[3]])
+    a("v_add_u32 %s, %s, %s" % (v(sz), v(sz), v(T[4])))
+    a("s_sub_u32 %s, 511, %s" % (s(S_X), s(cur(F_W))))                  # 511 - W
+    a("v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_X + 2), s(S_X), v(sz)))     # p + q == W + 1
+    a("v_cmp_lt_u32_e64 %s, %s, %s" % (sp(S_X + 4), s(S_X), v(sz)))     # p + q <= W
+    lab = a.uniq("unf")
+    a("s_cmp_eq_u64 %s, 0" % sp(S_X + 2))
+    a("s_cbranch_scc1 %s" % lab)
     col_product(a, X, Y, 16, hi_or=T[7])
     a("v_cmp_eq_u32 vcc, 0, %s" % v(T[7]))
-    a("v_cndmask_b32 %s, 0, 1, vcc" % v(R[0]))
-    for j in range(1, 8):
-        a("v_mov_b32 %s, 0" % v(R[j]))
+    a("s_and_b64 vcc, vcc, %s" % sp(S_X + 2))
+    a("s_or_b64 %s, %s, vcc" % (sp(S_X + 4), sp(S_X + 4)))
+    a.label(lab)
+    a("v_cndmask_b32_e64 %s, 0, 1, %s" % (v(R[0]), sp(S_X + 4)))
+    a("v_mov_b32 %s, 0" % v(R[1]))
+    for j in range(2, 8, 2):
+        a("v_mov_b64 %s, 0" % vp(R[j]))
     a("s_and_b32 %s, %s, 1" % (s(S_VAR), s(S_VAR)))      # Bool result: never masked
     heavy_finish(a, R)
 
