@@ -35,6 +35,7 @@ of the inline asm in ``mg_interp_asm.hip``) and ``csrc/mg_asm_handlers.h``
 from __future__ import annotations
 
 import os
+import re
 from typing import Dict, List, Optional
 
 NREG = 16                  # register-file slots (MG_NREG)
@@ -237,17 +238,19 @@ def finish(a: Asm, bank: int, res: List[int], root: bool, mask: bool):
 
 def write_narrow(a: Asm, bank: int, r0: str, dc: bool):
     """F[D] = (r0, 0, ..., 0); with dc the upper limbs are already zero.
-    (R1 is used as the zero half of the first 64-bit move.)"""
+    The first pair is one v_pk_mov_b32 of r0's half and an inline zero."""
     if dc:
         a.idx_on(fld(bank, F_D), "DST")
         a("v_mov_b32 %s, %s" % (v(F[0]), r0))
         a.idx_off()
         return
-    if r0 != v(R[0]):
+    m = re.fullmatch(r"v(\d+)", r0)
+    if not m:
         a("v_mov_b32 %s, %s" % (v(R[0]), r0))
-    a("v_mov_b32 %s, 0" % v(R[1]))
+        r0 = v(R[0])
+    n = int(re.fullmatch(r"v(\d+)", r0).group(1))
     a.idx_on(fld(bank, F_D), "DST")
-    a("v_mov_b64 %s, %s" % (vp(F[0]), vp(R[0])))
+    a("v_pk_mov_b32 %s, %s, 0 op_sel:[%d,0]" % (vp(F[0]), vp(n & ~1), n & 1))   # (r0, 0)
     for j in range(2, 8, 2):
         a("v_mov_b64 %s, 0" % vp(F[j]))
     a.idx_off()
@@ -1055,20 +1058,22 @@ def col_product(a: Asm, x: List[int], y: List[int], ncols: int, out: Optional[Li
     and the accumulator shifts down one word.  Column c < 8 goes to out[c]
     (if given); with hi_or, columns >= 8 and the bits of columns < 8 outside
     the masks s[S_M+c] (loaded and waited for) are OR-ed into v[hi_or].
-    Uses T4..T6, TMP, vcc, s[S_T+6:S_T+7]."""
+    Uses T4..T6 (T7 is read as the don't-care half of the shift's source
+    pair), TMP, vcc, s[S_T+6:S_T+7]."""
     A0, A1, A2 = T[4], T[5], T[6]
-    for r in (A0, A1, A2):
-        a("v_mov_b32 %s, 0" % v(r))
     if hi_or is not None:
         a("v_mov_b32 %s, 0" % v(hi_or))
     for c in range(ncols):
         last = c == ncols - 1
-        for i in range(max(0, c - 7), min(c, 7) + 1):
+        for n, i in enumerate(range(max(0, c - 7), min(c, 7) + 1)):
             j = c - i
-            a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (
-                A0, A1, sp(S_T + 6), v(x[i]), v(y[j]), A0, A1))
+            add = "0" if c == 0 else "v[%d:%d]" % (A0, A1)
+            a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (
+                A0, A1, sp(S_T + 6), v(x[i]), v(y[j]), add))
             if not last:
-                a("v_addc_co_u32 %s, vcc, 0, %s, %s" % (v(A2), v(A2), sp(S_T + 6)))
+                # the column's first carry starts the overflow word afresh
+                a("v_addc_co_u32_e64 %s, vcc, 0, %s, %s" % (v(A2), "0" if n == 0 else v(A2),
+                                                            sp(S_T + 6)))
         if out is not None and c < 8:
             a("v_mov_b32 %s, %s" % (v(out[c]), v(A0)))
         if hi_or is not None:
@@ -1077,10 +1082,8 @@ def col_product(a: Asm, x: List[int], y: List[int], ncols: int, out: Optional[Li
             else:
                 a("v_bfi_b32 %s, %s, 0, %s" % (v(TMP), s(S_M + c), v(A0)))
                 a("v_or_b32 %s, %s, %s" % (v(hi_or), v(hi_or), v(TMP)))
-        if not last:
-            a("v_mov_b32 %s, %s" % (v(A0), v(A1)))
-            a("v_mov_b32 %s, %s" % (v(A1), v(A2)))
-            a("v_mov_b32 %s, 0" % v(A2))
+        if not last:                                  # (A0, A1) <- (A1, A2)
+            a("v_pk_mov_b32 v[%d:%d], v[%d:%d], v[%d:%d] op_sel:[1,0]" % (A0, A1, A0, A1, A2, A2 + 1))
 
 
 def body_mul(a: Asm):
@@ -1164,22 +1167,28 @@ def exec_end(a: Asm, lab: str, save: int):
 
 
 def moves(a: Asm, dsts: List[int], srcs: List[Optional[int]]):
-    """dsts[i] <- srcs[i] (None = 0) in list order, two limbs per v_mov_b64
-    where both register pairs are even-aligned and consecutive.  The caller
-    orders the list so no source is overwritten before it is read."""
+    """dsts[i] <- srcs[i] (None = 0) in list order, two limbs per instruction
+    where the destinations form an even-aligned pair: v_mov_b64 when the
+    sources do too, else v_pk_mov_b32 picking each half from its aligned
+    source pair (full rate, profiles/r01/ubench2.log).  The caller orders
+    the list so no source is overwritten before it is read (a pair reads
+    both sources before writing)."""
     i = 0
     while i < len(dsts):
-        if i + 1 < len(dsts):
-            d0, d1, s0, s1 = dsts[i], dsts[i + 1], srcs[i], srcs[i + 1]
-            lo, hi = (0, 1) if d1 == d0 + 1 else (1, 0)
-            dl, sl = (d0, s0) if lo == 0 else (d1, s1)
-            dh, sh = (d1, s1) if lo == 0 else (d0, s0)
-            if dh == dl + 1 and dl % 2 == 0 and (
-                    (sl is None and sh is None) or
-                    (sl is not None and sh == sl + 1 and sl % 2 == 0)):
-                a("v_mov_b64 %s, %s" % (vp(dl), "0" if sl is None else vp(sl)))
-                i += 2
-                continue
+        if i + 1 < len(dsts) and abs(dsts[i + 1] - dsts[i]) == 1 and min(dsts[i], dsts[i + 1]) % 2 == 0:
+            lo, hi = (i, i + 1) if dsts[i + 1] == dsts[i] + 1 else (i + 1, i)
+            dl, sl, sh = dsts[lo], srcs[lo], srcs[hi]
+            if sl is None and sh is None:
+                a("v_mov_b64 %s, 0" % vp(dl))
+            elif sl is not None and sh == sl + 1 and sl % 2 == 0:
+                a("v_mov_b64 %s, %s" % (vp(dl), vp(sl)))
+            else:
+                o0 = "0" if sl is None else vp(sl & ~1)
+                o1 = "0" if sh is None else vp(sh & ~1)
+                a("v_pk_mov_b32 %s, %s, %s op_sel:[%d,%d]" % (
+                    vp(dl), o0, o1, 0 if sl is None else sl & 1, 0 if sh is None else sh & 1))
+            i += 2
+            continue
         a("v_mov_b32 %s, %s" % (v(dsts[i]), "0" if srcs[i] is None else v(srcs[i])))
         i += 1
 
@@ -1244,8 +1253,7 @@ def body_shift(a: Asm, kind: str):
     a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(over), v(T[0])))
     a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), s(cur(F_W)), v(Y[0])))
     a("s_or_b64 %s, %s, %s" % (sp(over), sp(over), sp(S_T)))
-    a("v_lshrrev_b32 %s, 5, %s" % (v(T[2]), v(Y[0])))
-    a("v_and_b32 %s, 7, %s" % (v(T[2]), v(T[2])))           # q (over lanes masked later)
+    a("v_bfe_u32 %s, %s, 5, 3" % (v(T[2]), v(Y[0])))         # q (over lanes masked later)
     a("v_and_b32 %s, 31, %s" % (v(T[3]), v(Y[0])))          # b
     fill = None
     if kind == "ASHR":
@@ -1258,6 +1266,9 @@ def body_shift(a: Asm, kind: str):
         for j in range(8):
             a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[4])))
         fill = T[4]
+    lab_all = a.uniq("sho")
+    a("s_andn2_b64 %s, exec, %s" % (sp(S_T), sp(over)))
+    a("s_cbranch_scc0 %s" % lab_all)                 # every lane shifts by >= W
     if kind == "SHL":
         a("v_sub_u32 %s, 32, %s" % (v(T[5]), v(T[3])))
         a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_X + 2), v(T[3])))
@@ -1271,6 +1282,8 @@ def body_shift(a: Asm, kind: str):
     if fill is not None:
         for j in range(8):
             a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(fill)))
+    a.label(lab_all)
+    if fill is not None:
         a("v_mov_b32 %s, %s" % (v(T[5]), v(fill)))
     lab = exec_begin(a, over, S_T)                   # shift >= W: 0 or sign fill
     moves(a, X, [None if fill is None else T[4 + (j & 1)] for j in range(8)])

@@ -84,6 +84,9 @@ _TOK = re.compile(r"\s*([^,]+\([^)]*\)|[^,]+)\s*(?:,|$)")
 def _split_ops(s: str) -> List[str]:
     out = []
     pos = 0
+    mo = re.search(r"\s+(op_sel:\[\d,\d\])\s*$", s)      # VOP3P modifier (has a comma)
+    if mo:
+        return _split_ops(s[:mo.start()]) + [mo.group(1)]
     while pos < len(s):
         m = _TOK.match(s, pos)
         if not m or m.end() == pos:
@@ -518,6 +521,15 @@ class Wave:
     def _vop3(self, a, f, n):
         srcs = [self.vread(a[1 + i], "SRC%d" % i) for i in range(n)]
         self.vwrite(a[0], f(*srcs) & np.uint64(M32))
+
+    def i_v_pk_mov_b32(self, a, pc):
+        """dst.lo = src0 half op_sel[0], dst.hi = src1 half op_sel[1]."""
+        sel = [int(x) for x in re.findall(r"\d", a[3])] if len(a) > 3 else [0, 0]
+        halves = []
+        for k, src in enumerate((a[1], a[2])):
+            val = self.vread(src, "SRC%d" % k, 64)
+            halves.append((val >> np.uint64(32 * sel[k])) & np.uint64(M32))
+        self.vwrite(a[0], halves[0] | (halves[1] << np.uint64(32)))
 
     def i_v_mad_u32_u24(self, a, pc):
         m24 = np.uint64(0xFFFFFF)

@@ -1,5 +1,5 @@
 // Second instruction microbenchmark (gfx950): 64-bit moves (plain and
-// GPR-indexed), 64-bit compares, 32-bit integer multiplies, and whether a
+// GPR-indexed), 64-bit compares, packed 2 x 32-bit moves (v_pk_mov_b32), 32-bit integer multiplies, and whether a
 // SALU stream of one wave co-issues with a VALU stream of another wave on
 // the same SIMD.  Reports SIMD cycles per instruction (2.4 GHz clock).
 //
@@ -48,6 +48,21 @@ __global__ __launch_bounds__(64) void k_cmp64(uint32_t* out, uint32_t s) {    //
                          "v_cmp_eq_u64_e64 s[54:55], v[112:113], v[102:103]\n")
                      ::: "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49",
                        "s50", "s51", "s52", "s53", "s54", "s55");
+    out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(64) void k_pkmov(uint32_t* out, uint32_t s) {    // 128 instrs
+    for (int i = 0; i < ITERS; ++i)
+        asm volatile(R16("v_pk_mov_b32 v[40:41], v[100:101], v[102:103] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[42:43], v[104:105], v[106:107] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[44:45], v[108:109], v[110:111] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[46:47], v[112:113], v[114:115] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[48:49], v[100:101], v[106:107] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[50:51], v[104:105], v[110:111] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[52:53], v[108:109], v[114:115] op_sel:[1,0]\n"
+                         "v_pk_mov_b32 v[54:55], v[112:113], v[102:103] op_sel:[1,0]\n")
+                     ::: "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49",
+                       "v50", "v51", "v52", "v53", "v54", "v55");
     out[blockIdx.x * 64 + threadIdx.x] = s;
 }
 
@@ -110,7 +125,8 @@ int main() {
     CHK(hipEventCreate(&e1));
     struct { const char* name; kfn fn; int instrs; } bs[] = {
         {"v_mov_b64", k_mov64, 128}, {"v_mov_b64 gpr_idx (+2 SALU/4)", k_mov64idx, 96},
-        {"v_cmp_eq_u64_e64", k_cmp64, 128}, {"v_mul_lo_u32", k_mullo, 128},
+        {"v_cmp_eq_u64_e64", k_cmp64, 128}, {"v_pk_mov_b32", k_pkmov, 128},
+        {"v_mul_lo_u32", k_mullo, 128},
         {"v_mul_hi_u32", k_mulhi, 128}};
     for (auto& b : bs) {
         for (int w : {1, 3, 8}) {
