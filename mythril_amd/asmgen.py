@@ -71,7 +71,8 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "SUBR",     # b - a   (SUB with the operands swapped: in place on a)
         "ITEN",     # c ? b : a (ITE with the operands swapped: in place on a)
         "LEAFD",    # 256-bit LEAF straight into slot = variant, loads left in flight
-        "WAITVM"]   # wait for in-flight LEAFD loads (inserted by the translator)
+        "WAITVM",   # wait for in-flight LEAFD / RELOADD loads (inserted by the translator)
+        "RELOADD"]  # scratch reload straight into slot = variant, loads left in flight
 AOP = {n: i for i, n in enumerate(AOPS)}
 V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
 NVAR = 32
@@ -99,8 +100,8 @@ DC_NEEDS_W32 = {"ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "ITE", "EXTRACT"
 
 
 def canon_var(name: str, var: int) -> int:
-    if name == "LEAFD":
-        return var & (NREG - 1)      # the variant is the destination slot
+    if name in ("LEAFD", "RELOADD"):
+        return var if var < NREG else 0      # the variant is the destination slot
     var &= SUPPORT[name]
     if name in NO_MASK:
         var &= ~V_MASK
@@ -1007,6 +1008,19 @@ def h_leafd(a: Asm, bank: int, slot: int):
     dispatch(a, 1 - bank)
 
 
+def h_reloadd(a: Asm, bank: int, slot: int):
+    """Scratch reload into slot ``slot`` (the variant) with the loads left in
+    flight; the translator hoists it above earlier instructions that leave
+    the slot and the spill slot alone, and puts a WAITVM before the first
+    instruction that touches the slot."""
+    fd = FB + 8 * slot
+    prologue(a, bank)
+    a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
+    a("scratch_load_dwordx4 v[%d:%d], off, %s" % (fd, fd + 3, s(S_T)))
+    a("scratch_load_dwordx4 v[%d:%d], off, %s offset:16" % (fd + 4, fd + 7, s(S_T)))
+    dispatch(a, 1 - bank)
+
+
 def h_waitvm(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a("s_waitcnt vmcnt(0)")
@@ -1634,6 +1648,8 @@ def generate() -> List[str]:
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
                 if name == "LEAFD":
                     h_leafd(a, bank, var)
+                elif name == "RELOADD":
+                    h_reloadd(a, bank, var)
                 elif name in CHEAP:
                     CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
                 else:

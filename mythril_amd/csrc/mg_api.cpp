@@ -194,8 +194,13 @@ static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, u
     case MG_NOP: return 0;
     case MG_CONST: case MG_LEAF: case MG_RELOAD: return 1u << d;
     case MG_SPILL: case MG_OUT: case MG_ROOT: return 1u << a;
-    case MG_NOT: case MG_NEG: case MG_MOV: case MG_EXTRACT: case MG_SEXT:
+    case MG_NOT: case MG_NEG: case MG_MOV: case MG_SEXT:
         return (1u << d) | (1u << a);
+    // the funnel shifts read one slot beyond their operand (masked off, but
+    // the registers are read): the next slot for EXTRACT, the previous one
+    // for CONCAT's high part
+    case MG_EXTRACT: return ((1u << d) | (3u << a)) & ((1u << MG_NREG) - 1);
+    case MG_CONCAT: return (1u << d) | (1u << a) | (a ? 1u << (a - 1) : 0u) | (1u << b);
     case MG_ITE: return (1u << d) | (1u << a) | (1u << b) | (1u << c);
     default: return (1u << d) | (1u << a) | (1u << b);
     }
@@ -219,6 +224,32 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         rec.resize(rec.size() + 8, 0);
         return rec.data() + rec.size() - 8;
     };
+    // Issue order: every scratch RELOAD moves up (at most 24 places) past the
+    // instructions that leave its destination slot and its spill slot alone,
+    // so its loads are in flight early (RELOADD) and waited for only at the
+    // first instruction that touches the slot.
+    std::vector<uint32_t> order(n_ins);
+    for (uint32_t i = 0; i < n_ins; ++i) order[i] = i;
+    for (uint32_t q = 0; q < n_ins; ++q) {
+        const uint32_t* in = code + 4 * order[q];
+        if ((in[0] & 0xFF) != MG_RELOAD || in[2] < n_lds) continue;
+        const uint32_t rd = in[1] & 0xFF, slot = in[2];
+        uint32_t t = q;
+        while (t > 0 && q - t < 24) {
+            const uint32_t* p = code + 4 * order[t - 1];
+            const uint32_t pop = p[0] & 0xFF;
+            if (slots_touched(pop, p[1] & 0xFF, (p[1] >> 8) & 0xFF, (p[1] >> 16) & 0xFF,
+                              (p[1] >> 24) & 0xFF) & (1u << rd))
+                break;
+            if (pop == MG_SPILL && p[2] == slot) break;
+            --t;
+        }
+        if (t < q) {
+            const uint32_t moved = order[q];
+            for (uint32_t k = q; k > t; --k) order[k] = order[k - 1];
+            order[t] = moved;
+        }
+    }
     for (uint32_t pc = 0; pc <= n_ins; ++pc) {
         if (pc == n_ins) {          // HALT, then one zeroed record (prefetch pad)
             if (pending) {
@@ -229,17 +260,18 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
             emit();
             break;
         }
-        const uint32_t* in = code + 4 * pc;
+        const uint32_t* in = code + 4 * order[pc];
         const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
         const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
                        c = (in[1] >> 24) & 0xFF;
         const bool leafd = op == MG_LEAF && w == 256;
+        const bool reloadd = op == MG_RELOAD && imm >= n_lds;
         if (pending && (slots_touched(op, d, a, b, c) & pending)) {
             emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
             bank = 1 - bank;
             pending = 0;
         }
-        if (leafd) pending |= 1u << d;
+        if (leafd || reloadd) pending |= 1u << d;
         uint32_t* r = emit();
         uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
         const bool writes = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
@@ -265,7 +297,7 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
             break;
         case MG_RELOAD:
             if (imm < n_lds) { aop = MGA_RELOAD_LDS; r[5] = imm * 2u * 256u * 16u; }
-            else { aop = MGA_RELOAD_SCR; r[5] = (imm - n_lds) * 32u; }
+            else { aop = MGA_RELOADD; var = d; r[5] = (imm - n_lds) * 32u; }
             break;
         case MG_ADD: aop = MGA_ADD; goto masked;
         case MG_SUB: aop = MGA_SUB; goto masked;

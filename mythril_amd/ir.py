@@ -509,10 +509,12 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         ptr[v.id] = p
         return u[p] if p < len(u) else 1 << 60
 
-    def alloc_reg(i: int, protect: set) -> int:
+    def alloc_reg(i: int, protect: set, oldest: bool = False) -> int:
         nonlocal n_lds, n_spill
         if free_regs:
-            return free_regs.pop()
+            # reloads take the register free the longest: the translator can
+            # then issue them early (mg_api.cpp translate, RELOADD)
+            return free_regs.pop(0 if oldest else -1)
         victim, far = None, -1
         for r, v in holder.items():
             if v.id in protect:
@@ -560,7 +562,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         protect = {a.id for a in n.args}
         for a in n.args:
             if a.id not in reg_of:
-                r = alloc_reg(i, protect)
+                r = alloc_reg(i, protect, oldest=a.op != I.CONST)
                 materialise(a, r)
                 reg_of[a.id] = r
                 holder[r] = a
