@@ -99,9 +99,13 @@ NO_MASK = {"AND", "OR", "XOR", "EQ", "ULT", "ULE", "ITE", "ITEN", "MOV", "CONST"
 DC_NEEDS_W32 = {"ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "ITE", "EXTRACT", "MOV", "CONST"}
 
 
+# families whose variant is a register slot (static registers in the handler)
+SLOT_VARIANT = {"LEAFD", "RELOADD", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS"}
+
+
 def canon_var(name: str, var: int) -> int:
-    if name in ("LEAFD", "RELOADD"):
-        return var if var < NREG else 0      # the variant is the destination slot
+    if name in SLOT_VARIANT:
+        return var if var < NREG else 0      # the variant is the register slot
     var &= SUPPORT[name]
     if name in NO_MASK:
         var &= ~V_MASK
@@ -724,30 +728,34 @@ def h_sext(a, bank, root, mask, dc=False, w32=False, ip=False):
     dispatch(a, 1 - bank)
 
 
-def h_spill_lds(a, bank, root, mask, dc=False, w32=False, ip=False):
+def h_spill_lds(a: Asm, bank: int, slot: int):
+    """LDS spill straight from slot ``slot`` (the variant)."""
+    fa = FB + 8 * slot
     prologue(a, bank)
-    a.read_slot(Y, fld(bank, F_A))
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
-    a("ds_write_b128 %s, v[%d:%d]" % (v(T[0]), Y[0], Y[3]))
-    a("ds_write_b128 %s, v[%d:%d] offset:4096" % (v(T[0]), Y[4], Y[7]))
+    a("ds_write_b128 %s, v[%d:%d]" % (v(T[0]), fa, fa + 3))
+    a("ds_write_b128 %s, v[%d:%d] offset:4096" % (v(T[0]), fa + 4, fa + 7))
     dispatch(a, 1 - bank)
 
 
-def h_reload_lds(a, bank, root, mask, dc=False, w32=False, ip=False):
+def h_reload_lds(a: Asm, bank: int, slot: int):
+    """LDS reload straight into slot ``slot`` (the variant); the dispatch's
+    lgkmcnt wait covers the reads."""
+    fd = FB + 8 * slot
     prologue(a, bank)
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
-    a("ds_read_b128 v[%d:%d], %s" % (R[0], R[3], v(T[0])))
-    a("ds_read_b128 v[%d:%d], %s offset:4096" % (R[4], R[7], v(T[0])))
-    a("s_waitcnt lgkmcnt(0)")
-    finish(a, bank, R, root, False)
+    a("ds_read_b128 v[%d:%d], %s" % (fd, fd + 3, v(T[0])))
+    a("ds_read_b128 v[%d:%d], %s offset:4096" % (fd + 4, fd + 7, v(T[0])))
+    dispatch(a, 1 - bank)
 
 
-def h_spill_scr(a, bank, root, mask, dc=False, w32=False, ip=False):
+def h_spill_scr(a: Asm, bank: int, slot: int):
+    """Scratch spill straight from slot ``slot`` (the variant)."""
+    fa = FB + 8 * slot
     prologue(a, bank)
-    a.read_slot(Y, fld(bank, F_A))
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
-    a("scratch_store_dwordx4 off, v[%d:%d], %s" % (Y[0], Y[3], s(S_T)))
-    a("scratch_store_dwordx4 off, v[%d:%d], %s offset:16" % (Y[4], Y[7], s(S_T)))
+    a("scratch_store_dwordx4 off, v[%d:%d], %s" % (fa, fa + 3, s(S_T)))
+    a("scratch_store_dwordx4 off, v[%d:%d], %s offset:16" % (fa + 4, fa + 7, s(S_T)))
     dispatch(a, 1 - bank)
 
 
@@ -1598,13 +1606,13 @@ def body_div(a: Asm):
 
 CHEAP = {
     "NOP": h_nop, "HALT": h_halt, "CONST": h_const, "LEAF": h_leaf,
-    "SPILL_LDS": h_spill_lds, "SPILL_SCR": h_spill_scr, "RELOAD_LDS": h_reload_lds,
     "RELOAD_SCR": h_reload_scr, "ADD": h_add, "SUB": h_sub, "AND": h_and, "OR": h_or,
     "XOR": h_xor, "NOT": h_not, "EQ": h_eq, "ULT": h_ult, "ULE": h_ule, "SLT": h_slt,
     "SLE": h_sle, "ITE": h_ite, "CONCAT": h_concat, "EXTRACT": h_extract, "SEXT": h_sext,
     "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov, "SUBR": h_subr, "ITEN": h_iten,
     "WAITVM": h_waitvm,
 }
+SLOT_HANDLERS = {"SPILL_LDS": h_spill_lds, "SPILL_SCR": h_spill_scr, "RELOAD_LDS": h_reload_lds}
 HEAVY = {"MUL": "MUL", "UMULNO": "UMULNO", "SHL": "SHL", "LSHR": "LSHR", "ASHR": "ASHR",
          "UDIV": "DIV", "UREM": "DIV", "SDIV": "DIV", "SREM": "DIV", "SMOD": "DIV"}
 HEAVY_AOPS = sorted(AOP[n] for n in HEAVY)
@@ -1650,6 +1658,8 @@ def generate() -> List[str]:
                     h_leafd(a, bank, var)
                 elif name == "RELOADD":
                     h_reloadd(a, bank, var)
+                elif name in SLOT_VARIANT:
+                    SLOT_HANDLERS[name](a, bank, var)
                 elif name in CHEAP:
                     CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
                 else:

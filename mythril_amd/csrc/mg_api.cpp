@@ -291,12 +291,12 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
             if (leafd) { aop = MGA_LEAFD; var = d; }
             else if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
             break;
-        case MG_SPILL:
-            if (imm < n_lds) { aop = MGA_SPILL_LDS; r[5] = imm * 2u * 256u * 16u; }
-            else { aop = MGA_SPILL_SCR; r[5] = (imm - n_lds) * 32u; }
+        case MG_SPILL:              // spills and reloads: the variant is the slot
+            if (imm < n_lds) { aop = MGA_SPILL_LDS; var = a; r[5] = imm * 2u * 256u * 16u; }
+            else { aop = MGA_SPILL_SCR; var = a; r[5] = (imm - n_lds) * 32u; }
             break;
         case MG_RELOAD:
-            if (imm < n_lds) { aop = MGA_RELOAD_LDS; r[5] = imm * 2u * 256u * 16u; }
+            if (imm < n_lds) { aop = MGA_RELOAD_LDS; var = d; r[5] = imm * 2u * 256u * 16u; }
             else { aop = MGA_RELOADD; var = d; r[5] = (imm - n_lds) * 32u; }
             break;
         case MG_ADD: aop = MGA_ADD; goto masked;
