@@ -72,7 +72,8 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "ITEN",     # c ? b : a (ITE with the operands swapped: in place on a)
         "LEAFD",    # 256-bit LEAF straight into slot = variant, loads left in flight
         "WAITVM",   # wait for in-flight LEAFD / RELOADD loads (inserted by the translator)
-        "RELOADD"]  # scratch reload straight into slot = variant, loads left in flight
+        "RELOADD",  # scratch reload straight into slot = variant, loads left in flight
+        "EQSEL"]    # fused EQ + ITE of a store-chain link (translator): see h_eqsel
 AOP = {n: i for i, n in enumerate(AOPS)}
 V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
 NVAR = 32
@@ -91,6 +92,8 @@ SUPPORT.update({n: SUPPORT[n] | V_IP for n in ("ADD", "SUB", "AND", "OR", "XOR",
 SUPPORT["SUBR"] = _RM | V_IP
 SUPPORT["ITEN"] = V_ROOT | V_IP
 SUPPORT["WAITVM"] = 0
+V_NEG, V_GEN = 1, 2          # EQSEL: copy where not equal / three-address form
+SUPPORT["EQSEL"] = V_NEG | V_GEN
 # families whose result is never masked (canonical inputs give canonical
 # outputs) and families where DC only matters for one-limb results
 NO_MASK = {"AND", "OR", "XOR", "EQ", "ULT", "ULE", "ITE", "ITEN", "MOV", "CONST", "NOP", "HALT",
@@ -1029,6 +1032,38 @@ def h_reloadd(a: Asm, bank: int, slot: int):
     dispatch(a, 1 - bank)
 
 
+def h_eqsel(a: Asm, bank: int, var: int):
+    """One link of a lowered select-over-store chain, EQ fused with the ITE
+    that consumes it (mg_api.cpp translate; the Bool is never stored):
+      in place (default):  F[D] <- F[C]   where (F[A] == F[B]) != NEG
+      GEN:                 F[D] <- (F[A] == F[B]) ? F[C] : F[IMM]
+    The copies run under exec, two limbs per v_mov_b64."""
+    prologue(a, bank)
+    a.read_slot(Y, fld(bank, F_B))
+    a.idx_on(fld(bank, F_A), "SRC0")
+    for j in range(0, 8, 2):
+        a("v_cmp_eq_u64_e64 %s, %s, %s" % (sp(S_T + j), vp(F[j]), vp(Y[j])))
+    a.idx_off()
+    a("s_and_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
+    a("s_and_b64 %s, %s, %s" % (sp(S_T + 4), sp(S_T + 4), sp(S_T + 6)))
+    a("s_and_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 4)))
+    if var & V_GEN:
+        a.read_slot(R, fld(bank, F_IMM))          # else value
+    a.read_slot(Y, fld(bank, F_C))                # value taken
+    if var & V_GEN:
+        lab = exec_begin(a, None, S_T)
+        moves(a, R, Y)
+        exec_end(a, lab, S_T)
+        a.write_slot(R, fld(bank, F_D))
+    else:
+        lab = exec_begin(a, None, S_T, invert=bool(var & V_NEG))
+        a.idx_on(fld(bank, F_D), "DST")
+        moves(a, F, Y)
+        a.idx_off()
+        exec_end(a, lab, S_T)
+    dispatch(a, 1 - bank)
+
+
 def h_waitvm(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a("s_waitcnt vmcnt(0)")
@@ -1660,6 +1695,8 @@ def generate() -> List[str]:
                     h_reloadd(a, bank, var)
                 elif name in SLOT_VARIANT:
                     SLOT_HANDLERS[name](a, bank, var)
+                elif name == "EQSEL":
+                    h_eqsel(a, bank, var)
                 elif name in CHEAP:
                     CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
                 else:
@@ -1706,6 +1743,7 @@ def write_outputs(csrc: str) -> None:
            "#define MGA_V_ROOT %d" % V_ROOT, "#define MGA_V_MASK %d" % V_MASK,
            "#define MGA_V_DC %d" % V_DC, "#define MGA_V_W32 %d" % V_W32,
            "#define MGA_V_IP %d" % V_IP,
+           "#define MGA_V_NEG %d" % V_NEG, "#define MGA_V_GEN %d" % V_GEN,
            "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
            "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,
            "enum mga_op {"]

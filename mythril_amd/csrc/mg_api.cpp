@@ -206,6 +206,21 @@ static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, u
     }
 }
 
+// slots an instruction reads (its destination only when it is also an operand)
+static uint32_t slots_read(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t m = slots_touched(op, d, a, b, c);
+    switch (op) {
+    case MG_NOP: case MG_CONST: case MG_LEAF: case MG_RELOAD: return 0;
+    case MG_SPILL: case MG_OUT: case MG_ROOT: return m;
+    default: break;
+    }
+    const bool d_operand = d == a || (op != MG_NOT && op != MG_NEG && op != MG_MOV &&
+                                      op != MG_EXTRACT && op != MG_SEXT && d == b) ||
+                           (op == MG_ITE && d == c) || (op == MG_EXTRACT && d == a + 1) ||
+                           (op == MG_CONCAT && a && d == a - 1);
+    return d_operand ? m : m & ~(1u << d);
+}
+
 static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
                       uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
     pool.base = n_consts;
@@ -264,6 +279,41 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
         const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
                        c = (in[1] >> 24) & 0xFF;
+        // a store-chain link: t = (a == b) of wide values, consumed only by
+        // the next instruction, an ITE on t -> one EQSEL record
+        if (op == MG_EQ && w > 32 && !(in[0] & MG_ROOT_FLAG) && pc + 1 < n_ins) {
+            const uint32_t* nx = code + 4 * order[pc + 1];
+            const uint32_t nd = nx[1] & 0xFF, na = (nx[1] >> 8) & 0xFF, nb = (nx[1] >> 16) & 0xFF,
+                           nc = (nx[1] >> 24) & 0xFF;
+            bool fuse = (nx[0] & 0xFF) == MG_ITE && !(nx[0] & MG_ROOT_FLAG) && nc == d &&
+                        na != d && nb != d;
+            for (uint32_t q = pc + 2; fuse && q < n_ins; ++q) {     // is t dead after the ITE?
+                const uint32_t* f = code + 4 * order[q];
+                const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
+                               fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
+                if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) fuse = false;
+                else if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
+            }
+            if (fuse) {
+                const uint32_t touch = slots_touched(op, d, a, b, c) | slots_touched(MG_ITE, nd, na, nb, nc);
+                if (pending & touch) {
+                    emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
+                    bank = 1 - bank;
+                    pending = 0;
+                }
+                uint32_t* r = emit();
+                uint32_t var;
+                r[1] = 8 * nd; r[2] = 8 * a; r[3] = 8 * b;
+                if (nd == na) { var = MGA_V_NEG; r[4] = 8 * nb; }          // keep F[d] where equal
+                else if (nd == nb) { var = 0; r[4] = 8 * na; }             // take F[a] where equal
+                else { var = MGA_V_GEN; r[4] = 8 * na; r[5] = 8 * nb; }
+                r[0] = hoff[MGA_HID(MGA_EQSEL, var, bank)];
+                bank = 1 - bank;
+                clean[nd] = ((nx[0] >> 8) & 0x3FF) <= 32;     // canonical values
+                ++pc;
+                continue;
+            }
+        }
         const bool leafd = op == MG_LEAF && w == 256;
         const bool reloadd = op == MG_RELOAD && imm >= n_lds;
         if (pending && (slots_touched(op, d, a, b, c) & pending)) {
