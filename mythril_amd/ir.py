@@ -123,6 +123,11 @@ class _Lowerer:
 
     # -- hash-consed constructors ------------------------------------------
     def mk(self, op: int, width: int, args=(), imm=None) -> LNode:
+        if op == I.CONCAT and width == I.MAX_WIDTH and args[0].op == I.EXTRACT and \
+                args[0].imm == 0 and args[0].args[0].width == I.MAX_WIDTH:
+            # concat(y[h:0], e) at 256 bits = (y << |e|) | e mod 2^256: the
+            # funnel shift drops y's high bits itself (no EXTRACT needed)
+            args = (args[0].args[0],) + tuple(args[1:])
         key = (op, width, tuple(a.id for a in args), imm)
         n = self.table.get(key)
         if n is None:
