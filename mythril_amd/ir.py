@@ -242,6 +242,35 @@ class _Lowerer:
             acc = self.mk(op, width, (acc, a))
         return acc
 
+    def _by_constant(self, op: str, w: int, n: Node) -> Optional[LNode]:
+        """Shifts by a constant and unsigned division / remainder by a power
+        of two as bit-field ops (EVM SHR/SHL/SAR and DIV/MOD by 2^k keep
+        their constant operand after z3's simplify): funnel EXTRACT /
+        CONCAT / SEXT instead of the variable-shift and division bodies."""
+        if n.args[1].op != "bvnum":
+            return None
+        c = n.args[1].params[0]
+        x = self._narrow(n.args[0])
+        if op in ("bvudiv", "bvurem"):
+            if c <= 0 or c & (c - 1):
+                return None
+            k = c.bit_length() - 1
+            if op == "bvurem":
+                return self.const(0, w) if k == 0 else self.mk(I.EXTRACT, k, (x,), 0)
+            op, c = "bvlshr", k
+        if op not in ("bvshl", "bvlshr", "bvashr"):
+            return None
+        if c == 0:
+            return x
+        if op == "bvashr":
+            c = min(c, w - 1)                     # >= w: every bit is the sign
+            return self.mk(I.SEXT, w, (self.mk(I.EXTRACT, w - c, (x,), c),), w - c)
+        if c >= w:
+            return self.const(0, w)
+        if op == "bvlshr":
+            return self.mk(I.EXTRACT, w - c, (x,), c)
+        return self.mk(I.CONCAT, w, (self.mk(I.EXTRACT, w - c, (x,), 0), self.const(0, c)), c)
+
     def _lower_one(self, n: Node) -> List[LNode]:
         op, w = n.op, n.width
         if w > CHUNK:
@@ -259,6 +288,9 @@ class _Lowerer:
                   "bvsrem": I.SREM, "bvsmod": I.SMOD, "bvshl": I.SHL, "bvlshr": I.LSHR,
                   "bvashr": I.ASHR}
         if op in simple:
+            red = self._by_constant(op, w, n)
+            if red is not None:
+                return [red]
             return [self.mk(simple[op], w, (A(0), A(1)))]
         nary = {"bvadd": I.ADD, "bvmul": I.MUL, "bvand": I.AND, "bvor": I.OR, "bvxor": I.XOR,
                 "and": I.AND, "or": I.OR}

@@ -192,6 +192,27 @@ def division_case():
     return constraints, probes, gen
 
 
+def const_shift_case(w: int):
+    """Shifts by constants and unsigned division / remainder by powers of
+    two (the forms EVM SHR/SHL/SAR/DIV/MOD by 2^k take), lowered to
+    bit-field ops; constants around limb boundaries and >= w."""
+    x = N.bv_var("cx%d" % w, w)
+    probes = []
+    for c in sorted({0, 1, 7, 31, 32, 33, w // 2, w - 1, w, w + 1, 224, 255, 256, 300}):
+        k = N.bv_num(c % (1 << w), w)
+        probes += [N.bv_op(op, x, k) for op in ("bvshl", "bvlshr", "bvashr")]
+    for e in sorted({0, 1, 5, 32, w - 1}):
+        if e < w:
+            p2 = N.bv_num(1 << e, w)
+            probes += [N.bv_op("bvudiv", x, p2), N.bv_op("bvurem", x, p2)]
+    probes += [N.bv_op("bvudiv", x, N.bv_num(3, w)), N.bv_op("bvurem", x, N.bv_num(0, w))]
+    constraints = [N.bv_cmp("bvule", probes[0], x)]
+
+    def gen(rng):
+        return Assignment(vars={x.params[0]: edge_value(rng, w)})
+    return constraints, probes, gen
+
+
 def named_cases():
     out = {}
     for w in WIDTHS:
@@ -205,4 +226,7 @@ def named_cases():
     out["overflow"] = (c, p, g, {})
     c, p, g = division_case()
     out["division_hard"] = (c, p, g, {})
+    for w in (8, 160, 256):
+        c, p, g = const_shift_case(w)
+        out["const_shift_w%d" % w] = (c, p, g, {})
     return out
