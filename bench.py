@@ -53,8 +53,11 @@ def cpu_baseline(corpus, budget_s=12.0):
     from oracle import build as obuild
     from oracle import evalref
     obuild.build()
-    threads = min(os.cpu_count() or 1, 64)
-    # calibrate on the first DAG, then spread the budget over a DAG sample
+    # the host-core share (the GPU box exports OMP_NUM_THREADS=16 for one
+    # GPU; os.cpu_count() there is the whole machine)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count() or 1, 64))
+    # calibrate on the first DAG (long enough to amortise thread start-up),
+    # then spread the budget over a DAG sample
     sample = corpus[:: max(1, len(corpus) // 64)][:64]
     total_nodes = 0
     t_total = 0.0
@@ -63,9 +66,10 @@ def cpu_baseline(corpus, budget_s=12.0):
         roots, _ = make_dag(dag_id, SEED)
         S = evalref.serialize(roots, prog)
         if per_dag is None:
+            n_cal = 16384
             t0 = time.perf_counter()
-            evalref.run_gen(S, prog, SEED, dag_id, 0, 2048, threads)
-            rate = 2048 * nodes / max(time.perf_counter() - t0, 1e-6)
+            evalref.run_gen(S, prog, SEED, dag_id, 0, n_cal, threads)
+            rate = n_cal * nodes / max(time.perf_counter() - t0, 1e-6)
             per_dag = max(256, int(rate * budget_s / len(sample) / max(nodes, 1)))
         t0 = time.perf_counter()
         evalref.run_gen(S, prog, SEED, dag_id, 0, per_dag, threads)
