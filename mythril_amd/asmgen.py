@@ -73,7 +73,9 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "LEAFD",    # 256-bit LEAF straight into slot = variant, loads left in flight
         "WAITVM",   # wait for in-flight LEAFD / RELOADD loads (inserted by the translator)
         "RELOADD",  # scratch reload straight into slot = variant, loads left in flight
-        "EQSEL"]    # fused EQ + ITE of a store-chain link (translator): see h_eqsel
+        "EQSEL",    # fused EQ + ITE of a store-chain link (translator): see h_eqsel
+        "EXTRACTN",  # EXTRACT to W > 32 bits: variant = result limbs - 1
+        "CONCATQ"]  # CONCAT: variant = limb shift q | 8 if a bit shift remains
 AOP = {n: i for i, n in enumerate(AOPS)}
 V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
 NVAR = 32
@@ -109,6 +111,10 @@ SLOT_VARIANT = {"LEAFD", "RELOADD", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS"}
 def canon_var(name: str, var: int) -> int:
     if name in SLOT_VARIANT:
         return var if var < NREG else 0      # the variant is the register slot
+    if name == "EXTRACTN":
+        return var & 7
+    if name == "CONCATQ":
+        return var & 15
     var &= SUPPORT[name]
     if name in NO_MASK:
         var &= ~V_MASK
@@ -713,6 +719,49 @@ def h_concat(a, bank, root, mask, dc=False, w32=False, ip=False):
     for j in range(8):
         a("v_bfi_b32 %s, %s, %s, %s" % (v(R[j]), s(S_M + j), v(R[j]), v(Y[j])))
     finish(a, bank, R, root, False)
+
+
+def h_extractn(a: Asm, bank: int, var: int):
+    """EXTRACT to W > 32 bits with nl = var + 1 result limbs known
+    statically: nl funnel shifts, the top limb masked with the value in MOFF
+    (bits < W mod 32, all ones when W is a multiple of 32), zero limbs
+    above, written as pairs."""
+    nl = var + 1
+    prologue(a, bank)
+    a.idx_on(fld(bank, F_C), "SRC0,SRC1")
+    for j in range(nl):
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(R[j]), v(G[j + 1]), v(G[j]), s(fld(bank, F_IMM))))
+    a.idx_off()
+    a("v_and_b32 %s, %s, %s" % (v(R[nl - 1]), s(fld(bank, F_MOFF)), v(R[nl - 1])))
+    a.idx_on(fld(bank, F_D), "DST")
+    moves(a, F, [R[j] if j < nl else None for j in range(8)])
+    a.idx_off()
+    dispatch(a, 1 - bank)
+
+
+def h_concatq(a: Asm, bank: int, var: int):
+    """CONCAT R = F[a] << k | F[b] with q = k >> 5 (var & 7) and a bit shift
+    k & 31 (var & 8) known statically: limbs below q come from F[b], limbs
+    from q up from the funnel shift of F[a] (C = funnel index, IMM = funnel
+    shift), limb q merged with MOFF = the bits >= k & 31; written as pairs."""
+    q, bs = var & 7, bool(var & 8)
+    ny = q + (1 if bs else 0)                 # limbs of F[b] needed
+    prologue(a, bank)
+    if ny:
+        a.idx_on(fld(bank, F_B), "SRC0")
+        for j in range(0, ny, 2):
+            a("v_mov_b64 %s, %s" % (vp(Y[j]), vp(F[j])))
+        a.idx_off()
+    a.idx_on(fld(bank, F_C), "SRC0,SRC1")
+    for j in range(q, 8):
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(R[j]), v(G[j + 1]), v(G[j]), s(fld(bank, F_IMM))))
+    a.idx_off()
+    if bs:
+        a("v_bfi_b32 %s, %s, %s, %s" % (v(R[q]), s(fld(bank, F_MOFF)), v(R[q]), v(Y[q])))
+    a.idx_on(fld(bank, F_D), "DST")
+    moves(a, F, [Y[j] if j < q else R[j] for j in range(8)])
+    a.idx_off()
+    dispatch(a, 1 - bank)
 
 
 def h_sext(a, bank, root, mask, dc=False, w32=False, ip=False):
@@ -1697,6 +1746,10 @@ def generate() -> List[str]:
                     SLOT_HANDLERS[name](a, bank, var)
                 elif name == "EQSEL":
                     h_eqsel(a, bank, var)
+                elif name == "EXTRACTN":
+                    h_extractn(a, bank, var)
+                elif name == "CONCATQ":
+                    h_concatq(a, bank, var)
                 elif name in CHEAP:
                     CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
                 else:

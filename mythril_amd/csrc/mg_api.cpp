@@ -375,19 +375,26 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         case MG_ULT: aop = MGA_ULT; break;
         case MG_ULE: aop = MGA_ULE; break;
         case MG_ITE: aop = MGA_ITE; break;
-        case MG_CONCAT: {           // R = a << imm | b
-            aop = MGA_CONCAT;
+        case MG_CONCAT: {           // R = a << imm | b: static limb shift in the variant
+            aop = MGA_CONCATQ;
             const uint32_t q = imm >> 5, bs = imm & 31;
+            var = q | (bs ? 8u : 0u);
             r[4] = 8 * a + 8 - q - (bs ? 1 : 0);
             r[5] = bs ? 32 - bs : 0;
-            r[7] = pool.add(mask_ge(imm));
+            r[7] = ~((1u << bs) - 1u);              // limb q: bits >= bs from a
             break;
         }
         case MG_EXTRACT:            // R = (a >> imm) & mask(w)
-            aop = MGA_EXTRACT;
             r[4] = 8 * a + (imm >> 5) + 8;
             r[5] = imm & 31;
-            r[7] = pool.add(mask_lt(w));
+            if (w > 32) {           // static result limbs; top-limb mask inline
+                aop = MGA_EXTRACTN;
+                var = (w + 31) / 32 - 1;
+                r[7] = (w & 31) ? (1u << (w & 31)) - 1u : 0xFFFFFFFFu;
+            } else {
+                aop = MGA_EXTRACT;
+                r[7] = pool.add(mask_lt(w));
+            }
             break;
         case MG_SEXT: {             // from imm bits to w bits: 16-word mask entry
             aop = MGA_SEXT;
