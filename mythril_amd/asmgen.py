@@ -1043,12 +1043,24 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     finish(a, bank, X, root, mask)
 
 
-def h_leafd(a: Asm, bank: int, slot: int):
+def _wait_if_flagged(a: Asm, bank: int):
+    """LEAFD / RELOADD whose consumer is the very next record: the translator
+    sets word W of the record, and the handler waits for its loads itself
+    instead of a separate WAITVM record."""
+    lab = a.uniq("nw")
+    a("s_cmp_eq_u32 %s, 0" % s(fld(bank, F_W)))
+    a("s_cbranch_scc1 %s" % lab)
+    a("s_waitcnt vmcnt(0)")
+    a.label(lab)
+
+
+def h_leafd(a: Asm, bank: int, var: int):
     """256-bit LEAF into slot ``slot`` (the variant): the value is built
     straight in the slot's registers and its memory loads (input SoA, or the
     generator's boundary / pool lanes) are left in flight, so a run of leaves
     pays one memory latency at the WAITVM the translator puts before the
     first instruction that touches a pending slot."""
+    slot = var
     fd = [FB + 8 * slot + j for j in range(8)]
     prologue(a, bank)
     lab_gen, lab_done = a.uniq("lgen"), a.uniq("ldone")
@@ -1065,19 +1077,21 @@ def h_leafd(a: Asm, bank: int, slot: int):
     _gen_leaf(a, bank, dst=fd, wait=False)
     _store_soa(a, fd, IN["lout"], fld(bank, F_C), wait_vm=True)
     a.label(lab_done)
+    _wait_if_flagged(a, bank)
     dispatch(a, 1 - bank)
 
 
-def h_reloadd(a: Asm, bank: int, slot: int):
+def h_reloadd(a: Asm, bank: int, var: int):
     """Scratch reload into slot ``slot`` (the variant) with the loads left in
     flight; the translator hoists it above earlier instructions that leave
     the slot and the spill slot alone, and puts a WAITVM before the first
     instruction that touches the slot."""
-    fd = FB + 8 * slot
+    fd = FB + 8 * var
     prologue(a, bank)
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
     a("scratch_load_dwordx4 v[%d:%d], off, %s" % (fd, fd + 3, s(S_T)))
     a("scratch_load_dwordx4 v[%d:%d], off, %s offset:16" % (fd + 4, fd + 7, s(S_T)))
+    _wait_if_flagged(a, bank)
     dispatch(a, 1 - bank)
 
 
@@ -1123,6 +1137,14 @@ def h_waitvm(a, bank, root, mask, dc=False, w32=False, ip=False):
 # heavy ops: per-(bank, variant) stubs copy the record to S_CUR and branch to
 # a shared body; the body prefetches the next record into bank A
 # ---------------------------------------------------------------------------
+
+def far_jump(a: Asm, label: str):
+    """Jump anywhere in the body (s_branch reaches only +-128 KiB): the
+    target's offset from .Lbase is an assembler-resolved literal."""
+    a("s_add_u32 %s, %s, (%s - .Lbase_%%=)" % (s(S_JMP), s(S_BASE), label))
+    a("s_addc_u32 %s, %s, 0" % (s(S_JMP + 1), s(S_BASE + 1)))
+    a("s_setpc_b64 %s" % sp(S_JMP))
+
 
 def heavy_stub(a: Asm, bank: int, varbits: int, body: str):
     b = BANK[bank]
@@ -1728,7 +1750,7 @@ def generate() -> List[str]:
         a("v_mov_b32 %s, (.Lh%d_%%= - .Lbase_%%=)" % (v(T[1]), canonical(h)))
         a("global_store_dword %s, %s, %s offset:%d" % (v(T[0]), v(T[1]), sp(S_T), 4 * (h % 512)))
     a("s_waitcnt vmcnt(0)")
-    a("s_branch .Lexit_%=")
+    far_jump(a, ".Lexit_%=")
     for name in AOPS:
         aop = AOP[name]
         for var in range(NVAR):

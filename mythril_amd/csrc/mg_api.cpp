@@ -239,6 +239,18 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         rec.resize(rec.size() + 8, 0);
         return rec.data() + rec.size() - 8;
     };
+    // the last record emitted, when it is a LEAFD / RELOADD: a wait right
+    // after it folds into that record (word W = 1, the handler waits)
+    size_t last_ld = SIZE_MAX;
+    auto wait_vm = [&]() {
+        if (last_ld != SIZE_MAX && last_ld + 8 == rec.size()) {
+            rec[last_ld + 6] = 1;           // the LEAFD / RELOADD waits itself
+        } else {
+            emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
+            bank = 1 - bank;
+        }
+        pending = 0;
+    };
     // Issue order: every scratch RELOAD moves up (at most 24 places) past the
     // instructions that leave its destination slot and its spill slot alone,
     // so its loads are in flight early (RELOADD) and waited for only at the
@@ -267,10 +279,7 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
     }
     for (uint32_t pc = 0; pc <= n_ins; ++pc) {
         if (pc == n_ins) {          // HALT, then one zeroed record (prefetch pad)
-            if (pending) {
-                emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
-                bank = 1 - bank;
-            }
+            if (pending) wait_vm();
             emit()[0] = hoff[MGA_HID(MGA_HALT, 0, bank)];
             emit();
             break;
@@ -296,11 +305,7 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
             }
             if (fuse) {
                 const uint32_t touch = slots_touched(op, d, a, b, c) | slots_touched(MG_ITE, nd, na, nb, nc);
-                if (pending & touch) {
-                    emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
-                    bank = 1 - bank;
-                    pending = 0;
-                }
+                if (pending & touch) wait_vm();
                 uint32_t* r = emit();
                 uint32_t var;
                 r[1] = 8 * nd; r[2] = 8 * a; r[3] = 8 * b;
@@ -316,11 +321,7 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         }
         const bool leafd = op == MG_LEAF && w == 256;
         const bool reloadd = op == MG_RELOAD && imm >= n_lds;
-        if (pending && (slots_touched(op, d, a, b, c) & pending)) {
-            emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
-            bank = 1 - bank;
-            pending = 0;
-        }
+        if (pending && (slots_touched(op, d, a, b, c) & pending)) wait_vm();
         if (leafd || reloadd) pending |= 1u << d;
         uint32_t* r = emit();
         uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
@@ -424,6 +425,10 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
             }
         }
         r[0] = hoff[MGA_HID(aop, var, bank)];
+        if (aop == MGA_LEAFD || aop == MGA_RELOADD) {
+            r[6] = 0;
+            last_ld = (size_t)(r - rec.data());
+        }
         if (writes) clean[d] = narrow;
         bank = mga_is_heavy(aop) ? 0 : 1 - bank;
     }
