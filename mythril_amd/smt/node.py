@@ -263,8 +263,8 @@ def _quote(name: str) -> str:
 
 
 def to_sexpr(n: Node, max_depth: int = -1) -> str:
-    """SMT-LIB 2 text of one term (no let-sharing; for debugging and fixtures
-    of moderate size use :func:`mythril_amd.smtlib.dump_query`)."""
+    """SMT-LIB 2 text of one term (no sharing; for debugging — whole queries
+    are written by :func:`mythril_amd.smtlib.dump_query`)."""
     if max_depth == 0:
         return "..."
     op = n.op

@@ -151,3 +151,22 @@ def test_independent_groups_are_searched_separately(engine):
     assert idx < 0                                  # jointly: a miss
     m = M.get_model(tuple(cs), enforce_execution_time=False)
     assert [m[x.raw.params[0]] for x in xs] == vals
+
+
+def test_capture_replay_on_gpu(engine, tmp_path):
+    """A captured query file replayed through the batched GPU search: the
+    satisfiable ones are found, the recorded-unsat one is not (a GPU witness
+    for it would be reported as unsound)."""
+    import json
+    from mythril_amd import capture, smtlib
+    x, y = BVS("rx", 256), BVS("ry", 256)
+    sets = [([x == BVV(77, 256)], "sat"), ([x + y == BVV(5, 256), y == BVV(2, 256)], "sat"),
+            ([x != x], "unsat")]
+    path = tmp_path / "q.jsonl"
+    with open(path, "w") as fh:
+        for i, (cs, res) in enumerate(sets):
+            fh.write(json.dumps({"id": i, "minimize": 0, "maximize": 0, "python_bools": [],
+                                 "smt2": smtlib.dump_query([c.raw for c in cs]),
+                                 "result": res}) + "\n")
+    rep = capture.replay_gpu(capture.read(str(path)))
+    assert rep["searched"] == 3 and rep["gpu_found"] == 2 and rep["unsound"] == []
