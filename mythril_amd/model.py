@@ -469,3 +469,15 @@ def install() -> None:
                 "mythril.laser.ethereum.state.constraints"):
         m = importlib.import_module(mod)
         m.get_model = get_model
+    # concrete hashes of reported transactions: one GPU Keccak batch
+    # (analysis/solver.py:119-152 -> mythril_amd.sha)
+    solver = importlib.import_module("mythril.analysis.solver")
+    if hasattr(solver, "_replace_with_actual_sha"):
+        from .sha import replace_with_actual_sha
+        kfm = importlib.import_module("mythril.laser.ethereum.keccak_function_manager")
+        sf = importlib.import_module("mythril.laser.smt").symbol_factory
+
+        def _replace(concrete_transactions, model, code=None):
+            replace_with_actual_sha(concrete_transactions, model,
+                                    kfm.keccak_function_manager, code, symbol_factory=sf)
+        solver._replace_with_actual_sha = _replace

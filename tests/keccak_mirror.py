@@ -18,12 +18,28 @@ class KeccakManager:
         self.interval_hook_for_size = {}
         self._index_counter = TOTAL_PARTS - 34534
         self.concrete_hashes = {}
+        self.hash_result_store = {}
 
     def get_function(self, length):
         if length not in self.store_function:
             self.store_function[length] = (Function("keccak256_{}".format(length), length, 256),
                                            Function("keccak256_{}-1".format(length), 256, length))
+            self.hash_result_store[length] = []
         return self.store_function[length]
+
+    def get_concrete_hash_data(self, model):
+        """keccak_function_manager.py:102-120: the model's values of every
+        symbolic hash created so far, per input size."""
+        out = {}
+        for size, vals in self.hash_result_store.items():
+            out[size] = []
+            for val in vals:
+                try:
+                    ev = model.eval(val.raw)
+                    out[size].append(ev.as_long() if hasattr(ev, "as_long") else int(ev))
+                except (AttributeError, TypeError):
+                    continue
+        return out
 
     def find_concrete_keccak(self, data):
         digest = self.hasher(data.value.to_bytes(data.size() // 8, "big"))
@@ -36,7 +52,9 @@ class KeccakManager:
             h = self.find_concrete_keccak(data)
             self.concrete_hashes[data] = h
             return h, And(func(data) == h, inverse(func(data)) == data)
-        return func(data), self._create_condition(data)
+        cond = self._create_condition(data)
+        self.hash_result_store[length].append(func(data))
+        return func(data), cond
 
     def _create_condition(self, func_input):
         length = func_input.size()

@@ -170,3 +170,17 @@ def test_capture_replay_on_gpu(engine, tmp_path):
                                  "result": res}) + "\n")
     rep = capture.replay_gpu(capture.read(str(path)))
     assert rep["searched"] == 3 and rep["gpu_found"] == 2 and rep["unsound"] == []
+
+
+def test_replace_with_actual_sha_on_gpu(engine):
+    """The batched concrete-hash replacement with the GPU Keccak gives the
+    reference walk's transactions (tests/test_sha.py restates the walk)."""
+    from mythril_amd.sha import replace_with_actual_sha
+    from test_sha import reference_walk, scenario
+    for seed in range(3):
+        km, model, txs = scenario(seed)
+        want = [dict(t) for t in txs]
+        reference_walk(want, model, km)
+        got = [dict(t) for t in txs]
+        replace_with_actual_sha(got, model, km)          # default: mg_keccak256
+        assert got == want

@@ -1,0 +1,117 @@
+"""Batched concrete-hash replacement against a
+line-by-line restatement of the reference's _replace_with_actual_sha
+(mythril/analysis/solver.py:119-152) on the same model and manager."""
+
+import random
+
+import pytest
+
+from keccak_mirror import KeccakManager
+from mythril_amd.sha import HASH_MATCHER, replace_with_actual_sha
+from mythril_amd.smt import symbol_factory
+from oracle import keccak_ref
+from oracle import smtlib_ref as R
+
+
+class TableModel:
+    """A model over UF tables: eval() runs the oracle evaluator."""
+
+    def __init__(self, funcs):
+        self.asg = R.Assignment({}, {}, funcs)
+
+    def eval(self, node):
+        return R.evaluate([node], self.asg)[0]
+
+
+def reference_walk(concrete_transactions, model, km, code=None):
+    """solver.py:124-152, transcribed (find_concrete_keccak on the host)."""
+    concrete_hashes = km.get_concrete_hash_data(model)
+    for tx in concrete_transactions:
+        if HASH_MATCHER not in tx["input"]:
+            continue
+        if code is not None and code.bytecode in tx["input"]:
+            s_index = len(code.bytecode) + 2
+        else:
+            s_index = 10
+        for i in range(s_index, len(tx["input"])):
+            data_slice = tx["input"][i: i + 64]
+            if HASH_MATCHER not in data_slice or len(data_slice) != 64:
+                continue
+            find_input = symbol_factory.BitVecVal(int(data_slice, 16), 256)
+            input_ = None
+            for size in concrete_hashes:
+                _, inverse = km.store_function[size]
+                if find_input.value not in concrete_hashes[size]:
+                    continue
+                input_ = symbol_factory.BitVecVal(int(model.eval(inverse(find_input).raw)), size)
+            if input_ is None:
+                continue
+            keccak = km.find_concrete_keccak(input_)
+            hex_keccak = hex(keccak.value)[2:]
+            if len(hex_keccak) != 64:
+                hex_keccak = "0" * (64 - len(hex_keccak)) + hex_keccak
+            tx["input"] = tx["input"][:s_index] + tx["input"][s_index:].replace(
+                tx["input"][i: 64 + i], hex_keccak)
+
+
+def scenario(seed):
+    """Symbolic hashes of 256- and 160-bit inputs whose model values carry the
+    'fffffff' prefix; transactions embedding them (and decoys) in calldata."""
+    rng = random.Random(seed)
+    km = KeccakManager(keccak_ref.keccak256)
+    funcs, outs = {}, []
+    for k, size in enumerate((256, 160, 256, 256)):
+        x = symbol_factory.BitVecSym("h%d_%d" % (seed, k), size)
+        km.create_keccak(x)
+        h = int("fffffff" + "%057x" % rng.getrandbits(228), 16) & ~63
+        inp = rng.getrandbits(size)
+        fn, inv = "keccak256_%d" % size, "keccak256_%d-1" % size
+        funcs.setdefault(fn, ([], 0))[0].append((inp, h))
+        funcs.setdefault(inv, ([], 0))[0].append((h, inp))
+        outs.append(h)
+    # bind every symbolic hash input to its table entry (the model's vars)
+    model = TableModel(funcs)
+    vars_ = {}
+    for fn, (entries, _) in funcs.items():
+        if fn.endswith("-1"):
+            continue
+        size = int(fn.split("_")[1])
+        for (inp, _), app in zip(entries, km.hash_result_store[size]):
+            vars_[app.raw.args[0].params[0]] = inp
+    model.asg = R.Assignment(vars_, {}, funcs)
+    txs = []
+    for t in range(3):
+        words = ["%064x" % rng.choice(outs + [rng.getrandbits(256), int("fffffff" + "0" * 57, 16)])
+                 for _ in range(rng.randrange(1, 5))]
+        txs.append({"input": "0x" + "a9059cbb" + "".join(words)})
+    txs.append({"input": "0x" + "12345678"})
+    return km, model, txs
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_batched_replacement_equals_reference_walk(seed):
+    km, model, txs = scenario(seed)
+    want = [dict(t) for t in txs]
+    reference_walk(want, model, km)
+    calls = []
+
+    def host_keccak(msgs):
+        calls.append(len(msgs))
+        return [keccak_ref.keccak256(m) for m in msgs]
+    got = [dict(t) for t in txs]
+    replace_with_actual_sha(got, model, km, keccak=host_keccak)
+    assert got == want
+    assert calls and calls[0] >= 1                  # one batch up front
+
+
+def test_replacement_known_answer():
+    km = KeccakManager(keccak_ref.keccak256)
+    x = symbol_factory.BitVecSym("kx", 256)
+    km.create_keccak(x)
+    h = int("fffffff" + "0" * 55 + "40", 16)
+    funcs = {"keccak256_256": ([(1, h)], 0), "keccak256_256-1": ([(h, 1)], 0)}
+    model = TableModel(funcs)
+    model.asg = R.Assignment({"kx": 1}, {}, funcs)
+    txs = [{"input": "0xa9059cbb" + "%064x" % h}]
+    replace_with_actual_sha(txs, model, km, keccak=lambda ms: [keccak_ref.keccak256(m) for m in ms])
+    assert txs[0]["input"] == "0xa9059cbb" + keccak_ref.keccak256((1).to_bytes(32, "big")).hex()
