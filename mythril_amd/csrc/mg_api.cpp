@@ -251,16 +251,17 @@ static void translate(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins
         }
         pending = 0;
     };
-    // Issue order: every scratch RELOAD moves up (at most 24 places) past the
-    // instructions that leave its destination slot and its spill slot alone,
-    // so its loads are in flight early (RELOADD) and waited for only at the
-    // first instruction that touches the slot.
+    // Issue order: every scratch RELOAD and 256-bit LEAF moves up (at most 24
+    // places) past the instructions that leave its destination slot (and spill
+    // slot) alone, so its loads are in flight early (RELOADD / LEAFD) and
+    // waited for only at the first instruction that touches the slot.
     std::vector<uint32_t> order(n_ins);
     for (uint32_t i = 0; i < n_ins; ++i) order[i] = i;
     for (uint32_t q = 0; q < n_ins; ++q) {
         const uint32_t* in = code + 4 * order[q];
-        if ((in[0] & 0xFF) != MG_RELOAD || in[2] < n_lds) continue;
-        const uint32_t rd = in[1] & 0xFF, slot = in[2];
+        const bool leafd = (in[0] & 0xFF) == MG_LEAF && ((in[0] >> 8) & 0x3FF) == 256;
+        if (!leafd && ((in[0] & 0xFF) != MG_RELOAD || in[2] < n_lds)) continue;
+        const uint32_t rd = in[1] & 0xFF, slot = leafd ? 0xFFFFFFFFu : in[2];
         uint32_t t = q;
         while (t > 0 && q - t < 24) {
             const uint32_t* p = code + 4 * order[t - 1];

@@ -500,7 +500,22 @@ def _schedule(sinks: List[LNode]) -> List[LNode]:
         out.append(n)
         stack.extend(a for a in n.args if a.id not in seen)
     out.sort(key=lambda n: (n.birth, n.id))
-    return out
+    # leaves are born first (the variables exist before the terms over them):
+    # each goes right before its first user instead, so it does not hold a
+    # register from the start (fewer spills); the translator issues its
+    # loads early again where the slot is free (mg_api.cpp, LEAFD)
+    lazy: List[LNode] = []
+    placed = set()
+    for n in out:
+        if n.op == I.LEAF:
+            continue
+        for a in n.args:
+            if a.op == I.LEAF and a.id not in placed:
+                placed.add(a.id)
+                lazy.append(a)
+        lazy.append(n)
+    lazy += [n for n in out if n.op == I.LEAF and n.id not in placed]
+    return lazy
 
 
 def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
