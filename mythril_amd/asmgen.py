@@ -1546,11 +1546,16 @@ def _div_digit(a: Asm, un, vn, j, d, dinv):
     A0, A1, P0, P1, CR, RH, QH = T[4], T[5], T[6], T[7], T[8], T[9], T[11]
     st = S_T
     lt = sp(st)                  # lanes with u2 < d (all but the u2 == d case)
-    # 2-by-1 quotient via the reciprocal: qq = dinv * a2 + (a2:u1), a2 = u2 < d ? u2 : 0
+    # 2-by-1 quotient via the reciprocal: qq = dinv * u2 + (u2:u1).  Lanes
+    # with u2 == d (not < d) compute garbage here and take qhat = b - 1 below.
+    # The addend is read in place when (u1, u2) is an aligned pair.
     a("v_cmp_lt_u32_e64 %s, %s, %s" % (lt, v(u2), v(d)))
-    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(A1), v(u2), lt))
-    a("v_mov_b32 %s, %s" % (v(A0), v(u1)))
-    a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (A0, A1, sp(st + 6), v(dinv), v(A1), A0, A1))
+    if u2 == u1 + 1 and u1 % 2 == 0:
+        add = vp(u1)
+    else:
+        a("v_pk_mov_b32 %s, %s, %s op_sel:[%d,%d]" % (vp(A0), vp(u1 & ~1), vp(u2 & ~1), u1 & 1, u2 & 1))
+        add = vp(A0)
+    a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (A0, A1, sp(st + 6), v(dinv), v(u2), add))
     a("v_add_u32 %s, 1, %s" % (v(QH), v(A1)))                       # q1 (A0 = q0)
     a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, 0" % (P0, P1, sp(st + 6), v(QH), v(d)))
     a("v_sub_u32 %s, %s, %s" % (v(CR), v(u1), v(P0)))                # r = u1 - q1*d
