@@ -1214,12 +1214,40 @@ def col_product(a: Asm, x: List[int], y: List[int], ncols: int, out: Optional[Li
             a("v_pk_mov_b32 v[%d:%d], v[%d:%d], v[%d:%d] op_sel:[1,0]" % (A0, A1, A0, A1, A2, A2 + 1))
 
 
+def low_product(a: Asm, x: List[int], y: List[int], out: List[int]):
+    """out[0..7] = (x*y) mod 2^256 by product scanning, with the column
+    accumulator placed so no digit needs a copy on even columns: column c
+    even accumulates in the aligned pair (out[c], out[c+1]) (the digit stays
+    in out[c]), column c odd in (A0, A1) with its digit copied to out[c]; one
+    v_pk_mov_b32 per column moves (high word, carry word) on.  Column 0's
+    single product cannot carry; the carries of column 6 would only reach
+    column 8, so they are not tracked.  Uses T4..T6, vcc, s[S_T+6:S_T+7]."""
+    A0, A1, A2 = T[4], T[5], T[6]
+    for c in range(8):
+        pair = (out[c], out[c + 1]) if c % 2 == 0 else (A0, A1)
+        for n, i in enumerate(range(0, c + 1)):
+            add = "0" if c == 0 else "v[%d:%d]" % pair
+            a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (
+                pair[0], pair[1], sp(S_T + 6), v(x[i]), v(y[c - i]), add))
+            if 1 <= c <= 5:
+                a("v_addc_co_u32_e64 %s, vcc, 0, %s, %s" % (v(A2), "0" if n == 0 else v(A2),
+                                                            sp(S_T + 6)))
+        if c % 2 == 1:
+            a("v_mov_b32 %s, %s" % (v(out[c]), v(A0)))
+            if c < 7:                                 # (out[c+1], out[c+2]) <- (A1, A2)
+                a("v_pk_mov_b32 v[%d:%d], v[%d:%d], v[%d:%d] op_sel:[1,0]" % (
+                    out[c + 1], out[c + 2], A0, A1, A2, A2 + 1))
+        else:                                         # (A0, A1) <- (out[c+1], A2 | 0)
+            a("v_pk_mov_b32 v[%d:%d], v[%d:%d], %s op_sel:[1,0]" % (
+                A0, A1, out[c], out[c + 1], "0" if c == 0 else "v[%d:%d]" % (A2, A2 + 1)))
+
+
 def body_mul(a: Asm):
     a.label(".Lbody_MUL_%=")
     heavy_prologue(a)
     a.read_slot(X, cur(F_A))
     a.read_slot(Y, cur(F_B))
-    col_product(a, X, Y, 8, out=R)
+    low_product(a, X, Y, R)
     heavy_finish(a, R)
 
 
