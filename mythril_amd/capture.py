@@ -154,7 +154,7 @@ def replay_gpu(records: List[dict]) -> Dict[str, object]:
     for k, cs in enumerate(sets):
         try:
             for b in M.dependence_buckets(cs):
-                progs.append(compile_constraints(b, extra_consts=M.harvest_hints(b)))
+                progs.append(M._compile_search(b))
                 owner.append(k)
         except Unsupported:
             continue

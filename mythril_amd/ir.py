@@ -90,6 +90,9 @@ class Program:
     table_sizes: Dict[str, int]
     table_kinds: Dict[str, str] = field(default_factory=dict)   # name -> array | func
     stats: Dict[str, object] = field(default_factory=dict)
+    # per-leaf (offset, count) of its candidate pool in the device constant
+    # table (consts); empty unless compiled with leaf_pools
+    pool_ranges: List[Tuple[int, int]] = field(default_factory=list)
 
     @property
     def n_ins(self) -> int:
@@ -670,14 +673,67 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
     return ins, n_lds, n_spill, n_reload
 
 
+_CMP_OPS = (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE)
+POOL_CAP = 128          # candidate values per leaf pool
+
+
+def _pool_values(c: int, w: int) -> List[int]:
+    """Candidate values a leaf of width w draws from a constant c it is
+    compared with: c itself, c rounded up to a multiple of 64 (keccak UF
+    outputs are 64-aligned, keccak_function_manager.py:136-140) and, for
+    narrow leaves, every byte-aligned w-bit slice of c (calldata bytes are
+    Concat-ed into the words compared with selectors, calldata.py:47-54)."""
+    out = [c, (c + 63) & ((1 << 256) - 1) & ~63]
+    if w < 256:
+        for k in range(0, max(8, c.bit_length()), 8):
+            out.append((c >> k) & ((1 << w) - 1))
+    return out
+
+
+def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
+    """Constraint-guided candidate pools: every comparison (=, <, <=, signed
+    or not) makes the constants under it candidates for the leaves under it,
+    so a leaf draws the values it is actually tested against instead of any
+    constant of the query.  Leaves under no comparison with a constant get
+    an empty list (the caller falls back to the whole constant table)."""
+    under_l: Dict[int, frozenset] = {}
+    under_c: Dict[int, frozenset] = {}
+    pools: List[Dict[int, None]] = [dict() for _ in leaves]
+    for n in order:                                   # topological
+        if n.op == I.LEAF:
+            under_l[n.id], under_c[n.id] = frozenset((n.imm,)), frozenset()
+            continue
+        if n.op == I.CONST:
+            under_l[n.id], under_c[n.id] = frozenset(), frozenset((n.imm,))
+            continue
+        ls, cs = frozenset(), frozenset()
+        for a in n.args:
+            ls |= under_l.get(a.id, frozenset())
+            cs |= under_c.get(a.id, frozenset())
+        if len(cs) > POOL_CAP:                        # keep the walk linear-ish
+            cs = frozenset(sorted(cs)[:POOL_CAP])
+        under_l[n.id], under_c[n.id] = ls, cs
+        if n.op in _CMP_OPS and cs:
+            for li in ls:
+                p = pools[li]
+                for c in sorted(cs):
+                    for v in _pool_values(c, leaves[li].width):
+                        if len(p) < POOL_CAP:
+                            p.setdefault(v & ((1 << 256) - 1))
+    return [list(p) for p in pools]
+
+
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
-                        extra_consts: Sequence[int] = ()) -> Program:
+                        extra_consts: Sequence[int] = (), leaf_pools: bool = False) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
     optional probe nodes (256-bit values written per assignment).  ``nreg``
     is the library's register-file size (``Engine.nreg``); ``extra_consts``
-    are added to the constant pool (candidate-generator hints)."""
+    are added to the constant pool (candidate-generator hints).  With
+    ``leaf_pools`` every leaf also gets its own candidate pool
+    (``_leaf_pools``), stored after the CONST values in the device constant
+    table; ``Program.pool_ranges[leaf]`` = (offset, count) in that table."""
     lw = _Lowerer(table_sizes or {}, default_entries)
     sinks: List[LNode] = []
     for c in constraints:
@@ -711,11 +767,21 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
         code[k, 0] = op | (width << 8) | (fl[0] if fl else 0)
         code[k, 1] = I.w1(d, a, b, c)
         code[k, 2] = imm
-    consts = np.array([_limbs(v) for v in const_values], dtype=np.uint32).reshape(-1, 8)
+    table = list(const_values)
+    pool_ranges: List[Tuple[int, int]] = []
+    if leaf_pools:
+        for li, p in enumerate(_leaf_pools(order, lw.leaves)):
+            if p:
+                pool_ranges.append((len(table), len(p)))
+                table.extend(p)
+                lw.leaves[li].pool = tuple(p)
+            else:
+                pool_ranges.append((0, len(const_values)))
+    consts = np.array([_limbs(v) for v in table], dtype=np.uint32).reshape(-1, 8)
     hist: Dict[str, int] = {}
     for n in order:
         hist[I.OPNAME[n.op]] = hist.get(I.OPNAME[n.op], 0) + 1
     stats = {"lnodes": len(order), "n_ins": len(ins), "spills": n_spill, "reloads": n_reload,
              "hist": hist}
     return Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
-                   len(constraints), lw.table_sizes, lw.table_kinds, stats)
+                   len(constraints), lw.table_sizes, lw.table_kinds, stats, pool_ranges)

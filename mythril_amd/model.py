@@ -180,9 +180,19 @@ def _raw_nodes(constraints) -> List[N.Node]:
 
 def search_leafgen(prog: Program) -> List[LeafGen]:
     """Candidate generator for witness search: 20 % uniform, 20 % small,
-    20 % boundary values, 40 % constants harvested from the query (+-1)."""
+    20 % boundary values, 40 % pool values (+-1).  A program compiled with
+    leaf_pools draws each leaf's pool values from the constants it is
+    compared with (ir._leaf_pools); otherwise from every constant of the
+    query."""
     n_c = len(prog.const_values)
+    if prog.pool_ranges:
+        return [LeafGen(l.width, off, n, 20, 40, 60)
+                for l, (off, n) in zip(prog.leaves, prog.pool_ranges)]
     return [LeafGen(l.width, 0, n_c, 20, 40, 60) for l in prog.leaves]
+
+
+def _compile_search(nodes: Sequence[N.Node]) -> Program:
+    return compile_constraints(nodes, extra_consts=harvest_hints(nodes), leaf_pools=True)
 
 
 def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
@@ -252,14 +262,14 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     buckets = dependence_buckets(nodes)
     eng = get_engine()
     if len(buckets) > 1:
-        progs = [compile_constraints(b, extra_consts=harvest_hints(b)) for b in buckets]
+        progs = [_compile_search(b) for b in buckets]
         loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
         hits = eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES)
         stats.gpu_candidates += sum(SEARCH_CANDIDATES if i < 0 else i + 1 for i, _ in hits)
         if any(i < 0 for i, _ in hits):
             return None
         return _merge([unpack(p, w) for p, (_, w) in zip(progs, hits)]), progs
-    prog = compile_constraints(nodes, extra_consts=harvest_hints(nodes))
+    prog = _compile_search(nodes)
     lp = eng.load(prog, search_leafgen(prog), prog_seed=0)
     t0 = time.perf_counter()
     chunk = 1 << 20
@@ -408,7 +418,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
             cs = [c for c in cs if type(c) != bool]
             try:
                 nodes = _raw_nodes(cs)
-                progs = [compile_constraints(b, extra_consts=harvest_hints(b))
+                progs = [_compile_search(b)
                          for b in dependence_buckets(nodes)]
             except Unsupported as e:
                 stats.unsupported += 1

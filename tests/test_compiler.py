@@ -135,3 +135,67 @@ def test_deep_concat_chain_compiles():
         acc = N.bv_op("bvadd", acc, N.bv_num(i, 256))
     prog = compile_constraints([N.bv_cmp("bvult", acc, w)])
     assert prog.n_ins > 3000
+
+
+# ---- constraint-guided candidate pools (search mode) -------------------------
+
+def _table_values(prog):
+    return [sum(int(prog.consts[i, j]) << (32 * j) for j in range(8))
+            for i in range(prog.consts.shape[0])]
+
+
+def test_leaf_pools_follow_comparisons():
+    """A leaf's pool holds the constants it is compared with (and their byte
+    slices for narrow leaves), not the query's other constants."""
+    bs = [N.bv_var("b%d" % i, 8) for i in range(4)]
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    cons = [N.eq(N.concat(*bs), N.bv_num(0xA9059CBB, 32)),
+            N.eq(x, N.bv_num(0xDEADBEEF, 256)),
+            N.bv_cmp("bvult", y, N.bv_num(1000, 256))]
+    plain = compile_constraints(cons)
+    prog = compile_constraints(cons, leaf_pools=True)
+    # the CONST prefix is that of the plain compile; pools only follow it
+    assert prog.const_values == plain.const_values
+    assert prog.n_ins == plain.n_ins
+    assert _table_values(prog)[:len(prog.const_values)] == prog.const_values
+    table = _table_values(prog)
+    idx = prog.leaf_index()
+    pools = {}
+    for name, li in idx.items():
+        off, n = prog.pool_ranges[li]
+        assert 0 < n and off + n <= len(table)
+        pools[name] = set(table[off:off + n])
+        assert tuple(table[off:off + n]) == prog.leaves[li].pool
+    for i in range(4):
+        assert {0xA9, 0x05, 0x9C, 0xBB} <= pools["b%d" % i]
+        assert 0xDEADBEEF not in pools["b%d" % i]
+    assert 0xDEADBEEF in pools["x"] and 1000 not in pools["x"]
+    assert 1000 in pools["y"] and 1024 in pools["y"] and 0xDEADBEEF not in pools["y"]
+
+
+def test_leaf_without_constant_comparison_uses_whole_table():
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    cons = [N.bv_cmp("bvult", x, y), N.eq(N.bv_op("bvadd", x, N.bv_num(5, 256)), N.bv_num(9, 256))]
+    prog = compile_constraints(cons, leaf_pools=True)
+    li = prog.leaf_index()
+    assert prog.pool_ranges[li["y"]] == (0, len(prog.const_values))
+    off, n = prog.pool_ranges[li["x"]]
+    assert {5, 9} <= set(_table_values(prog)[off:off + n])
+
+
+@pytest.mark.parametrize("dag_id", [1, 7, 20])
+def test_corpus_dag_with_leaf_pools_through_ir(dag_id):
+    """Per-leaf pools only add table entries: the program still evaluates
+    exactly the DAG under generator values drawn from them."""
+    roots, _ = make_dag(dag_id)
+    prog = compile_constraints(roots, leaf_pools=True)
+    table = _table_values(prog)
+    for idx in range(12):
+        lv = []
+        for li, l in enumerate(prog.leaves):
+            off, n = prog.pool_ranges[li]
+            lv.append(gen_ref.gen_leaf(0x1234, dag_id, li, idx, l.width, table[off:off + n],
+                                       pct=(20, 40, 60)))
+        asg = to_oracle(prog, lv)
+        root, _ = ir_sim.run(prog, lv)
+        assert root == R.eval_constraints(roots, asg)

@@ -184,3 +184,31 @@ def test_replace_with_actual_sha_on_gpu(engine):
         got = [dict(t) for t in txs]
         replace_with_actual_sha(got, model, km)          # default: mg_keccak256
         assert got == want
+
+
+def test_leaf_pools_find_coupled_witness(engine):
+    """Four variables pinned to constants and coupled by one more constraint
+    (one dependence group, so splitting cannot help).  Drawing every leaf
+    from the whole constant table the joint hit is ~(1/75)^4 per candidate
+    and the search misses; with constraint-guided per-leaf pools
+    (ir._leaf_pools) each leaf hits its constant at ~1/30 and get_model
+    returns the witness."""
+    from mythril_amd.ir import compile_constraints
+    vals = [0x1234567, 0xDEADBEEF1, 0xABCDEF12345, 0x42424242]
+    xs = [BVS("p%d" % i, 256) for i in range(4)]
+    cs = [x == BVV(v, 256) for x, v in zip(xs, vals)]
+    cs.append((xs[0] + xs[1] + xs[2] + xs[3]) != BVV(7, 256))
+    raws = [c.raw for c in cs]
+    assert len(M.dependence_buckets(raws)) == 1
+    prog = compile_constraints(raws, extra_consts=M.harvest_hints(raws))
+    lp = engine.load(prog, M.search_leafgen(prog), prog_seed=0)
+    idx, _ = engine.search(lp, M.SEARCH_SEED, M.SEARCH_CANDIDATES)
+    assert idx < 0                                  # whole-table pools: a miss
+    prog = M._compile_search(raws)
+    assert prog.pool_ranges
+    lp = engine.load(prog, M.search_leafgen(prog), prog_seed=0)
+    idx, _ = engine.search(lp, M.SEARCH_SEED, M.SEARCH_CANDIDATES)
+    assert 0 <= idx < M.SEARCH_CANDIDATES
+    assert check(cs)
+    m = M.get_model(tuple(cs), enforce_execution_time=False)
+    assert [m[x.raw.params[0]] for x in xs] == vals
