@@ -46,7 +46,7 @@ def build_corpus(n_dags, workers):
         return sorted(pool.map(_compile_one, range(n_dags), chunksize=16), key=lambda t: t[0])
 
 
-def cpu_baseline(corpus, budget_s=12.0):
+def cpu_baseline(corpus, budget_s=20.0):
     """Time the C restatement oracle on a bounded sample of the same workload
     (same DAGs, same generator) with all host cores."""
     from mythril_amd.corpus import make_dag
