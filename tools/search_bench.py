@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Search-mode measurements ("Search mode may short-circuit;
+report it separately as candidates/sec"), next to bench.py's eval-mode line.
+
+Three numbers, printed as one JSON line:
+
+* ``unsat_candidates_per_s`` -- mg_search (the kernel get_model's GPU
+  pre-filter runs, mythril_amd/model.py gpu_search) on a query that no
+  candidate satisfies, so every candidate of every chunk is evaluated and
+  nothing short-circuits: x*y == 2^255+1 with x, y odd-free (both even);
+* ``corpus_batch`` -- mg_batch_search over C2 corpus DAGs (same DAGs as
+  bench.py) with 2^20 candidates each: wall time, programs solved, and the
+  candidate rate over the candidates actually needed (a solved program stops
+  at its first hit, an unsolved one scans all 2^20);
+* ``get_model_ms`` -- the drop-in ``get_model`` (reference
+  mythril/support/model.py:15-49) on the reference's own satisfiable test
+  queries (tests/laser/keccak_tests.py, smt/model_test.py,
+  state/calldata_test.py), host flattening + compile + GPU search + witness
+  check, median of 5 with the lru cache cleared; and ``batch_is_possible``
+  over the same queries as sibling states (one batched search).
+
+Usage:  python tools/search_bench.py [--dags 1024]
+"""
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def reference_sat_queries(engine):
+    from keccak_mirror import KeccakManager
+    from mythril_amd.smt import And, Array, If, symbol_factory
+    BVV, BVS = symbol_factory.BitVecVal, symbol_factory.BitVecSym
+
+    def keccak_pair(i1, i2):
+        km = KeccakManager(lambda b: engine.keccak256([b])[0])
+        o1, c1 = km.create_keccak(i1)
+        o2, c2 = km.create_keccak(i2)
+        return [And(c1, c2), o1 == o2]
+    x = BVS("x", 256)
+    cd = Array("1_calldata", 256, 8)
+    size = BVS("1_calldatasize", 256)
+    return {
+        "keccak_same8": keccak_pair(BVV(100, 8), BVV(100, 8)),
+        "keccak_sym": keccak_pair(BVS("N1", 256), BVS("N2", 256)),
+        "keccak_val_sym": keccak_pair(BVV(100, 256), BVS("N1", 256)),
+        "model_x_eq_2": [x == BVV(2, 256)],
+        "calldata_byte": [If(BVV(3, 256) < size, cd[BVV(3, 256)], BVV(0, 8)) == BVV(0xA9, 8),
+                          size == BVV(4, 256)],
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dags", type=int, default=1024)
+    ap.add_argument("--chunks", type=int, default=8, help="2^20-candidate chunks (unsat query)")
+    args = ap.parse_args()
+
+    import bench
+    import mythril_amd.model as M
+    from mythril_amd.engine import get_engine
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.smt import symbol_factory
+
+    corpus = bench.build_corpus(args.dags, min(16, os.cpu_count() or 1))
+    eng = get_engine(0)
+    out = {"device": eng.device_name}
+
+    # --- unsat query: every candidate evaluated --------------------------
+    BVS, BVV = symbol_factory.BitVecSym, symbol_factory.BitVecVal
+    x, y = BVS("sx", 256), BVS("sy", 256)
+    one = BVV(1, 256)
+    cons = [(x & one) == BVV(0, 256), (y & one) == BVV(0, 256), x * y == BVV(2**255 + 1, 256)]
+    prog = compile_constraints([c.raw for c in cons],
+                               extra_consts=M.harvest_hints([c.raw for c in cons]))
+    lp = eng.load(prog, M.search_leafgen(prog), prog_seed=0)
+    chunk = 1 << 20
+    eng.search(lp, M.SEARCH_SEED, chunk)                      # warm-up
+    t0 = time.perf_counter()
+    for k in range(args.chunks):
+        idx, _ = eng.search(lp, M.SEARCH_SEED, chunk, first_index=k * chunk)
+        assert idx < 0, "an even*even product cannot be odd"
+    dt = time.perf_counter() - t0
+    out["unsat_candidates_per_s"] = args.chunks * chunk / dt
+    out["unsat_query"] = {"ir_instructions": int(len(prog.code)), "candidates": args.chunks * chunk,
+                          "ms_per_2^20_chunk": dt * 1000.0 / args.chunks}
+
+    # --- C2 corpus, batched search -----------------------------------------
+    loaded = [eng.load(p, M.search_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
+    eng.batch_search(loaded[:8], M.SEARCH_SEED, chunk)         # warm-up
+    t0 = time.perf_counter()
+    hits = eng.batch_search(loaded, M.SEARCH_SEED, chunk)
+    dt = time.perf_counter() - t0
+    needed = sum(chunk if i < 0 else i + 1 for i, _ in hits)
+    out["corpus_batch"] = {"dags": args.dags, "candidates_per_dag": chunk,
+                           "solved": sum(i >= 0 for i, _ in hits), "wall_s": dt,
+                           "candidates_needed": needed, "candidates_per_s": needed / dt,
+                           "node_candidates_per_s": sum(
+                               (chunk if i < 0 else i + 1) * n
+                               for (i, _), (_, _, n, _) in zip(hits, corpus)) / dt}
+
+    # --- get_model on the reference's satisfiable test queries --------------
+    M.time_handler.start_execution(3600)
+    queries = reference_sat_queries(eng)
+    lat = {}
+    for name, q in queries.items():
+        ts = []
+        for _ in range(5):
+            M.get_model.cache_clear()
+            t0 = time.perf_counter()
+            M.get_model(tuple(q), enforce_execution_time=False)
+            ts.append((time.perf_counter() - t0) * 1000.0)
+        lat[name] = statistics.median(ts)
+    out["get_model_ms"] = lat
+    ts = []
+    for _ in range(5):
+        M.get_model.cache_clear()
+        t0 = time.perf_counter()
+        ok = M.batch_is_possible(list(queries.values()), enforce_execution_time=False)
+        ts.append((time.perf_counter() - t0) * 1000.0)
+        assert ok == [True] * len(queries)
+    out["batch_is_possible_ms"] = {"queries": len(queries), "median": statistics.median(ts)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
