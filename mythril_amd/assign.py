@@ -44,6 +44,15 @@ def _padded_entries(tab: Table, n: int) -> List[Tuple[int, int]]:
     return entries + [filler] * (n - len(entries))
 
 
+def lookup(tab: Table, key: int) -> int:
+    """First-match table semantics (how a z3 model interprets an array)."""
+    entries, default = tab
+    for k, v in entries:
+        if k == key:
+            return v
+    return default
+
+
 def leaf_values(program: Program, asg: Assignment) -> List[int]:
     out = []
     for leaf in program.leaves:
@@ -51,10 +60,15 @@ def leaf_values(program: Program, asg: Assignment) -> List[int]:
             v = asg.vars.get(leaf.source, 0)
         else:
             tab = asg.table(leaf.source)
-            if leaf.kind == "else":
+            if leaf.kind == "cval":
+                v = lookup(tab, program.table_ckeys[leaf.source][leaf.entry])
+            elif leaf.kind == "else":
                 v = tab[1]
             else:
-                ent = _padded_entries(tab, program.table_sizes[leaf.source])[leaf.entry]
+                # entries at constant keys are served by the cval leaves
+                ck = set(program.table_ckeys.get(leaf.source, ()))
+                rest = ([e for e in tab[0] if e[0] not in ck], tab[1]) if ck else tab
+                ent = _padded_entries(rest, program.table_sizes[leaf.source])[leaf.entry]
                 v = ent[0] if leaf.kind == "key" else ent[1]
         v = int(v) >> (CHUNK * leaf.chunk)
         out.append(v & ((1 << leaf.width) - 1))
@@ -87,8 +101,10 @@ def unpack(program: Program, leaves: np.ndarray) -> Assignment:
         if leaf.kind == "var":
             vars_[leaf.source] = vars_.get(leaf.source, 0) | part
         else:
-            t = tables.setdefault(leaf.source, {"k": {}, "v": {}, "else": 0})
-            if leaf.kind == "else":
+            t = tables.setdefault(leaf.source, {"k": {}, "v": {}, "c": {}, "else": 0})
+            if leaf.kind == "cval":
+                t["c"][leaf.entry] = t["c"].get(leaf.entry, 0) | part
+            elif leaf.kind == "else":
                 t["else"] |= part
             else:
                 d = t["k" if leaf.kind == "key" else "v"]
@@ -96,6 +112,8 @@ def unpack(program: Program, leaves: np.ndarray) -> Assignment:
     arrays, funcs = {}, {}
     for name, t in tables.items():
         n = program.table_sizes.get(name, 0)
-        tab = ([(t["k"].get(e, 0), t["v"].get(e, 0)) for e in range(n)], t["else"])
+        ck = program.table_ckeys.get(name, [])
+        tab = ([(c, t["c"].get(i, 0)) for i, c in enumerate(ck)] +
+               [(t["k"].get(e, 0), t["v"].get(e, 0)) for e in range(n)], t["else"])
         (funcs if program.table_kinds.get(name) == "func" else arrays)[name] = tab
     return Assignment(vars_, arrays, funcs)

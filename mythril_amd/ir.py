@@ -89,6 +89,10 @@ class Program:
     n_roots: int
     table_sizes: Dict[str, int]
     table_kinds: Dict[str, str] = field(default_factory=dict)   # name -> array | func
+    # per table: the constant keys it is read at (compiled with const_keys);
+    # entry i of the model is (table_ckeys[name][i], leaf "name#c<i>"), in
+    # front of the table_sizes[name] leaf-keyed entries
+    table_ckeys: Dict[str, List[int]] = field(default_factory=dict)
     stats: Dict[str, object] = field(default_factory=dict)
     # per-leaf (offset, count) of its candidate pool in the device constant
     # table (consts); empty unless compiled with leaf_pools
@@ -123,6 +127,7 @@ class _Lowerer:
         self.default_entries = default_entries
         self.consts_seen: set = set()
         self.birth = 0
+        self.table_ckeys: Dict[str, List[int]] = {}
 
     # -- hash-consed constructors ------------------------------------------
     def mk(self, op: int, width: int, args=(), imm=None) -> LNode:
@@ -423,22 +428,43 @@ class _Lowerer:
         return [self.mk(I.ITE, x.width, (c, x, y)) for x, y in zip(a, b)]
 
     def _table(self, name: str, key: List[LNode], kw: int, vw: int, kind: str) -> List[LNode]:
+        """Lookup of a free array / UF in the model's table: first match over
+        the constant-keyed entries (``table_ckeys``: the constant indices
+        the query reads, keys fixed, one value leaf each), then the
+        leaf-keyed entries (key and value leaves), then ``else`` — the
+        finite-entries-plus-default interpretation of a z3 model
+        (``laser/smt/model.py``).  A lookup at one of the constant keys is
+        that entry's value leaf itself."""
         self.table_kinds[name] = kind
         memo_key = (("T", name), tuple(k.id for k in key))
         hit = self.sel_memo.get(memo_key)
         if hit is not None:
             return hit
         entries = self.table_sizes.setdefault(name, self.default_entries)
+        ckeys = self.table_ckeys.get(name, [])
 
         def cell(kind: str, e: int, width: int) -> List[LNode]:
-            tag = {"key": "k%d" % e, "val": "v%d" % e, "else": "else"}[kind]
+            tag = {"key": "k%d" % e, "val": "v%d" % e, "else": "else", "cval": "c%d" % e}[kind]
             return [self.leaf("%s#%s#%d" % (name, tag, k), self.chunk_width(width, k), kind,
                               name, chunk=k, entry=e)
                     for k in range(self.nchunks(width))]
-        acc = cell("else", 0, vw)
-        for e in reversed(range(entries)):
-            acc = self._ite_chunks(self._chunk_eq(key, cell("key", e, kw), kw),
-                                   cell("val", e, vw), acc)
+        kval = None
+        if all(k.op == I.CONST for k in key):
+            kval = 0
+            for i, k in enumerate(key):
+                kval |= k.imm << (CHUNK * i)
+        if kval is not None and kval in ckeys:
+            acc = cell("cval", ckeys.index(kval), vw)
+        else:
+            acc = cell("else", 0, vw)
+            for e in reversed(range(entries)):
+                acc = self._ite_chunks(self._chunk_eq(key, cell("key", e, kw), kw),
+                                       cell("val", e, vw), acc)
+            if kval is None:         # a symbolic key may equal any constant key
+                for i in reversed(range(len(ckeys))):
+                    c = [self.const(ckeys[i] >> (CHUNK * k), self.chunk_width(kw, k))
+                         for k in range(self.nchunks(kw))]
+                    acc = self._ite_chunks(self._chunk_eq(key, c, kw), cell("cval", i, vw), acc)
         self.sel_memo[memo_key] = acc
         return acc
 
@@ -564,6 +590,11 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         ptr[v.id] = p
         return u[p] if p < len(u) else 1 << 60
 
+    def free_to_drop(v: LNode) -> bool:
+        """Evicting v needs no spill: constants and leaves are
+        rematerialised, a spilled value still has its slot."""
+        return v.op in (I.CONST, I.LEAF) or v.id in lds_of
+
     def alloc_reg(i: int, protect: set, oldest: bool = False) -> int:
         nonlocal n_lds, n_spill
         if free_regs:
@@ -579,16 +610,26 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
                 victim, far = v, nu
         if victim is None:
             raise Unsupported("register pressure")
+        if not free_to_drop(victim) and not free_lds and n_lds >= MAX_SPILL:
+            # spill slots exhausted: evict the furthest value that needs
+            # none (a leaf is regenerated / reloaded from the input instead)
+            victim, far = None, -1
+            for r, v in holder.items():
+                if v.id in protect or not free_to_drop(v):
+                    continue
+                nu = next_use(v, i)
+                if nu > far:
+                    victim, far = v, nu
+            if victim is None:
+                raise Unsupported("spill budget exceeded")
         r = reg_of.pop(victim.id)
         del holder[r]
-        if victim.op != I.CONST and victim.id not in lds_of:
+        if not free_to_drop(victim):
             if free_lds:
                 s = free_lds.pop()
             else:
                 s = n_lds
                 n_lds += 1
-                if n_lds > MAX_SPILL:
-                    raise Unsupported("spill budget exceeded")
             lds_of[victim.id] = s
             ins.append((I.SPILL, 1, trash, r, 0, 0, s))
             n_spill += 1
@@ -599,9 +640,11 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         reg_clean[r] = v.width <= 32
         if v.op == I.CONST:
             ins.append((I.CONST, v.width, r, 0, 0, 0, const_index[v.imm]))
-        else:
+        elif v.id in lds_of:
             ins.append((I.RELOAD, v.width, r, 0, 0, 0, lds_of[v.id]))
             n_reload += 1
+        else:                                   # a leaf evicted without a spill
+            ins.append((I.LEAF, v.width, r, 0, 0, 0, v.imm))
 
     def release(v: LNode, i: int):
         if next_use(v, i + 1) >= (1 << 60):
@@ -699,6 +742,8 @@ def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
     under_l: Dict[int, frozenset] = {}
     under_c: Dict[int, frozenset] = {}
     pools: List[Dict[int, None]] = [dict() for _ in leaves]
+    pv: Dict[Tuple[int, int], List[int]] = {}
+    M256 = (1 << 256) - 1
     for n in order:                                   # topological
         if n.op == I.LEAF:
             under_l[n.id], under_c[n.id] = frozenset((n.imm,)), frozenset()
@@ -714,27 +759,94 @@ def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
             cs = frozenset(sorted(cs)[:POOL_CAP])
         under_l[n.id], under_c[n.id] = ls, cs
         if n.op in _CMP_OPS and cs:
+            ordered = None
             for li in ls:
                 p = pools[li]
-                for c in sorted(cs):
-                    for v in _pool_values(c, leaves[li].width):
-                        if len(p) < POOL_CAP:
-                            p.setdefault(v & ((1 << 256) - 1))
+                if len(p) >= POOL_CAP:
+                    continue
+                w = leaves[li].width
+                if ordered is None:
+                    ordered = sorted(cs)
+                for c in ordered:
+                    vals = pv.get((c, w))
+                    if vals is None:
+                        vals = pv[(c, w)] = [v & M256 for v in _pool_values(c, w)]
+                    for v in vals:
+                        p.setdefault(v)
+                        if len(p) >= POOL_CAP:
+                            break
+                    if len(p) >= POOL_CAP:
+                        break
     return [list(p) for p in pools]
+
+
+CKEY_CAP = 128          # constant-keyed entries per table
+CKEY_LINKS = 2048       # symbolic-key lookups x constant keys per table
+
+
+def scan_const_keys(nodes: Sequence[Node], cap: int = CKEY_CAP,
+                    max_links: int = CKEY_LINKS) -> Dict[str, List[int]]:
+    """The constant indices every free array / UF is read at: ``select`` over
+    a store / ite chain ending in a free array, and UF applications, whose
+    index is a numeral (calldata bytes at fixed offsets, ``calldata.py:219-
+    232``; storage slots at fixed keys, ``account.py:37-62``).  A lookup at a
+    symbolic index compares it with every constant key, so a table whose
+    symbolic lookups x constant keys exceed ``max_links`` keeps the plain
+    leaf-keyed form (e.g. calldata read at a symbolic ABI offset)."""
+    out: Dict[str, Dict[int, None]] = {}
+    sym: Dict[str, set] = {}
+
+    def bases(a: Node):
+        stack, seen = [a], set()
+        while stack:
+            x = stack.pop()
+            if x.id in seen:
+                continue
+            seen.add(x.id)
+            if x.op == "store":
+                stack.append(x.args[0])
+            elif x.op == "ite":
+                stack.extend(x.args[1:])
+            elif x.op == "array":
+                yield x.params[0]
+
+    def note(name: str, key: Node):
+        if key.op == "bvnum":
+            d = out.setdefault(name, {})
+            if len(d) < cap:
+                d.setdefault(key.params[0])
+        else:
+            sym.setdefault(name, set()).add(key.id)
+
+    for n in topo_order(list(nodes)):
+        if n.op == "select":
+            for name in bases(n.args[0]):
+                note(name, n.args[1])
+        elif n.op == "apply":
+            note(n.params[0], n.args[0])
+    return {k: sorted(v) for k, v in out.items()
+            if v and len(sym.get(k, ())) * len(v) <= max_links}
 
 
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
-                        extra_consts: Sequence[int] = (), leaf_pools: bool = False) -> Program:
+                        extra_consts: Sequence[int] = (), leaf_pools: bool = False,
+                        const_keys: bool = False) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
     optional probe nodes (256-bit values written per assignment).  ``nreg``
     is the library's register-file size (``Engine.nreg``); ``extra_consts``
     are added to the constant pool (candidate-generator hints).  With
     ``leaf_pools`` every leaf also gets its own candidate pool
     (``_leaf_pools``), stored after the CONST values in the device constant
-    table; ``Program.pool_ranges[leaf]`` = (offset, count) in that table."""
+    table; ``Program.pool_ranges[leaf]`` = (offset, count) in that table.
+    With ``const_keys`` every free array / UF gets one constant-keyed entry
+    per numeral index it is read at (``scan_const_keys``), so reads at fixed
+    offsets are plain leaves instead of lookups in a small leaf-keyed table
+    (search mode: every calldata byte a query reads can differ)."""
     lw = _Lowerer(table_sizes or {}, default_entries)
+    if const_keys:
+        lw.table_ckeys = scan_const_keys(list(constraints) + list(probes))
     sinks: List[LNode] = []
     for c in constraints:
         if not c.is_bool():
@@ -783,5 +895,6 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
         hist[I.OPNAME[n.op]] = hist.get(I.OPNAME[n.op], 0) + 1
     stats = {"lnodes": len(order), "n_ins": len(ins), "spills": n_spill, "reloads": n_reload,
              "hist": hist}
+    ckeys = {k: v for k, v in lw.table_ckeys.items() if k in lw.table_kinds}
     return Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
-                   len(constraints), lw.table_sizes, lw.table_kinds, stats, pool_ranges)
+                   len(constraints), lw.table_sizes, lw.table_kinds, ckeys, stats, pool_ranges)

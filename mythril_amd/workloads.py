@@ -1,0 +1,593 @@
+"""Shape-faithful stand-ins for the captured-query configs of BASELINE.json
+(C1 ``suicide.sol -t 2``, C3 ``BECToken.sol -t 3`` integer-overflow checks,
+C4 ``WalletLibrary.sol`` + ``token.sol`` mapping/storage constraints).
+
+These are NOT captured queries: capturing needs z3 and solc, which exist on
+neither this container nor the GPU box.  Each query is built
+with the z3-free ``laser.smt`` mirror (:mod:`mythril_amd.smt`) by replaying,
+opcode handler by opcode handler, the lowering LASER applies on the path a
+function call takes through the contract's compiled dispatcher:
+
+* transaction setup — ``sender_{N}`` constrained to the three actors
+  (``transaction/symbolic.py:165-167``), ``UGE(balance[sender], call_value{N})``
+  and the balance transfer store chain (``transaction_models.py:121-133``);
+* calldata — ``{N}_calldata`` (256 -> 8) and ``{N}_calldatasize``; a word is
+  ``Concat`` of 32 ``If(off + i < size, calldata[off + i], 0)`` with the
+  SIGNED ``<`` of ``BitVec.__lt__`` (``calldata.py:47-54,219-232``);
+* dispatcher — ``Not(ULT(calldatasize, 4))``, the selector
+  ``0xffffffff & UDiv(word(0), 2**224)`` compared with each function id
+  (``instructions.py:480-490,330-352,716-740``), a JUMPI appending ``condi`` or
+  ``Not(condi)`` (``instructions.py:1543-1619``), ISZERO as ``If(.., 1, 0)``
+  (``:743-760``) so a BitVec JUMPI condition becomes ``x != 0``;
+* mappings — ``sha3`` of ``Concat(key, slot)`` as the keccak UF pair with the
+  interval / mod-64 / known-hash condition (``keccak_function_manager.py:
+  83-149``, ``instructions.py:1010-1048``; concrete data hashed on the host),
+  read and written through the ``Storage{addr}`` store chain
+  (``state/account.py:18-82``; ``K(256, 256, 0)`` after a creation
+  transaction);
+* overflow checks — ``Not(BVAddNoOverflow)``, ``Not(BVMulNoOverflow)``,
+  ``Not(BVSubNoUnderflow)`` on the operands of ADD / MUL / SUB, appended to
+  the path constraints at the transaction end exactly as the integer module
+  poses them (``analysis/module/modules/integer.py:143-157,268-280``).
+
+z3's ``simplify`` is not reproduced (``smt.simplify`` is structural), so the
+DAGs carry LASER's pre-simplification shapes.  Every query is a list of Bool
+DAG nodes, the argument ``get_model`` receives.
+"""
+
+from __future__ import annotations
+
+import random
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from . import smt as S
+from .smt import node as N
+
+# ---------------------------------------------------------------------------
+# host Keccak-256 for concrete hash data (keccak_function_manager.py:43-57
+# hashes concrete inputs on the host with ethereum.utils.sha3)
+# ---------------------------------------------------------------------------
+
+_RC = [0x0000000000000001, 0x0000000000008082, 0x800000000000808A, 0x8000000080008000,
+       0x000000000000808B, 0x0000000080000001, 0x8000000080008081, 0x8000000000008009,
+       0x000000000000008A, 0x0000000000000088, 0x0000000080008009, 0x000000008000000A,
+       0x000000008000808B, 0x800000000000008B, 0x8000000000008089, 0x8000000000008003,
+       0x8000000000008002, 0x8000000000000080, 0x000000000000800A, 0x800000008000000A,
+       0x8000000080008081, 0x8000000000008080, 0x0000000080000001, 0x8000000080008008]
+_ROT = [[0, 36, 3, 41, 18], [1, 44, 10, 45, 2], [62, 6, 43, 15, 61], [28, 55, 25, 21, 56],
+        [27, 20, 39, 8, 14]]
+_M = (1 << 64) - 1
+
+
+def _rol(x: int, n: int) -> int:
+    return ((x << n) | (x >> (64 - n))) & _M if n else x
+
+
+def keccak256(data: bytes) -> bytes:
+    """Keccak-256 (original 0x01 padding, as Ethereum uses)."""
+    rate = 136
+    msg = bytearray(data) + b"\x01" + b"\x00" * ((-len(data) - 1) % rate)
+    msg[-1] |= 0x80
+    st = [[0] * 5 for _ in range(5)]
+    for off in range(0, len(msg), rate):
+        for i in range(rate // 8):
+            st[i % 5][i // 5] ^= int.from_bytes(msg[off + 8 * i: off + 8 * i + 8], "little")
+        for rc in _RC:
+            c = [st[x][0] ^ st[x][1] ^ st[x][2] ^ st[x][3] ^ st[x][4] for x in range(5)]
+            d = [c[(x - 1) % 5] ^ _rol(c[(x + 1) % 5], 1) for x in range(5)]
+            st = [[st[x][y] ^ d[x] for y in range(5)] for x in range(5)]
+            b = [[0] * 5 for _ in range(5)]
+            for x in range(5):
+                for y in range(5):
+                    b[y][(2 * x + 3 * y) % 5] = _rol(st[x][y], _ROT[x][y])
+            st = [[b[x][y] ^ (~b[(x + 1) % 5][y] & b[(x + 2) % 5][y]) for y in range(5)]
+                  for x in range(5)]
+            st[0][0] ^= rc
+    return b"".join(st[i % 5][i // 5].to_bytes(8, "little") for i in range(4))
+
+
+def selector(signature: str) -> int:
+    return int.from_bytes(keccak256(signature.encode())[:4], "big")
+
+
+# ---------------------------------------------------------------------------
+# keccak UF pairs (keccak_function_manager.py:24-149)
+# ---------------------------------------------------------------------------
+
+TOTAL_PARTS = 10 ** 40
+PART = (2 ** 256 - 1) // TOTAL_PARTS
+INTERVAL_DIFFERENCE = 10 ** 30
+
+
+class KeccakFunctionManager:
+    """``KeccakFunctionManager``: ``keccak256_N`` / ``keccak256_N-1`` UF pairs,
+    one interval ``[idx*PART, idx*PART + PART)`` per input width, outputs
+    ``= 0 mod 64``, and an ``Or`` over every concrete hash seen so far."""
+
+    def __init__(self, hasher=keccak256):
+        self.hasher = hasher
+        self.store_function: Dict[int, Tuple[S.Function, S.Function]] = {}
+        self.interval_hook_for_size: Dict[int, int] = {}
+        self._index_counter = TOTAL_PARTS - 34534
+        self.concrete_hashes: Dict[S.BitVec, S.BitVec] = {}
+        self.hash_result_store: Dict[int, List[S.BitVec]] = {}
+
+    def get_function(self, length: int):
+        if length not in self.store_function:
+            self.store_function[length] = (S.Function("keccak256_{}".format(length), length, 256),
+                                           S.Function("keccak256_{}-1".format(length), 256, length))
+            self.hash_result_store[length] = []
+        return self.store_function[length]
+
+    def get_concrete_hash_data(self, model) -> Dict[int, List[int]]:
+        """``keccak_function_manager.py:103-119``: the model's values of every
+        symbolic hash created so far, per input size."""
+        out: Dict[int, List[int]] = {}
+        for size, vals in self.hash_result_store.items():
+            out[size] = []
+            for val in vals:
+                try:
+                    ev = model.eval(val.raw)
+                    out[size].append(ev.as_long() if hasattr(ev, "as_long") else int(ev))
+                except (AttributeError, TypeError):
+                    continue
+        return out
+
+    def find_concrete_keccak(self, data: S.BitVec) -> S.BitVec:
+        digest = self.hasher(data.value.to_bytes(data.size() // 8, "big"))
+        return S.symbol_factory.BitVecVal(int.from_bytes(digest, "big"), 256)
+
+    def create_keccak(self, data: S.BitVec):
+        length = data.size()
+        func, inverse = self.get_function(length)
+        if not data.symbolic:
+            h = self.find_concrete_keccak(data)
+            self.concrete_hashes[data] = h
+            return h, S.And(func(data) == h, inverse(func(data)) == data)
+        cond = self._create_condition(data)
+        self.hash_result_store[length].append(func(data))
+        return func(data), cond
+
+    def _create_condition(self, func_input: S.BitVec) -> S.Bool:
+        length = func_input.size()
+        func, inv = self.get_function(length)
+        if length not in self.interval_hook_for_size:
+            self.interval_hook_for_size[length] = self._index_counter
+            self._index_counter -= INTERVAL_DIFFERENCE
+        lower = self.interval_hook_for_size[length] * PART
+        upper = lower + PART
+        cond = S.And(inv(func(func_input)) == func_input,
+                     S.ULE(S.symbol_factory.BitVecVal(lower, 256), func(func_input)),
+                     S.ULT(func(func_input), S.symbol_factory.BitVecVal(upper, 256)),
+                     S.URem(func(func_input), S.symbol_factory.BitVecVal(64, 256)) == 0)
+        concrete_cond = S.symbol_factory.Bool(False)
+        for key, keccak in self.concrete_hashes.items():
+            concrete_cond = S.Or(concrete_cond, S.And(func(func_input) == keccak, key == func_input))
+        return S.And(inv(func(func_input)) == func_input, S.Or(cond, concrete_cond))
+
+
+# ---------------------------------------------------------------------------
+# symbolic world / transactions
+# ---------------------------------------------------------------------------
+
+ACTORS = (0xAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFEAFFE,      # CREATOR
+          0xDEADBEEFDEADBEEFDEADBEEFDEADBEEFDEADBEEF,      # ATTACKER
+          0xAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAAA)      # SOMEGUY
+CONTRACT = 0x0901D12EBE1B195E5AA8748E62BD7734AE19B51F
+ADDR_MASK = (1 << 160) - 1
+
+
+def bv(v: int, w: int = 256) -> S.BitVec:
+    return S.symbol_factory.BitVecVal(v, w)
+
+
+def _bitvec(x) -> S.BitVec:
+    """``util.pop_bitvec`` (``laser/ethereum/util.py:67-88``)."""
+    if isinstance(x, S.Bool):
+        return S.If(x, bv(1), bv(0))
+    if isinstance(x, int):
+        return bv(x)
+    return x
+
+
+class Calldata:
+    """``SymbolicCalldata`` (``calldata.py:207-232``)."""
+
+    def __init__(self, tx_id: int):
+        self.size = S.symbol_factory.BitVecSym("{}_calldatasize".format(tx_id), 256)
+        self.array = S.Array("{}_calldata".format(tx_id), 256, 8)
+
+    def load(self, item: S.BitVec) -> S.BitVec:
+        return S.If(item < self.size, self.array[item], bv(0, 8))
+
+    def word(self, offset) -> S.BitVec:
+        """``get_word_at`` over the slice walk of ``BaseCalldata.__getitem__``:
+        concrete offsets give constant indices, symbolic ones ``off + i``."""
+        if isinstance(offset, int):
+            parts = [self.load(bv(offset + i)) for i in range(32)]
+        else:
+            parts = [self.load(offset if i == 0 else offset + bv(i)) for i in range(32)]
+        return S.Concat(parts)
+
+
+class Storage:
+    """``Storage`` (``account.py:18-62``): ``K(256, 256, 0)`` for an account
+    created by the analysed creation transaction, ``Storage{addr}`` else."""
+
+    def __init__(self, address: int, concrete: bool):
+        self.array = S.K(256, 256, 0) if concrete else S.Array("Storage{}".format(address), 256, 256)
+
+    def __getitem__(self, item: S.BitVec) -> S.BitVec:
+        return self.array[item]
+
+    def __setitem__(self, key: S.BitVec, value) -> None:
+        self.array[key] = _bitvec(value)
+
+
+class World:
+    """Path constraints, balances, storage and the keccak manager of one
+    symbolic execution path (``world_state.py``)."""
+
+    def __init__(self, concrete_storage: bool = True):
+        self.constraints: List[S.Bool] = []
+        self.balance = S.Array("balance", 256, 256)          # world_state.py:33
+        self.storage = Storage(CONTRACT, concrete_storage)
+        self.kfm = KeccakFunctionManager()
+        self.next_tx = 0
+
+    def tx(self, creation: bool = False) -> "Tx":
+        t = Tx(self, self.next_tx, creation)
+        self.next_tx += 1
+        return t
+
+    def query(self, extra: Sequence[S.Bool] = ()) -> List[N.Node]:
+        return [c.raw for c in list(self.constraints) + list(extra)]
+
+
+class Tx:
+    """One message call (``transaction/symbolic.py:70-108``) or the contract
+    creation (``:110-150``, caller = CREATOR)."""
+
+    def __init__(self, world: World, tx_id: int, creation: bool):
+        self.world = world
+        self.id = tx_id
+        self.caller = bv(ACTORS[0]) if creation else S.symbol_factory.BitVecSym(
+            "sender_{}".format(tx_id), 256)
+        self.callvalue = S.symbol_factory.BitVecSym("call_value{}".format(tx_id), 256)
+        self.calldata = Calldata(tx_id)
+        # initial_global_state_from_environment (transaction_models.py:121-133)
+        bal = world.balance
+        world.constraints.append(S.UGE(bal[self.caller], self.callvalue))
+        bal[bv(CONTRACT)] = bal[bv(CONTRACT)] + self.callvalue
+        bal[self.caller] = bal[self.caller] - self.callvalue
+        # _setup_global_state_for_execution (symbolic.py:165-167)
+        world.constraints.append(S.Or(*[self.caller == bv(a) for a in ACTORS]))
+
+    # -- control flow -----------------------------------------------------------
+    def jumpi(self, condition, taken: bool) -> None:
+        """``jumpi_``: the true branch appends ``condi``, the false branch
+        ``Not(condition)`` (a BitVec condition is compared with 0)."""
+        if isinstance(condition, S.Bool):
+            c = condition if taken else S.Not(condition)
+        else:
+            c = (condition != 0) if taken else (condition == 0)
+        self.world.constraints.append(c)
+
+    @staticmethod
+    def iszero(x) -> S.BitVec:
+        e = S.Not(x) if isinstance(x, S.Bool) else (x == 0)
+        return S.If(e, bv(1), bv(0))
+
+    def require(self, cond) -> None:
+        """``require(c)``: ``c ISZERO PUSH tag JUMPI`` falls through on c."""
+        self.jumpi(self.iszero(cond), taken=False)
+
+    # -- ABI ----------------------------------------------------------------------
+    def selector_expr(self) -> S.BitVec:
+        return bv(0xFFFFFFFF) & S.UDiv(self.calldata.word(0), bv(1 << 224))
+
+    def dispatch(self, selectors: Sequence[int], k: int) -> None:
+        """The function dispatcher down to ``selectors[k]``."""
+        self.jumpi(S.ULT(self.calldata.size, bv(4)), taken=False)
+        sel = self.selector_expr()
+        for j in range(k + 1):
+            self.jumpi(bv(selectors[j]) == sel, taken=(j == k))
+
+    def nonpayable(self) -> None:
+        self.jumpi(self.iszero(self.callvalue), taken=True)
+
+    def arg(self, i: int) -> S.BitVec:
+        return self.calldata.word(4 + 32 * i)
+
+    def arg_address(self, i: int) -> S.BitVec:
+        return bv(ADDR_MASK) & self.arg(i)
+
+    def sender(self) -> S.BitVec:
+        return bv(ADDR_MASK) & self.caller
+
+    # -- storage ------------------------------------------------------------------
+    def sha3(self, data: S.BitVec) -> S.BitVec:
+        h, cond = self.world.kfm.create_keccak(data)
+        self.world.constraints.append(cond)
+        return h
+
+    def mapping(self, key: S.BitVec, slot: int) -> S.BitVec:
+        """``keccak256(key . slot)``: the 64-byte memory of the Solidity
+        mapping access, as one 512-bit Concat."""
+        if not key.symbolic:
+            return self.sha3(bv((key.value << 256) | slot, 512))
+        return self.sha3(S.Concat(key, bv(slot)))
+
+    def sload(self, idx) -> S.BitVec:
+        return self.world.storage[_bitvec(idx)]
+
+    def sstore(self, idx, value) -> None:
+        self.world.storage[_bitvec(idx)] = value
+
+
+# ---------------------------------------------------------------------------
+# C1: suicide.sol -t 2
+# ---------------------------------------------------------------------------
+
+SUICIDE_FUNCS = [selector("kill(address)")]
+
+
+def c1_queries(n: int = 64, seed: int = 0xC1) -> List[List[N.Node]]:
+    """``Suicide.kill(address)`` over two transactions (``-t 2``): the
+    is_possible checks of every JUMPI branch (``svm.py:257-262``) and the
+    SWC-106 check ``addr == 0`` at SELFDESTRUCT."""
+    rng = random.Random(seed)
+    out: List[List[N.Node]] = []
+    while len(out) < n:
+        w = World(concrete_storage=True)
+        for _ in range(1 + rng.randrange(2)):
+            t = w.tx()
+            if rng.randrange(3) == 0:                       # fallback: size < 4
+                t.jumpi(S.ULT(t.calldata.size, bv(4)), taken=True)
+                out.append(w.query())
+                continue
+            t.dispatch(SUICIDE_FUNCS, 0)
+            out.append(w.query())
+            addr = t.arg_address(0)
+            hit = rng.randrange(2) == 0
+            t.jumpi(S.Not(addr == bv(0)) if rng.randrange(2) else (addr == bv(0)), taken=hit)
+            out.append(w.query())
+    return out[:n]
+
+
+# ---------------------------------------------------------------------------
+# C3: BECToken.sol -t 3 integer-overflow checks
+# ---------------------------------------------------------------------------
+
+BEC_FUNCS = sorted(selector(s) for s in (
+    "transfer(address,uint256)", "transferFrom(address,address,uint256)",
+    "approve(address,uint256)", "batchTransfer(address[],uint256)",
+    "increaseApproval(address,uint256)", "decreaseApproval(address,uint256)",
+    "balanceOf(address)", "allowance(address,address)", "pause()", "unpause()"))
+_BAL, _ALLOW, _OWNER_PAUSED, _TOTAL = 1, 2, 3, 0
+
+
+def _when_not_paused(t: Tx) -> None:
+    packed = t.sload(bv(_OWNER_PAUSED))                        # owner | paused << 160
+    paused = bv(0xFF) & S.UDiv(packed, bv(1 << 160))
+    t.require(t.iszero(paused))
+
+
+def _bec_transfer(t: Tx, checks: List[S.Bool], from_arg: bool) -> None:
+    k = BEC_FUNCS.index(selector("transferFrom(address,address,uint256)" if from_arg
+                                 else "transfer(address,uint256)"))
+    t.dispatch(BEC_FUNCS, k)
+    t.nonpayable()
+    _when_not_paused(t)
+    frm = t.arg_address(0) if from_arg else t.sender()
+    to = t.arg_address(1 if from_arg else 0)
+    value = t.arg(2 if from_arg else 1)
+    t.require(S.Not(to == bv(0)))
+    slot_from = t.mapping(frm, _BAL)
+    bal_from = t.sload(slot_from)
+    t.require(S.And(S.UGT(value, bv(0)), S.Not(S.UGT(value, bal_from))))
+    if from_arg:                                                # allowed[_from][msg.sender]
+        allow = t.sload(t.sha3(S.Concat(t.sender(), t.mapping(frm, _ALLOW))))
+        t.require(S.Not(S.UGT(value, allow)))
+    # SafeMath.sub: assert(b <= a); SUB annotated by the integer module
+    t.require(S.Not(S.UGT(value, bal_from)))
+    checks.append(S.Not(S.BVSubNoUnderflow(bal_from, value, False)))
+    t.sstore(slot_from, bal_from - value)
+    slot_to = t.mapping(to, _BAL)
+    bal_to = t.sload(slot_to)
+    s = bal_to + value
+    checks.append(S.Not(S.BVAddNoOverflow(bal_to, value, False)))
+    t.require(S.Not(S.ULT(s, bal_to)))                         # SafeMath.add: assert(c >= a)
+    t.sstore(slot_to, s)
+
+
+def _bec_batch(t: Tx, checks: List[S.Bool], receivers: int) -> None:
+    t.dispatch(BEC_FUNCS, BEC_FUNCS.index(selector("batchTransfer(address[],uint256)")))
+    t.nonpayable()
+    _when_not_paused(t)
+    off = t.arg(0)                                              # ABI offset of _receivers
+    cnt = t.calldata.word(off + bv(4))                          # _receivers.length
+    value = t.arg(1)
+    amount = cnt * value
+    checks.append(S.Not(S.BVMulNoOverflow(cnt, value, False)))
+    t.require(S.And(S.UGT(cnt, bv(0)), S.Not(S.UGT(cnt, bv(20)))))
+    slot_s = t.mapping(t.sender(), _BAL)
+    bal_s = t.sload(slot_s)
+    t.require(S.And(S.UGT(value, bv(0)), S.Not(S.ULT(bal_s, amount))))
+    t.require(S.Not(S.UGT(amount, bal_s)))
+    checks.append(S.Not(S.BVSubNoUnderflow(bal_s, amount, False)))
+    t.sstore(slot_s, bal_s - amount)
+    for i in range(receivers):
+        t.jumpi(S.ULT(bv(i), cnt), taken=True)                 # for (i < cnt)
+        rcv = bv(ADDR_MASK) & t.calldata.word(off + bv(36 + 32 * i))
+        slot_r = t.mapping(rcv, _BAL)
+        bal_r = t.sload(slot_r)
+        checks.append(S.Not(S.BVAddNoOverflow(bal_r, value, False)))
+        t.require(S.Not(S.ULT(bal_r + value, bal_r)))
+        t.sstore(slot_r, bal_r + value)
+    t.jumpi(S.ULT(bv(receivers), cnt), taken=False)
+
+
+def _bec_approve(t: Tx, checks: List[S.Bool], increase: bool) -> None:
+    name = "increaseApproval(address,uint256)" if increase else "approve(address,uint256)"
+    t.dispatch(BEC_FUNCS, BEC_FUNCS.index(selector(name)))
+    t.nonpayable()
+    _when_not_paused(t)
+    spender, value = t.arg_address(0), t.arg(1)
+    outer = t.mapping(t.sender(), _ALLOW)
+    slot = t.sha3(S.Concat(spender, outer))                     # allowed[owner][spender]
+    if increase:
+        cur = t.sload(slot)
+        checks.append(S.Not(S.BVAddNoOverflow(cur, value, False)))
+        t.require(S.Not(S.ULT(cur + value, cur)))
+        t.sstore(slot, cur + value)
+    else:
+        t.sstore(slot, value)
+
+
+def c3_queries(n: int = 256, seed: int = 0xC3) -> List[List[N.Node]]:
+    """BECToken under ``-t 3``: up to three transactions after the creation
+    transaction; every ADD/MUL/SUB the integer module annotates becomes one
+    query ``path constraints + [Not(BV*NoOverflow(..))]`` at the end of the
+    transaction (``integer.py:268-280``)."""
+    rng = random.Random(seed)
+    out: List[List[N.Node]] = []
+    while len(out) < n:
+        w = World(concrete_storage=True)
+        c = w.tx(creation=True)                                 # constructor: totalSupply
+        supply = bv(7000000000 * 10 ** 18)
+        c.sstore(bv(_TOTAL), supply)
+        c.sstore(c.mapping(bv(ACTORS[0]), _BAL), supply)
+        c.sstore(bv(_OWNER_PAUSED), bv(ACTORS[0]))
+        for _ in range(1 + rng.randrange(3)):
+            t = w.tx()
+            checks: List[S.Bool] = []
+            kind = rng.randrange(6)
+            if kind == 0:
+                _bec_batch(t, checks, 1 + rng.randrange(2))
+            elif kind in (1, 2):
+                _bec_transfer(t, checks, from_arg=kind == 2)
+            elif kind == 3:
+                _bec_approve(t, checks, increase=True)
+            elif kind == 4:
+                _bec_approve(t, checks, increase=False)
+            else:
+                _bec_batch(t, checks, 1)
+            for chk in checks:
+                out.append(w.query([chk]))
+    return out[:n]
+
+
+# ---------------------------------------------------------------------------
+# C4: WalletLibrary.sol + token.sol mapping / storage constraints
+# ---------------------------------------------------------------------------
+
+TOKEN_FUNCS = sorted(selector(s) for s in ("transfer(address,uint256)", "balanceOf(address)",
+                                           "totalSupply()"))
+WALLET_FUNCS = sorted(selector(s) for s in (
+    "isOwner(address)", "confirm(bytes32)", "addOwner(address)", "execute(address,uint256,bytes)",
+    "revoke(bytes32)", "changeOwner(address,address)", "kill(address)",
+    "hasConfirmed(bytes32,address)", "initWallet(address[],uint256,uint256)"))
+_W_REQUIRED, _W_NUMOWNERS, _W_OWNERS, _W_OWNERIDX, _W_PENDING = 0, 1, 2, 0x103, 0x104
+
+
+def _token_transfer(t: Tx, checks: List[S.Bool]) -> None:
+    """``token.sol`` ``transfer``: ``require(balances[msg.sender] - _value
+    >= 0)`` (always true: the underflow is the finding), ``-=``, ``+=``."""
+    t.dispatch(TOKEN_FUNCS, TOKEN_FUNCS.index(selector("transfer(address,uint256)")))
+    to, value = t.arg_address(0), t.arg(1)
+    slot_s = t.mapping(t.sender(), 0)
+    bal_s = t.sload(slot_s)
+    checks.append(S.Not(S.BVSubNoUnderflow(bal_s, value, False)))
+    t.require(S.Not(S.ULT(bal_s - value, bv(0))))
+    t.sstore(slot_s, t.sload(slot_s) - value)
+    slot_t = t.mapping(to, 0)
+    bal_t = t.sload(slot_t)
+    checks.append(S.Not(S.BVAddNoOverflow(bal_t, value, False)))
+    t.sstore(slot_t, bal_t + value)
+
+
+def _wallet_owner_index(t: Tx, who: S.BitVec) -> S.BitVec:
+    return t.sload(t.mapping(who, _W_OWNERIDX))                  # m_ownerIndex[uint(who)]
+
+
+def _wallet_call(t: Tx, kind: int, checks: List[S.Bool], rng: random.Random) -> None:
+    names = ["isOwner(address)", "confirm(bytes32)", "addOwner(address)",
+             "execute(address,uint256,bytes)", "revoke(bytes32)", "kill(address)"]
+    name = names[kind % len(names)]
+    t.dispatch(WALLET_FUNCS, WALLET_FUNCS.index(selector(name)))
+    if name == "isOwner(address)":
+        t.jumpi(S.UGT(_wallet_owner_index(t, t.arg_address(0)), bv(0)), taken=rng.randrange(2) == 0)
+        return
+    t.nonpayable()
+    if name in ("addOwner(address)", "kill(address)"):
+        # onlymanyowners(keccak256(msg.data)): symbolic length -> forced 64
+        t.world.constraints.append(t.calldata.size == bv(64))
+        op = t.sha3(S.Concat(t.calldata.word(0), t.calldata.word(32)))
+    elif name == "execute(address,uint256,bytes)":
+        idx = _wallet_owner_index(t, t.sender())                  # onlyowner
+        t.require(S.UGT(idx, bv(0)))
+        value = t.arg(1)
+        spent = t.sload(bv(0x105))
+        checks.append(S.Not(S.BVAddNoOverflow(spent, value, False)))
+        t.require(S.Not(S.UGT(spent + value, t.sload(bv(0x106)))))
+        return
+    else:
+        op = t.arg(0)                                            # confirm / revoke(_h)
+    # confirmAndCheck(_operation)
+    idx = _wallet_owner_index(t, t.sender())
+    t.require(S.Not(idx == bv(0)))
+    pending = t.mapping(op, _W_PENDING)                         # m_pending[_operation]
+    needed = t.sload(pending)
+    t.jumpi(needed == bv(0), taken=rng.randrange(2) == 0)
+    bit = t.sload(pending + bv(1))                              # ownersDone
+    t.require(S.Not((bit & bv(1)) == bv(0)) if name == "revoke(bytes32)" else
+              ((bit & bv(1)) == bv(0)))
+    checks.append(S.Not(S.BVSubNoUnderflow(needed, bv(1), False)))
+    t.sstore(pending, needed - bv(1))
+
+
+def c4_queries(n: int = 256, seed: int = 0xC4) -> List[List[N.Node]]:
+    """``token.sol`` transfers and ``WalletLibrary`` owner / multi-sig paths
+    over 1-3 transactions: every storage access is a keccak UF application
+    over a 512-bit ``Concat(key, slot)`` read through a store chain, and
+    every transaction carries its keccak conditions (the C4 shape)."""
+    rng = random.Random(seed)
+    out: List[List[N.Node]] = []
+    while len(out) < n:
+        w = World(concrete_storage=True)
+        c = w.tx(creation=True)
+        wallet = rng.randrange(2) == 0
+        if wallet:                                              # initWallet([creator], 1, limit)
+            c.sstore(bv(_W_NUMOWNERS), bv(1))
+            c.sstore(bv(_W_OWNERS + 1), bv(ACTORS[0]))
+            c.sstore(c.mapping(bv(ACTORS[0]), _W_OWNERIDX), bv(1))
+            c.sstore(bv(_W_REQUIRED), bv(1))
+        else:                                                   # constructor(_initialSupply)
+            supply = c.arg(0)
+            c.sstore(bv(1), supply)
+            c.sstore(c.mapping(bv(ACTORS[0]), 0), supply)
+        for _ in range(1 + rng.randrange(3)):
+            t = w.tx()
+            checks: List[S.Bool] = []
+            if wallet:
+                _wallet_call(t, rng.randrange(6), checks, rng)
+            else:
+                _token_transfer(t, checks)
+            out.append(w.query())                              # is_possible of the new state
+            for chk in checks:
+                out.append(w.query([chk]))
+    return out[:n]
+
+
+WORKLOADS = {"c1": c1_queries, "c3": c3_queries, "c4": c4_queries}
+
+
+def queries(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> List[List[N.Node]]:
+    fn = WORKLOADS[name.lower()]
+    kw = {}
+    if n is not None:
+        kw["n"] = n
+    if seed is not None:
+        kw["seed"] = seed
+    return fn(**kw)

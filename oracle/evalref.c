@@ -40,6 +40,10 @@ typedef struct {
     const uint32_t* key_leaf;   /* [entries] leaf index of chunk 0 of key  */
     const uint32_t* val_leaf;   /* [entries]                               */
     uint32_t else_leaf;
+    /* constant-keyed entries, matched first (ir.scan_const_keys) */
+    uint32_t n_ckeys;
+    const uint32_t* ckey;       /* [n_ckeys] const index of the key        */
+    const uint32_t* cval_leaf;  /* [n_ckeys] leaf index of chunk 0 of value */
 } table_t;
 
 static void vzero(V* a) { memset(a, 0, sizeof *a); }
@@ -301,6 +305,14 @@ static void leaf_value(const V* leaves, uint32_t idx, uint32_t width, V* out) {
 
 static void table_lookup(const dag_t* g, const V* leaves, uint32_t t, const V* key, V* out) {
     const table_t* T = &g->tables[t];
+    for (uint32_t e = 0; e < T->n_ckeys; ++e) {
+        V k;
+        memcpy(k.w, g->consts + (size_t)T->ckey[e] * L, sizeof k.w);
+        if (vcmp(&k, key) == 0) {
+            leaf_value(leaves, T->cval_leaf[e], T->val_w, out);
+            return;
+        }
+    }
     for (uint32_t e = 0; e < T->entries; ++e) {
         V k;
         leaf_value(leaves, T->key_leaf[e], T->key_w, &k);
@@ -478,6 +490,7 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
 typedef struct {
     uint32_t key_w, val_w, entries, else_leaf;
     uint32_t key_leaf_off, val_leaf_off;   /* offsets into a shared u32 array */
+    uint32_t n_ckeys, ckey_off, cval_leaf_off;
 } table_desc;
 
 static void make_tables(const table_desc* td, uint32_t n, const uint32_t* leafidx, table_t* out) {
@@ -488,6 +501,9 @@ static void make_tables(const table_desc* td, uint32_t n, const uint32_t* leafid
         out[t].key_leaf = leafidx + td[t].key_leaf_off;
         out[t].val_leaf = leafidx + td[t].val_leaf_off;
         out[t].else_leaf = td[t].else_leaf;
+        out[t].n_ckeys = td[t].n_ckeys;
+        out[t].ckey = leafidx + td[t].ckey_off;
+        out[t].cval_leaf = leafidx + td[t].cval_leaf_off;
     }
 }
 

@@ -34,7 +34,8 @@ _CMP = {"bvult": ("ULT", 0), "bvule": ("ULE", 0), "bvugt": ("ULT", 1), "bvuge": 
 class TableDesc(C.Structure):
     _fields_ = [("key_w", C.c_uint32), ("val_w", C.c_uint32), ("entries", C.c_uint32),
                 ("else_leaf", C.c_uint32), ("key_leaf_off", C.c_uint32),
-                ("val_leaf_off", C.c_uint32)]
+                ("val_leaf_off", C.c_uint32), ("n_ckeys", C.c_uint32),
+                ("ckey_off", C.c_uint32), ("cval_leaf_off", C.c_uint32)]
 
 
 class Serialized:
@@ -70,8 +71,18 @@ def serialize(constraints: Sequence[Node], program, probes: Sequence[Node] = ())
             S.leafidx += [li["%s#k%d#0" % (name, e)] for e in range(n)]
             voff = len(S.leafidx)
             S.leafidx += [li["%s#v%d#0" % (name, e)] for e in range(n)]
+            # constant-keyed entries first (ir.scan_const_keys): key constant
+            # indices, then their value leaves (a value leaf a query never
+            # reads is absent from the program: index it as leaf 0, which the
+            # lookup below then never reaches for a different key)
+            ck = program.table_ckeys.get(name, [])
+            ckoff = len(S.leafidx)
+            S.leafidx += [const(c) for c in ck]
+            cvoff = len(S.leafidx)
+            S.leafidx += [li.get("%s#c%d#0" % (name, i), 0) for i in range(len(ck))]
             table_ix[name] = len(S.tables)
-            S.tables.append(TableDesc(key_w, val_w, n, li["%s#else#0" % name], koff, voff))
+            S.tables.append(TableDesc(key_w, val_w, n, li.get("%s#else#0" % name, 0), koff, voff,
+                                      len(ck), ckoff, cvoff))
         return table_ix[name]
 
     ix = S.node_index

@@ -1,0 +1,190 @@
+"""CPU checks of the C1 / C3 / C4 stand-in query builders
+(mythril_amd/workloads.py): host Keccak against the oracle, planted models
+that satisfy the paths the builders claim are feasible (pinning the lowering
+against the reference's semantics through the oracle), and the compiled IR
+(both table modes) against the oracle on every workload shape."""
+
+import random
+
+import numpy as np
+import pytest
+
+import ir_sim
+from mythril_amd import workloads as W
+from mythril_amd.assign import leaf_values, unpack
+from mythril_amd.ir import compile_constraints
+from oracle import gen_ref
+from oracle import smtlib_ref as R
+from oracle.keccak_ref import keccak256 as ref_keccak
+from test_oracle_golden import load
+
+ATTACKER, SOMEGUY, CREATOR = W.ACTORS[1], W.ACTORS[2], W.ACTORS[0]
+
+
+def test_host_keccak_matches_oracle():
+    for k in load("keccak_kat.json"):
+        assert W.keccak256(bytes.fromhex(k["msg_hex"])).hex() == k["digest"][2:]
+    rng = random.Random(4)
+    for n in list(range(0, 70)) + [135, 136, 137, 300]:
+        m = bytes(rng.randrange(256) for _ in range(n))
+        assert W.keccak256(m) == ref_keccak(m)
+    assert W.selector("transfer(address,uint256)") == 0xA9059CBB
+
+
+def _calldata(sel, words):
+    data = sel.to_bytes(4, "big") + b"".join(w.to_bytes(32, "big") for w in words)
+    return [(i, b) for i, b in enumerate(data) if b], len(data)
+
+
+def test_c1_kill_zero_path_is_satisfied_by_planted_model():
+    w = W.World()
+    t = w.tx()
+    t.dispatch(W.SUICIDE_FUNCS, 0)
+    t.jumpi(t.arg_address(0) == W.bv(0), taken=True)
+    q = w.query()
+    ents, size = _calldata(W.SUICIDE_FUNCS[0], [0])
+    asg = R.Assignment(vars={"sender_0": ATTACKER, "call_value0": 0, "0_calldatasize": size},
+                       arrays={"0_calldata": (ents, 0), "balance": ([], 0)})
+    assert R.eval_constraints(q, asg) == 1
+    bad = R.Assignment(vars=dict(asg.vars),
+                       arrays={"0_calldata": (ents + [(35, 1)], 0), "balance": ([], 0)})
+    assert R.eval_constraints(q, bad) == 0
+    # short calldata: the selector bytes past the size read as 0
+    short = R.Assignment(vars=dict(asg.vars, **{"0_calldatasize": 3}), arrays=asg.arrays)
+    assert R.eval_constraints(q, short) == 0
+    # a caller outside the three actors violates the setup constraint
+    stranger = R.Assignment(vars=dict(asg.vars, sender_0=5), arrays=asg.arrays)
+    assert R.eval_constraints(q, stranger) == 0
+
+
+def test_c4_token_underflow_is_satisfied_by_planted_model():
+    """token.sol transfer from an account holding nothing: the SUB underflow
+    check (integer.py:157) is satisfiable once the keccak UF pair maps the
+    sender's and receiver's mapping slots into the 512-bit interval."""
+    w = W.World()
+    c = w.tx(creation=True)
+    supply = c.arg(0)
+    c.sstore(W.bv(1), supply)
+    c.sstore(c.mapping(W.bv(CREATOR), 0), supply)
+    t = w.tx()
+    checks = []
+    W._token_transfer(t, checks)
+    q = w.query([checks[0]])
+    lo = w.kfm.interval_hook_for_size[512] * W.PART
+    h_a = (lo + 63) // 64 * 64 + 64
+    h_t = h_a + 64
+    k_c, k_a, k_t = CREATOR << 256, ATTACKER << 256, SOMEGUY << 256
+    h_c = int.from_bytes(W.keccak256(k_c.to_bytes(64, "big")), "big")
+    ents, size = _calldata(W.TOKEN_FUNCS[W.TOKEN_FUNCS.index(W.selector("transfer(address,uint256)"))],
+                           [SOMEGUY, 1])
+    vars_ = {"sender_1": ATTACKER, "call_value1": 0, "1_calldatasize": size, "call_value0": 0,
+             "0_calldatasize": 36}
+    arrays = {"1_calldata": (ents, 0), "0_calldata": ([(35, 7)], 0), "balance": ([], 0)}
+    funcs = {"keccak256_512": ([(k_c, h_c), (k_a, h_a), (k_t, h_t)], 0),
+             "keccak256_512-1": ([(h_c, k_c), (h_a, k_a), (h_t, k_t)], 0)}
+    asg = R.Assignment(vars=vars_, arrays=arrays, funcs=funcs)
+    assert R.eval_constraints(q, asg) == 1
+    # the underflow check itself is what the model satisfies: value 0 fails it
+    ents0, _ = _calldata(W.TOKEN_FUNCS[W.TOKEN_FUNCS.index(W.selector("transfer(address,uint256)"))],
+                         [SOMEGUY, 0])
+    zero = R.Assignment(vars=vars_, arrays=dict(arrays, **{"1_calldata": (ents0, 0)}), funcs=funcs)
+    assert R.eval_constraints(q, zero) == 0
+    # a slot hash outside the 512-bit interval violates the keccak condition
+    off = R.Assignment(vars=vars_, arrays=arrays,
+                       funcs={"keccak256_512": ([(k_c, h_c), (k_a, h_a + 1), (k_t, h_t)], 0),
+                              "keccak256_512-1": ([(h_c, k_c), (h_a + 1, k_a), (h_t, k_t)], 0)})
+    assert R.eval_constraints(q, off) == 0
+
+
+@pytest.mark.parametrize("name", ["c1", "c3", "c4"])
+def test_workload_shapes(name):
+    qs = W.queries(name, 48)
+    assert len(qs) == 48
+    ops = set()
+    from mythril_amd.smt.node import topo_order
+    for q in qs:
+        for n in topo_order(q):
+            ops.add(n.op)
+    assert {"select", "ite", "concat", "bvslt", "bvult", "="} <= ops
+    if name == "c3":
+        assert {"bvumul_noovfl", "apply", "store", "K"} <= ops
+    if name == "c4":
+        assert {"apply", "store", "bvurem"} <= ops
+    # deterministic
+    assert [len(q) for q in W.queries(name, 48)] == [len(q) for q in qs]
+
+
+def _to_oracle(prog, lv):
+    arr = np.zeros((len(prog.leaves), 8), dtype=np.uint32)
+    for i, v in enumerate(lv):
+        for j in range(8):
+            arr[i, j] = (v >> (32 * j)) & 0xFFFFFFFF
+    a = unpack(prog, arr)
+    return R.Assignment(a.vars, a.arrays, a.funcs)
+
+
+@pytest.mark.parametrize("name,const_keys", [("c1", False), ("c1", True), ("c3", False),
+                                             ("c3", True), ("c4", False), ("c4", True)])
+def test_workload_programs_through_ir(name, const_keys):
+    """Compiled IR (leaf-keyed or constant-keyed tables) executed by the
+    reference executor equals direct oracle evaluation of the source DAG
+    under generator candidates, pools included."""
+    qs = W.queries(name, 40)[::5]
+    for qi, q in enumerate(qs):
+        prog = compile_constraints(q, const_keys=const_keys, leaf_pools=const_keys)
+        table = [sum(int(prog.consts[i, j]) << (32 * j) for j in range(8))
+                 for i in range(prog.consts.shape[0])]
+        for idx in range(6):
+            lv = []
+            for li, l in enumerate(prog.leaves):
+                off, n = prog.pool_ranges[li] if prog.pool_ranges else (0, len(prog.const_values))
+                lv.append(gen_ref.gen_leaf(0xABC, qi, li, idx, l.width, table[off:off + n],
+                                           pct=(20, 40, 60)))
+            asg = _to_oracle(prog, lv)
+            root, _ = ir_sim.run(prog, lv)
+            assert root == R.eval_constraints(q, asg), (name, qi, idx)
+            # the model packs back to leaves that evaluate the same (a
+            # leaf-keyed entry at a constant key is shadowed, so it may move)
+            back = leaf_values(prog, unpack(prog, _pack1(lv)))
+            assert ir_sim.run(prog, back)[0] == root
+
+
+def _pack1(lv):
+    arr = np.zeros((len(lv), 8), dtype=np.uint32)
+    for i, v in enumerate(lv):
+        for j in range(8):
+            arr[i, j] = (v >> (32 * j)) & 0xFFFFFFFF
+    return arr
+
+
+def test_const_keys_fold_constant_reads_to_leaves():
+    from mythril_amd.smt import node as N
+    cd = N.array_var("cd", 256, 8)
+    x = N.bv_var("x", 256)
+    q = [N.eq(N.select(cd, N.bv_num(3, 256)), N.bv_num(0x2A, 8)),
+         N.eq(N.select(cd, x), N.bv_num(7, 8))]
+    prog = compile_constraints(q, const_keys=True)
+    assert prog.table_ckeys == {"cd": [3]}
+    kinds = sorted(l.kind for l in prog.leaves)
+    assert kinds.count("cval") == 1
+    # model: cd[3] = 0x2A, x = 3 reads the same entry -> second constraint false
+    lv_ok = {"cd#c0#0": 0x2A, "x": 9, "cd#k0#0": 9, "cd#v0#0": 7}
+    lv = [lv_ok.get(l.name, 0) for l in prog.leaves]
+    root, _ = ir_sim.run(prog, lv)
+    assert root == 1 and R.eval_constraints(q, _to_oracle(prog, lv)) == 1
+    lv_bad = dict(lv_ok, x=3)
+    lv = [lv_bad.get(l.name, 0) for l in prog.leaves]
+    root, _ = ir_sim.run(prog, lv)
+    assert root == 0 and R.eval_constraints(q, _to_oracle(prog, lv)) == 0
+
+
+def test_const_keys_skip_tables_read_at_many_symbolic_offsets():
+    from mythril_amd.ir import scan_const_keys
+    from mythril_amd.smt import node as N
+    cd = N.array_var("cd", 256, 8)
+    reads = [N.select(cd, N.bv_num(i, 256)) for i in range(40)]
+    reads += [N.select(cd, N.bv_op("bvadd", N.bv_var("o", 256), N.bv_num(i, 256)))
+              for i in range(60)]
+    q = [N.eq(N.concat(*reads), N.bv_num(0, 800))]
+    assert scan_const_keys(q) == {}
+    assert scan_const_keys(q, max_links=10 ** 6)["cd"] == list(range(40))
