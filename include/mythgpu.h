@@ -90,7 +90,9 @@ int mg_eval_gen(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_
 
 /* Witness search: smallest candidate index in [gen->first_index,
  * gen->first_index + n_cand) whose assignment satisfies every ROOT, or -1.
- * witness_leaves ([n_leaves][8], may be NULL) receives its leaf values. */
+ * witness_leaves ([n_leaves][8], may be NULL) receives its leaf values.  The
+ * whole range is queued on the device at once (no host round trip per
+ * chunk); waves beyond the first witness found so far exit immediately. */
 int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_cand,
               int64_t* first_sat, uint32_t* witness_leaves);
 
@@ -109,11 +111,13 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* batch, uint64_t seed, uint64_t firs
  * get_model loop at mythril/laser/ethereum/svm.py:201-203 and :257-262):
  * for every program of the batch, the smallest candidate index in
  * [gen->first_index, gen->first_index + n_cand) that satisfies it, or -1, in
- * first_sat[n_progs].  All programs share each launch; programs already
- * solved stop consuming lanes.  Witness leaves: mg_search with n_cand = 1 at
- * the returned index. */
+ * first_sat[n_progs].  All programs share each launch; waves of programs
+ * already solved stop consuming lanes, with no host round trip.
+ * witness_leaves (may be NULL): [n_progs][max_leaves][8] u32, the leaf values
+ * of each solved program's witness (one regeneration launch for all);
+ * max_leaves must be >= the batch's largest leaf count. */
 int mg_batch_search(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_cand,
-                    int64_t* first_sat);
+                    int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves);
 
 /* Keccak-256 (0x01 padding) of n messages, one GPU lane per message.
  *   data/offsets/lens describe the messages in one host byte buffer;

@@ -3,7 +3,7 @@
  * (mythril_amd/ir.py) emits for one get_model constraint set.  The library
  * validates it and translates it into the records of the gfx950 assembly
  * interpreter (mythril_amd/asmgen.py, mg_interp_asm.hip), which executes it
- * per lane (mg_kernels.hip holds the first C++ interpreter, kept for A/B).
+ * per lane.
  *
  * One lane evaluates one candidate assignment.  Values are bit-vectors of
  * width 1..256 held as 8 little-endian 32-bit limbs, always canonical (bits

@@ -9,14 +9,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "mythril_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "mythril_amd", "lib")
 LIB = os.path.join(LIBDIR, "libmythgpu.so")
-SOURCES = ["mg_interp_asm.hip", "mg_kernels.hip", "mg_keccak.hip", "mg_api.cpp"]
+SOURCES = ["mg_interp_asm.hip", "mg_keccak.hip", "mg_host.cpp", "mg_api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
 
 
 def _deps():
     files = [os.path.join(CSRC, s) for s in SOURCES]
-    files += [os.path.join(CSRC, "mg_device.h"), os.path.join(ROOT, "include", "mythgpu.h"),
+    files += [os.path.join(CSRC, "mg_device.h"), os.path.join(CSRC, "mg_host.h"),
+              os.path.join(ROOT, "include", "mythgpu.h"),
               os.path.join(ROOT, "include", "mythgpu_ir.h"),
               os.path.join(ROOT, "mythril_amd", "asmgen.py")]
     return files

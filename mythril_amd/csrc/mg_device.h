@@ -1,4 +1,4 @@
-/* Structures shared by the HIP kernels (mg_kernels.hip) and the C-ABI host
+/* Structures shared by the HIP kernels (mg_interp_asm.hip) and the C-ABI host
  * layer (mg_api.cpp).  Device-resident; never crosses the C ABI. */
 #ifndef MG_DEVICE_H
 #define MG_DEVICE_H
@@ -45,9 +45,15 @@ struct mg_run {
     uint32_t* leaves_out;      /* generator mode: dump generated leaves    */
     uint64_t seed;             /* generator seed                           */
     uint64_t first_index;      /* candidate index of lane 0                */
-    uint32_t skip_solved;      /* search: blocks of programs whose first_sat
-                                  is below first_index (solved by an earlier
-                                  chunk) return at once                    */
+    uint32_t skip_solved;      /* search: a wave whose first candidate index
+                                  is at or beyond its program's first_sat
+                                  (read with a memory-side atomic, so hits
+                                  of other XCDs in the same launch count)
+                                  returns at once                          */
+    const uint64_t* first_per_prog; /* witness regeneration: program p's
+                                  candidate index (first_index ignored);
+                                  ~0 = unsolved, the program returns      */
+    uint64_t lout_prog_words;  /* leaves_out stride between programs       */
 };
 
 #endif

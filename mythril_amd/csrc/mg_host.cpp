@@ -1,0 +1,404 @@
+// Host-only half of libmythgpu: program validation and the IR -> record
+// translation of the assembly interpreter.  No HIP runtime calls, so this
+// file also builds with plain g++ under ASan/UBSan (tests/test_host_sanitize.py
+// fuzzes it with malformed programs): it is the safety boundary that keeps a
+// kernel from indexing outside the register file, the spill area, the
+// constant pool, the leaf table or the probe buffer.
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mg_host.h"
+
+static int fail(std::string* err, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (err) *err = buf;
+    return code;
+}
+
+// ---- IR -> assembly-interpreter records (8 words each) ----------------------
+//
+// w0 handler byte offset | w1 8*dst | w2 8*a | w3 8*b | w4 8*c / funnel index /
+// leaf or probe index | w5 immediate (const / spill byte offset, funnel shift,
+// source width) | w6 width | w7 byte offset of an 8- (SEXT: 16-) word mask
+// entry appended to the constant table.  The record after a heavy op lives in
+// bank A, otherwise banks alternate (asmgen.py: prefetch into the other bank).
+
+
+static std::vector<uint32_t> mask_lt(uint32_t w) {     // bits < w
+    std::vector<uint32_t> m(8);
+    for (uint32_t j = 0; j < 8; ++j)
+        m[j] = j < w / 32 ? 0xFFFFFFFFu : (j == w / 32 ? ((1u << (w % 32)) - 1u) : 0u);
+    return m;
+}
+
+static std::vector<uint32_t> mask_ge(uint32_t w) {     // bits >= w
+    std::vector<uint32_t> m = mask_lt(w);
+    for (auto& x : m) x = ~x;
+    return m;
+}
+
+static bool is_compare(uint32_t op) {
+    return op == MG_EQ || op == MG_ULT || op == MG_ULE || op == MG_SLT || op == MG_SLE ||
+           op == MG_UMULNO;
+}
+
+// ops with a one-limb (W32) handler when operands and result fit 32 bits
+static bool has_w32(uint32_t op) {
+    switch (op) {
+    case MG_ADD: case MG_SUB: case MG_AND: case MG_OR: case MG_XOR: case MG_NOT: case MG_NEG:
+    case MG_ITE: case MG_EQ: case MG_ULT: case MG_ULE: case MG_EXTRACT: case MG_MOV:
+    case MG_CONST:
+        return true;
+    default:
+        return false;
+    }
+}
+
+// register slots an IR instruction reads or writes (bit mask)
+static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
+    switch (op) {
+    case MG_NOP: return 0;
+    case MG_CONST: case MG_LEAF: case MG_RELOAD: return 1u << d;
+    case MG_SPILL: case MG_OUT: case MG_ROOT: return 1u << a;
+    case MG_NOT: case MG_NEG: case MG_MOV: case MG_SEXT:
+        return (1u << d) | (1u << a);
+    // the funnel shifts read one slot beyond their operand (masked off, but
+    // the registers are read): the next slot for EXTRACT, the previous one
+    // for CONCAT's high part
+    case MG_EXTRACT: return ((1u << d) | (3u << a)) & ((1u << MG_NREG) - 1);
+    case MG_CONCAT: return (1u << d) | (1u << a) | (a ? 1u << (a - 1) : 0u) | (1u << b);
+    case MG_ITE: return (1u << d) | (1u << a) | (1u << b) | (1u << c);
+    default: return (1u << d) | (1u << a) | (1u << b);
+    }
+}
+
+// slots an instruction reads (its destination only when it is also an operand)
+static uint32_t slots_read(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t m = slots_touched(op, d, a, b, c);
+    switch (op) {
+    case MG_NOP: case MG_CONST: case MG_LEAF: case MG_RELOAD: return 0;
+    case MG_SPILL: case MG_OUT: case MG_ROOT: return m;
+    default: break;
+    }
+    const bool d_operand = d == a || (op != MG_NOT && op != MG_NEG && op != MG_MOV &&
+                                      op != MG_EXTRACT && op != MG_SEXT && d == b) ||
+                           (op == MG_ITE && d == c) || (op == MG_EXTRACT && d == a + 1) ||
+                           (op == MG_CONCAT && a && d == a - 1);
+    return d_operand ? m : m & ~(1u << d);
+}
+
+void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
+                      uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
+    pool.base = n_consts;
+    const uint32_t ones = pool.add(mask_lt(256));
+    rec.clear();
+    rec.reserve((size_t)(n_ins + 4) * 8);
+    // clean[s]: limbs 1..7 of slot s are known to be zero (its last value had
+    // at most 32 bits); registers start uninitialised
+    bool clean[MG_NREG];
+    for (int k = 0; k < MG_NREG; ++k) clean[k] = false;
+    // slots whose LEAFD loads may still be in flight: a WAITVM record goes
+    // before the first instruction that reads or writes one of them
+    uint32_t pending = 0;
+    int bank = 0;
+    auto emit = [&rec]() {
+        rec.resize(rec.size() + 8, 0);
+        return rec.data() + rec.size() - 8;
+    };
+    // the last record emitted, when it is a LEAFD / RELOADD: a wait right
+    // after it folds into that record (word W = 1, the handler waits)
+    size_t last_ld = SIZE_MAX;
+    auto wait_vm = [&]() {
+        if (last_ld != SIZE_MAX && last_ld + 8 == rec.size()) {
+            rec[last_ld + 6] = 1;           // the LEAFD / RELOADD waits itself
+        } else {
+            emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
+            bank = 1 - bank;
+        }
+        pending = 0;
+    };
+    // Issue order: every scratch RELOAD and 256-bit LEAF moves up (at most 24
+    // places) past the instructions that leave its destination slot (and spill
+    // slot) alone, so its loads are in flight early (RELOADD / LEAFD) and
+    // waited for only at the first instruction that touches the slot.
+    std::vector<uint32_t> order(n_ins);
+    for (uint32_t i = 0; i < n_ins; ++i) order[i] = i;
+    for (uint32_t q = 0; q < n_ins; ++q) {
+        const uint32_t* in = code + 4 * order[q];
+        const bool leafd = (in[0] & 0xFF) == MG_LEAF && ((in[0] >> 8) & 0x3FF) == 256;
+        if (!leafd && ((in[0] & 0xFF) != MG_RELOAD || in[2] < n_lds)) continue;
+        const uint32_t rd = in[1] & 0xFF, slot = leafd ? 0xFFFFFFFFu : in[2];
+        uint32_t t = q;
+        while (t > 0 && q - t < 24) {
+            const uint32_t* p = code + 4 * order[t - 1];
+            const uint32_t pop = p[0] & 0xFF;
+            if (slots_touched(pop, p[1] & 0xFF, (p[1] >> 8) & 0xFF, (p[1] >> 16) & 0xFF,
+                              (p[1] >> 24) & 0xFF) & (1u << rd))
+                break;
+            if (pop == MG_SPILL && p[2] == slot) break;
+            --t;
+        }
+        if (t < q) {
+            const uint32_t moved = order[q];
+            for (uint32_t k = q; k > t; --k) order[k] = order[k - 1];
+            order[t] = moved;
+        }
+    }
+    for (uint32_t pc = 0; pc <= n_ins; ++pc) {
+        if (pc == n_ins) {          // HALT, then one zeroed record (prefetch pad)
+            if (pending) wait_vm();
+            emit()[0] = hoff[MGA_HID(MGA_HALT, 0, bank)];
+            emit();
+            break;
+        }
+        const uint32_t* in = code + 4 * order[pc];
+        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
+        const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
+                       c = (in[1] >> 24) & 0xFF;
+        // a store-chain link: t = (a == b) of wide values, consumed only by
+        // the next instruction, an ITE on t -> one EQSEL record
+        if (op == MG_EQ && w > 32 && !(in[0] & MG_ROOT_FLAG) && pc + 1 < n_ins) {
+            const uint32_t* nx = code + 4 * order[pc + 1];
+            const uint32_t nd = nx[1] & 0xFF, na = (nx[1] >> 8) & 0xFF, nb = (nx[1] >> 16) & 0xFF,
+                           nc = (nx[1] >> 24) & 0xFF;
+            bool fuse = (nx[0] & 0xFF) == MG_ITE && !(nx[0] & MG_ROOT_FLAG) && nc == d &&
+                        na != d && nb != d;
+            for (uint32_t q = pc + 2; fuse && q < n_ins; ++q) {     // is t dead after the ITE?
+                const uint32_t* f = code + 4 * order[q];
+                const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
+                               fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
+                if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) fuse = false;
+                else if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
+            }
+            if (fuse) {
+                const uint32_t touch = slots_touched(op, d, a, b, c) | slots_touched(MG_ITE, nd, na, nb, nc);
+                if (pending & touch) wait_vm();
+                uint32_t* r = emit();
+                uint32_t var;
+                r[1] = 8 * nd; r[2] = 8 * a; r[3] = 8 * b;
+                if (nd == na) { var = MGA_V_NEG; r[4] = 8 * nb; }          // keep F[d] where equal
+                else if (nd == nb) { var = 0; r[4] = 8 * na; }             // take F[a] where equal
+                else { var = MGA_V_GEN; r[4] = 8 * na; r[5] = 8 * nb; }
+                r[0] = hoff[MGA_HID(MGA_EQSEL, var, bank)];
+                bank = 1 - bank;
+                clean[nd] = ((nx[0] >> 8) & 0x3FF) <= 32;     // canonical values
+                ++pc;
+                continue;
+            }
+        }
+        const bool leafd = op == MG_LEAF && w == 256;
+        const bool reloadd = op == MG_RELOAD && imm >= n_lds;
+        if (pending && (slots_touched(op, d, a, b, c) & pending)) wait_vm();
+        if (leafd || reloadd) pending |= 1u << d;
+        uint32_t* r = emit();
+        uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
+        const bool writes = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
+        // result fits one limb: Bool results, or values of at most 32 bits
+        const bool narrow = is_compare(op) || (writes && w <= 32);
+        const bool w32 = has_w32(op) && w <= 32;       // compares: w = operand width
+        if (w32) var |= MGA_V_W32;
+        if (writes && narrow && clean[d]) var |= MGA_V_DC;
+        const uint32_t maskv = w32 ? (w < 32 ? MGA_V_MASK : 0) : ((w >= 1 && w < 256) ? MGA_V_MASK : 0);
+        r[1] = 8 * d; r[2] = 8 * a; r[3] = 8 * b; r[4] = 8 * c; r[5] = 0; r[6] = w; r[7] = ones;
+        int aop = MGA_NOP;
+        switch (op) {
+        case MG_NOP: aop = MGA_NOP; break;
+        case MG_CONST: aop = MGA_CONST; r[5] = imm * 32u; break;
+        case MG_LEAF:
+            aop = MGA_LEAF; r[4] = imm;
+            if (leafd) { aop = MGA_LEAFD; var = d; }
+            else if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
+            break;
+        case MG_SPILL:              // spills and reloads: the variant is the slot
+            if (imm < n_lds) { aop = MGA_SPILL_LDS; var = a; r[5] = imm * 2u * 256u * 16u; }
+            else { aop = MGA_SPILL_SCR; var = a; r[5] = (imm - n_lds) * 32u; }
+            break;
+        case MG_RELOAD:
+            if (imm < n_lds) { aop = MGA_RELOAD_LDS; var = d; r[5] = imm * 2u * 256u * 16u; }
+            else { aop = MGA_RELOADD; var = d; r[5] = (imm - n_lds) * 32u; }
+            break;
+        case MG_ADD: aop = MGA_ADD; goto masked;
+        case MG_SUB: aop = MGA_SUB; goto masked;
+        case MG_MUL: aop = MGA_MUL; goto masked;
+        case MG_NEG: aop = MGA_NEG; goto masked;
+        case MG_NOT: aop = MGA_NOT; goto masked;
+        case MG_UDIV: aop = MGA_UDIV; goto masked;
+        case MG_UREM: aop = MGA_UREM; goto masked;
+        case MG_SDIV: aop = MGA_SDIV; goto masked;
+        case MG_SREM: aop = MGA_SREM; goto masked;
+        case MG_SMOD: aop = MGA_SMOD; goto masked;
+        case MG_SHL: aop = MGA_SHL; goto masked;
+        case MG_LSHR: aop = MGA_LSHR; goto masked;
+        case MG_ASHR: aop = MGA_ASHR; goto masked;
+        case MG_SLT: aop = MGA_SLT; goto masked;
+        case MG_SLE: aop = MGA_SLE; goto masked;
+        case MG_UMULNO: aop = MGA_UMULNO;
+        masked:
+            if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
+            break;
+        case MG_AND: aop = MGA_AND; break;
+        case MG_OR: aop = MGA_OR; break;
+        case MG_XOR: aop = MGA_XOR; break;
+        case MG_EQ: aop = MGA_EQ; break;
+        case MG_ULT: aop = MGA_ULT; break;
+        case MG_ULE: aop = MGA_ULE; break;
+        case MG_ITE: aop = MGA_ITE; break;
+        case MG_CONCAT: {           // R = a << imm | b: static limb shift in the variant
+            aop = MGA_CONCATQ;
+            const uint32_t q = imm >> 5, bs = imm & 31;
+            var = q | (bs ? 8u : 0u);
+            r[4] = 8 * a + 8 - q - (bs ? 1 : 0);
+            r[5] = bs ? 32 - bs : 0;
+            r[7] = ~((1u << bs) - 1u);              // limb q: bits >= bs from a
+            break;
+        }
+        case MG_EXTRACT:            // R = (a >> imm) & mask(w)
+            r[4] = 8 * a + (imm >> 5) + 8;
+            r[5] = imm & 31;
+            if (w > 32) {           // static result limbs; top-limb mask inline
+                aop = MGA_EXTRACTN;
+                var = (w + 31) / 32 - 1;
+                r[7] = (w & 31) ? (1u << (w & 31)) - 1u : 0xFFFFFFFFu;
+            } else {
+                aop = MGA_EXTRACT;
+                r[7] = pool.add(mask_lt(w));
+            }
+            break;
+        case MG_SEXT: {             // from imm bits to w bits: 16-word mask entry
+            aop = MGA_SEXT;
+            r[5] = imm;
+            std::vector<uint32_t> m = mask_lt(imm), m2 = mask_lt(w);
+            m.insert(m.end(), m2.begin(), m2.end());
+            r[7] = pool.add(m);
+            break;
+        }
+        case MG_OUT: aop = MGA_OUT; r[4] = imm; break;
+        case MG_ROOT: aop = MGA_ROOT; break;
+        case MG_MOV: aop = MGA_MOV; break;
+        default: aop = MGA_NOP; break;
+        }
+        // in place: the destination is operand a's slot (swap operands of
+        // commutative ops, use the reversed forms SUBR / ITEN otherwise)
+        if (!(var & MGA_V_W32)) {
+            const bool comm = op == MG_ADD || op == MG_AND || op == MG_OR || op == MG_XOR;
+            if ((comm || op == MG_SUB || op == MG_ITE) && d == b && d != a) {
+                const uint32_t t = r[2]; r[2] = r[3]; r[3] = t;
+                if (op == MG_SUB) aop = MGA_SUBR;
+                if (op == MG_ITE) aop = MGA_ITEN;
+                var |= MGA_V_IP;
+            } else if ((comm || op == MG_SUB || op == MG_ITE || op == MG_NOT || op == MG_NEG) &&
+                       d == a) {
+                var |= MGA_V_IP;
+            }
+        }
+        r[0] = hoff[MGA_HID(aop, var, bank)];
+        if (aop == MGA_LEAFD || aop == MGA_RELOADD) {
+            r[6] = 0;
+            last_ld = (size_t)(r - rec.data());
+        }
+        if (writes) clean[d] = narrow;
+        bank = mga_is_heavy(aop) ? 0 : 1 - bank;
+    }
+}
+
+int mg_validate(std::string* err, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
+                    const mg_leafgen* leaves, uint32_t n_leaves, uint32_t n_lds,
+                    uint32_t n_spill, uint32_t n_probes) {
+    if (n_lds > MG_MAX_LDS) return fail(err, MG_E_ARG, "too many LDS slots (%u)", n_lds);
+    if (n_spill < n_lds || n_spill - n_lds > MG_MAX_PSLOTS)
+        return fail(err, MG_E_ARG, "spill slots %u (LDS %u)", n_spill, n_lds);
+    for (uint32_t i = 0; leaves && i < n_leaves; ++i) {
+        const mg_leafgen& g = leaves[i];
+        if (g.width < 1 || g.width > MG_MAX_WIDTH)
+            return fail(err, MG_E_ARG, "leaf %u: width %u", i, g.width);
+        if ((uint64_t)g.pool_off + g.pool_n > n_consts)
+            return fail(err, MG_E_ARG, "leaf %u: pool outside const table", i);
+        if (!(g.pct_uniform <= g.pct_small && g.pct_small <= g.pct_boundary &&
+              g.pct_boundary <= 100))
+            return fail(err, MG_E_ARG, "leaf %u: class thresholds", i);
+    }
+    for (uint32_t pc = 0; pc < n_ins; ++pc) {
+        const uint32_t* in = code + 4 * pc;
+        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm0 = in[2];
+        if (op >= MG_NUM_OPS) return fail(err, MG_E_ARG, "ins %u: bad opcode %u", pc, op);
+        if ((in[0] & ~(0x3FFFFu | MG_ROOT_FLAG)) != 0)
+            return fail(err, MG_E_ARG, "ins %u: reserved bits set", pc);
+        for (int k = 0; k < 4; ++k)
+            if (((in[1] >> (8 * k)) & 0xFF) >= MG_NREG)
+                return fail(err, MG_E_ARG, "ins %u: slot out of range", pc);
+        const bool needs_w = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
+        if (needs_w && (w < 1 || w > MG_MAX_WIDTH))
+            return fail(err, MG_E_ARG, "ins %u: width %u", pc, w);
+        switch (op) {
+        case MG_CONST:
+            if (imm0 >= n_consts) return fail(err, MG_E_ARG, "ins %u: const %u", pc, imm0);
+            break;
+        case MG_LEAF:
+            if (imm0 >= n_leaves) return fail(err, MG_E_ARG, "ins %u: leaf %u", pc, imm0);
+            break;
+        case MG_SPILL:
+        case MG_RELOAD:
+            if (imm0 >= n_spill) return fail(err, MG_E_ARG, "ins %u: spill slot %u", pc, imm0);
+            break;
+        case MG_OUT:
+            if (imm0 >= n_probes) return fail(err, MG_E_ARG, "ins %u: probe %u", pc, imm0);
+            break;
+        case MG_CONCAT:
+            if (imm0 < 1 || imm0 >= w) return fail(err, MG_E_ARG, "ins %u: concat split", pc);
+            break;
+        case MG_EXTRACT:
+            if (imm0 + w > MG_MAX_WIDTH) return fail(err, MG_E_ARG, "ins %u: extract range", pc);
+            break;
+        case MG_SEXT:
+            if (imm0 < 1 || imm0 > w) return fail(err, MG_E_ARG, "ins %u: sext width", pc);
+            break;
+        default:
+            break;
+        }
+    }
+    return MG_OK;
+}
+
+extern "C" {
+
+int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32_t n_lds,
+                 const uint32_t* handler_off, uint32_t n_handlers, uint32_t* records,
+                 uint32_t max_record_words, uint32_t* n_record_words, uint32_t* masks,
+                 uint32_t max_mask_words, uint32_t* n_mask_words) {
+    if ((n_ins && !code) || !handler_off || n_handlers != MGA_NUM_HANDLERS || !n_record_words ||
+        !n_mask_words)
+        return MG_E_ARG;
+    // leaf and probe tables are not known here: only their indices' shape
+    int rc = mg_validate(nullptr, code, n_ins, n_consts, nullptr, 0xFFFFFFFFu, MG_MAX_LDS,
+                      MG_MAX_LDS + MG_MAX_PSLOTS, 0xFFFFFFFFu);
+    if (rc) return rc;
+    if (n_lds > MG_MAX_LDS) return MG_E_ARG;
+    std::vector<uint32_t> rec;
+    MaskPool pool;
+    mg_translate_records(handler_off, code, n_ins, n_consts, n_lds, rec, pool);
+    *n_record_words = (uint32_t)rec.size();
+    *n_mask_words = (uint32_t)pool.words.size();
+    if (rec.size() > max_record_words || pool.words.size() > max_mask_words) return MG_E_ARG;
+    if (records) memcpy(records, rec.data(), rec.size() * 4);
+    if (masks && !pool.words.empty()) memcpy(masks, pool.words.data(), pool.words.size() * 4);
+    return MG_OK;
+}
+
+int mg_config(uint32_t* out, uint32_t n) {
+    const uint32_t cfg[4] = {MG_VERSION, MG_NREG, MG_MAX_LDS, MG_MAX_PSLOTS};
+    if (!out) return MG_E_ARG;
+    for (uint32_t i = 0; i < n && i < 4; ++i) out[i] = cfg[i];
+    return MG_OK;
+}
+
+int mg_version(void) { return MG_VERSION; }
+
+}  // extern "C"

@@ -56,7 +56,10 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         if not os.path.exists(path):
             raise EngineUnavailable("libmythgpu.so not built (%s); run "
                                     "`python -m mythril_amd.build`" % path)
-        lib = C.CDLL(path)
+        try:
+            lib = C.CDLL(path)
+        except OSError as e:            # e.g. the HIP runtime it links is missing
+            raise EngineUnavailable("cannot load %s: %s" % (path, e)) from e
         p, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
         lib.mg_version.restype = C.c_int
         lib.mg_init.argtypes = [C.c_int, C.POINTER(p)]
@@ -75,7 +78,7 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_batch_free.argtypes = [p]
         lib.mg_batch_free.restype = None
         lib.mg_batch_eval_gen.argtypes = [p, p, u64, u64, u64, p, p, p]
-        lib.mg_batch_search.argtypes = [p, p, C.POINTER(Gen), u64, p]
+        lib.mg_batch_search.argtypes = [p, p, C.POINTER(Gen), u64, p, p, u32]
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
         lib.mg_config.argtypes = [p, u32]
         lib.mg_asm_digest.restype = C.c_char_p
@@ -238,26 +241,24 @@ class Engine:
     def batch_search(self, loaded: Sequence[LoadedProgram], seed: int, n_cand: int,
                      first_index: int = 0) -> List[Tuple[int, Optional[np.ndarray]]]:
         """Witness search over many programs in shared launches
-        (mg_batch_search); per program (index, leaves) or (-1, None)."""
+        (mg_batch_search, witnesses regenerated in one launch); per program
+        (index, leaves) or (-1, None)."""
         if not loaded:
             return []
         h = self.batch_create(loaded)
+        max_leaves = max(1, max(len(lp.program.leaves) for lp in loaded))
         try:
             first = np.full(len(loaded), -1, dtype=np.int64)
+            wit = np.zeros((len(loaded), max_leaves, 8), dtype=np.uint32)
             g = Gen(seed & (2**64 - 1), first_index)
-            rc = self.lib.mg_batch_search(self._ctx, h, C.byref(g), n_cand, _ptr(first))
+            rc = self.lib.mg_batch_search(self._ctx, h, C.byref(g), n_cand, _ptr(first), _ptr(wit),
+                                          max_leaves)
             self._check(rc, "mg_batch_search")
         finally:
             self.batch_free(h)
         out = []
-        for lp, f in zip(loaded, first.tolist()):
-            if f < 0:
-                out.append((-1, None))
-            else:
-                idx, wit = self.search(lp, seed, 1, first_index=f)   # regenerate the witness
-                if idx != f:
-                    raise EngineError("batch witness %d did not re-verify" % f)
-                out.append((f, wit))
+        for k, (lp, f) in enumerate(zip(loaded, first.tolist())):
+            out.append((-1, None) if f < 0 else (f, wit[k, :len(lp.program.leaves)].copy()))
         return out
 
 
@@ -278,11 +279,23 @@ def limbs_to_int(limbs) -> int:
 
 
 _engines: Dict[int, Engine] = {}
+_failed: Dict[int, str] = {}
 
 
 def get_engine(device: int = 0) -> Engine:
+    """The device's engine; an initialisation failure is remembered, so later
+    calls raise EngineUnavailable at once instead of retrying mg_init."""
     e = _engines.get(device)
     if e is None:
-        e = Engine(device)
+        if device in _failed:
+            raise EngineUnavailable(_failed[device])
+        try:
+            e = Engine(device)
+        except EngineUnavailable as x:
+            _failed[device] = str(x)
+            raise
+        except Exception as x:  # noqa: BLE001 - any init failure means no engine
+            _failed[device] = "%s: %s" % (type(x).__name__, x)
+            raise EngineUnavailable(_failed[device]) from x
         _engines[device] = e
     return e

@@ -81,33 +81,76 @@ args = Args()
 time_handler = TimeHandler()
 
 
+PHASES = ("flatten", "compile", "load", "search", "verify")
+
+
 class SolverStatistics:
-    """``SolverStatistics`` (``solver_statistics.py:29-43``) plus the
-    pre-filter's own counters."""
+    """``SolverStatistics`` (``solver_statistics.py:29-43``: query count and z3
+    time, counted while ``enabled``) plus the pre-filter's own counters and a
+    per-phase time breakdown of the GPU path (seconds).  ``install()`` makes
+    Mythril's own singleton print these lines too, where ``fire_lasers`` logs
+    it (``mythril_analyzer.py:181``)."""
 
     def __init__(self):
         self.enabled = False
         self.query_count = 0
         self.solver_time = 0.0
+        self.reset_gpu()
+
+    def reset_gpu(self):
         self.gpu_queries = 0
         self.gpu_hits = 0
         self.gpu_candidates = 0
         self.gpu_time = 0.0
+        self.kernel_time = 0.0
         self.fallbacks = 0
         self.unsupported = 0
+        self.errors = 0
+        self.rejected = 0
+        self.phase = {k: 0.0 for k in PHASES}
+
+    def gpu_report(self) -> str:
+        return ("GPU pre-filter: queries: {} hits: {} fallbacks: {} unsupported: {} errors: {} "
+                "rejected by z3: {}\nGPU candidates: {} time: {:.3f}s (kernel {:.3f}s; "
+                "{})").format(
+            self.gpu_queries, self.gpu_hits, self.fallbacks, self.unsupported, self.errors,
+            self.rejected, self.gpu_candidates, self.gpu_time, self.kernel_time,
+            ", ".join("%s %.3fs" % (k, self.phase[k]) for k in PHASES))
 
     def __repr__(self):
-        return ("Query count: {} \nSolver time: {}\nGPU queries: {} hits: {} candidates: {} "
-                "time: {:.3f}s fallbacks: {} unsupported: {}").format(
-            self.query_count, self.solver_time, self.gpu_queries, self.gpu_hits,
-            self.gpu_candidates, self.gpu_time, self.fallbacks, self.unsupported)
+        return "Query count: {} \nSolver time: {}\n{}".format(self.query_count, self.solver_time,
+                                                              self.gpu_report())
+
+
+class _Phase:
+    """``with _Phase("compile"):`` adds the block's wall time to the phase."""
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        dt = time.perf_counter() - self.t0
+        stats.phase[self.name] += dt
+        if self.name == "search":
+            stats.kernel_time += dt
+        return False
 
 
 stats = SolverStatistics()
 
-# candidate budget per query (device-generated, counter-based streams)
+# candidate budget per query (device-generated, counter-based streams) and
+# the wall-time share of the query's timeout the GPU search may use
 SEARCH_CANDIDATES = 1 << 22
 SEARCH_SEED = 0x6D797468
+SEARCH_BUDGET_MS = 200
+# conservative engine throughput (IR instructions x candidates per second)
+# used to size a search so it fits its time budget (one device launch
+# sequence cannot be interrupted)
+INS_CAND_PER_S = 3.0e11
 
 
 class Model:
@@ -125,6 +168,9 @@ class Model:
         self.table_sizes: Dict[str, int] = {}
         for p in self.programs:
             self.table_sizes.update(p.table_sizes)
+        if assignment is not None:     # constant-keyed entries count too
+            for name, (entries, _) in list(assignment.arrays.items()) + list(assignment.funcs.items()):
+                self.table_sizes[name] = max(self.table_sizes.get(name, 0), len(entries))
 
     def decls(self):
         out = []
@@ -133,11 +179,19 @@ class Model:
         return out
 
     def __getitem__(self, item):
-        for m in self.raw:
-            r = m[item]
-            if r is not None:
-                return r
-        if self.assignment is not None and isinstance(item, str):
+        """``laser/smt/model.py:27-43``: the first internal model with an
+        interpretation; an IndexError of the last model propagates.  A
+        witness-only model (no z3) answers variable names from the witness."""
+        for i, m in enumerate(self.raw):
+            try:
+                r = m[item]
+                if r is not None:
+                    return r
+            except IndexError:
+                if i == len(self.raw) - 1:
+                    raise
+                continue
+        if not self.raw and self.assignment is not None and isinstance(item, str):
             return self.assignment.vars.get(item)
         return None
 
@@ -192,7 +246,8 @@ def search_leafgen(prog: Program) -> List[LeafGen]:
 
 
 def _compile_search(nodes: Sequence[N.Node]) -> Program:
-    return compile_constraints(nodes, extra_consts=harvest_hints(nodes), leaf_pools=True)
+    return compile_constraints(nodes, extra_consts=harvest_hints(nodes), leaf_pools=True,
+                               const_keys=True)
 
 
 def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
@@ -254,41 +309,45 @@ def _merge(parts: Sequence[Assignment]) -> Assignment:
     return out
 
 
+def _n_cand(progs: Sequence[Program], budget_ms: float) -> int:
+    """Candidates that fit the time budget (power of two, <= SEARCH_CANDIDATES)."""
+    ins = max(1, sum(p.n_ins for p in progs))
+    n = int(max(budget_ms, 0.0) / 1000.0 * INS_CAND_PER_S / ins)
+    n = min(SEARCH_CANDIDATES, max(1 << 16, n))
+    return 1 << (n.bit_length() - 1)
+
+
 def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     """(assignment, programs) of a satisfying candidate, or None.  Queries
     that split into independent groups (dependence_buckets) search every
     group in one batched launch sequence and join the group witnesses, so the
-    hit probability is per group rather than their product."""
+    hit probability is per group rather than their product.  The candidate
+    count is sized to ``budget_ms``; the whole range runs on the device with
+    no host round trip (mg_search / mg_batch_search)."""
     buckets = dependence_buckets(nodes)
-    eng = get_engine()
-    if len(buckets) > 1:
+    with _Phase("compile"):
         progs = [_compile_search(b) for b in buckets]
+    eng = get_engine()
+    n_cand = _n_cand(progs, budget_ms)
+    with _Phase("load"):
         loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
-        hits = eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES)
-        stats.gpu_candidates += sum(SEARCH_CANDIDATES if i < 0 else i + 1 for i, _ in hits)
-        if any(i < 0 for i, _ in hits):
-            return None
-        return _merge([unpack(p, w) for p, (_, w) in zip(progs, hits)]), progs
-    prog = _compile_search(nodes)
-    lp = eng.load(prog, search_leafgen(prog), prog_seed=0)
-    t0 = time.perf_counter()
-    chunk = 1 << 20
-    first = 0
-    while first < SEARCH_CANDIDATES:
-        idx, wit = eng.search(lp, SEARCH_SEED, chunk, first_index=first)
-        stats.gpu_candidates += chunk if idx < 0 else idx - first + 1
-        if idx >= 0:
-            return unpack(prog, wit), [prog]
-        first += chunk
-        if (time.perf_counter() - t0) * 1000.0 > budget_ms:
-            break
-    return None
+    with _Phase("search"):
+        if len(progs) > 1:
+            hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
+        else:
+            hits = [eng.search(loaded[0], SEARCH_SEED, n_cand)]
+    stats.gpu_candidates += sum(n_cand if i < 0 else i + 1 for i, _ in hits)
+    if any(i < 0 for i, _ in hits):
+        return None
+    return _merge([unpack(p, w) for p, (_, w) in zip(progs, hits)]), progs
 
 
 # Set by install(): the reference's own Optimize wrapper
-# (mythril/laser/smt/solver/solver.py:86-105, timed by @stat_smt_query), so
-# inside Mythril the fallback is literally the stock code path.
+# (mythril/laser/smt/solver/solver.py:86-105, timed by @stat_smt_query) and
+# Model class (laser/smt/model.py), so inside Mythril the fallback is
+# literally the stock code path and a GPU answer is a stock Model.
 _stock_optimize = None
+_stock_model = None
 
 
 def _z3_check(constraints, minimize, maximize, timeout):
@@ -336,8 +395,92 @@ def _z3_check(constraints, minimize, maximize, timeout):
     raise UnsatError
 
 
+def _wrap(z3_model, assignment, progs):
+    if _stock_model is not None:
+        return _stock_model([z3_model])
+    return Model([z3_model], assignment, progs)
+
+
+def _accept(constraints, assignment, progs, deadline: float):
+    """get_model's rule for a GPU witness: re-verified by z3 (substitute +
+    simplify, then a genuine z3 model) when the constraints are z3 ASTs and
+    z3 is present; otherwise accepted as is — it was evaluated bit-exactly
+    on the device.  Returns the model, or None when z3 rejects it."""
+    if z3bridge.available():
+        raws = [getattr(c, "raw", c) for c in constraints]
+        if raws and all(not isinstance(r, N.Node) for r in raws):
+            with _Phase("verify"):
+                m = z3bridge.verify(raws, assignment, _remaining_ms(deadline))
+            if m is None:
+                stats.rejected += 1
+                log.warning("GPU witness rejected by z3; falling back")
+                return None
+            return _wrap(m, assignment, progs)
+    return Model(None, assignment, progs)
+
+
+def _remaining_ms(deadline: float) -> int:
+    return max(1, int((deadline - time.perf_counter()) * 1000.0))
+
+
+# Hand-over from batch_is_possible to get_model (bounded, oldest dropped):
+# sets whose batched search found a witness (get_model then returns it
+# without searching again) and sets it missed (get_model goes straight to z3).
+_BATCH_MEMO = 1 << 14
+_batch_witness: "Dict[tuple, tuple]" = {}
+_gpu_missed: "Dict[tuple, bool]" = {}
+
+
+def _remember(d: dict, key, value) -> None:
+    try:
+        d[key] = value
+    except TypeError:                      # unhashable constraint: nothing to hand over
+        return
+    if len(d) > _BATCH_MEMO:
+        d.pop(next(iter(d)))
+
+
+def _take(d: dict, key):
+    try:
+        return d.pop(key, None)
+    except TypeError:
+        return None
+
+
+# Engine initialisation failures are remembered: a machine without a usable
+# GPU pays for the attempt once, then every query goes straight to z3.
+_engine_failed: Optional[str] = None
+
+
+def _prefilter(key, constraints, timeout: int, deadline: float):
+    """GPU path of get_model: a model, or None (miss / rejected witness)."""
+    global _engine_failed
+    hit = _take(_batch_witness, key)
+    if hit is None:
+        if _take(_gpu_missed, key) or _engine_failed is not None:
+            return None
+        with _Phase("flatten"):
+            nodes = _raw_nodes(constraints)
+        stats.gpu_queries += 1
+        t0 = time.perf_counter()
+        try:
+            hit = gpu_search(nodes, budget_ms=min(timeout, SEARCH_BUDGET_MS))
+        except EngineUnavailable as e:
+            _engine_failed = str(e)
+            raise
+        finally:
+            stats.gpu_time += time.perf_counter() - t0
+        if hit is None:
+            return None
+    m = _accept(constraints, hit[0], hit[1], deadline)
+    if m is not None:
+        stats.gpu_hits += 1
+    return m
+
+
 @lru_cache(maxsize=2 ** 23)
 def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True):
+    key = constraints
     timeout = args.solver_timeout
     if enforce_execution_time:
         timeout = min(timeout, time_handler.time_remaining() - 500)
@@ -347,48 +490,23 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         if type(constraint) == bool and not constraint:
             raise UnsatError
     constraints = [c for c in constraints if type(c) != bool]
+    # one deadline for the whole query: GPU search, witness verification and
+    # the z3 fallback together stay within the reference's timeout
+    deadline = time.perf_counter() + timeout / 1000.0
 
     if not minimize and not maximize:
         try:
-            nodes = _raw_nodes(constraints)
-            stats.gpu_queries += 1
-            t0 = time.perf_counter()
-            hit = gpu_search(nodes, budget_ms=min(timeout, 200))
-            stats.gpu_time += time.perf_counter() - t0
-            if hit is not None:
-                assignment, progs = hit
-                if z3bridge.available():
-                    raws = [getattr(c, "raw", c) for c in constraints]
-                    if all(not isinstance(r, N.Node) for r in raws):
-                        m = z3bridge.verify(raws, assignment, timeout)
-                        if m is not None:
-                            stats.gpu_hits += 1
-                            return Model([m], assignment, progs)
-                        log.warning("GPU witness rejected by z3; falling back")
-                    else:
-                        stats.gpu_hits += 1
-                        return Model(None, assignment, progs)
-                else:
-                    stats.gpu_hits += 1
-                    return Model(None, assignment, progs)
+            m = _prefilter(key, constraints, timeout, deadline)
+            if m is not None:
+                return m
         except Unsupported as e:
             stats.unsupported += 1
             log.debug("GPU pre-filter: unsupported (%s)", e)
-        except (EngineUnavailable, EngineError, z3bridge.Z3Unavailable) as e:
-            log.debug("GPU pre-filter unavailable: %s", e)
+        except Exception as e:  # noqa: BLE001 - any engine failure falls back to z3
+            stats.errors += 1
+            log.debug("GPU pre-filter failed (%s: %s); falling back to z3", type(e).__name__, e)
         stats.fallbacks += 1
-    return _z3_check(constraints, minimize, maximize, timeout)
-
-
-def _witness_accepted(constraints, assignment, timeout) -> bool:
-    """get_model's rule for a GPU witness: re-verified by z3 when the
-    constraints are z3 ASTs and z3 is present, otherwise accepted (it was
-    evaluated bit-exactly on the device)."""
-    if z3bridge.available():
-        raws = [getattr(c, "raw", c) for c in constraints]
-        if all(not isinstance(r, N.Node) for r in raws):
-            return z3bridge.verify(raws, assignment, timeout) is not None
-    return True
+    return _z3_check(constraints, minimize, maximize, _remaining_ms(deadline))
 
 
 def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool]:
@@ -399,59 +517,74 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
     (``mythril/laser/ethereum/state/constraints.py:26-35``: possible iff
     ``get_model(tuple(self))`` does not raise ``UnsatError``), called once per
     state by LASER's state filters (``mythril/laser/ethereum/svm.py:201-203``
-    open states per transaction, ``:257-262`` new states per step).  A set
-    with a GPU witness (accepted by the same rule as ``get_model``) is
-    possible; every other set goes through ``get_model`` itself — its cache,
-    timeout arithmetic, Python-bool handling and z3 fallback — so the answers
-    are the ones the per-state loop gives, and UNSAT is only concluded by
-    z3."""
+    open states per transaction, ``:257-262`` new states per step).  Every set
+    then goes through ``get_model`` itself — its cache, timeout arithmetic,
+    Python-bool handling and z3 fallback — so the answers are the ones the
+    per-state loop gives and UNSAT is only concluded by z3: a set with a GPU
+    witness hands it to get_model (accepted by the same rule, no second
+    search), a set the batch missed goes straight to z3."""
+    global _engine_failed
     sets = [tuple(c) for c in constraint_sets]
-    results: List[Optional[bool]] = [None] * len(sets)
     timeout = args.solver_timeout
     if enforce_execution_time:
         timeout = min(timeout, time_handler.time_remaining() - 500)
-    pending = []                          # (set index, constraints, bucket programs)
-    if timeout > 0:
-        for i, cs in enumerate(sets):
+    pending = []                          # (set, bucket programs)
+    if timeout > 0 and _engine_failed is None:
+        for cs in sets:
             if any(type(c) == bool and not c for c in cs):
                 continue                                   # get_model raises UnsatError
-            cs = [c for c in cs if type(c) != bool]
             try:
-                nodes = _raw_nodes(cs)
-                progs = [_compile_search(b)
-                         for b in dependence_buckets(nodes)]
+                with _Phase("flatten"):
+                    nodes = _raw_nodes([c for c in cs if type(c) != bool])
+                with _Phase("compile"):
+                    progs = [_compile_search(b) for b in dependence_buckets(nodes)]
             except Unsupported as e:
                 stats.unsupported += 1
                 log.debug("GPU pre-filter: unsupported (%s)", e)
                 continue
-            pending.append((i, cs, progs))
+            except Exception as e:  # noqa: BLE001
+                stats.errors += 1
+                log.debug("GPU pre-filter failed on a set: %s", e)
+                continue
+            pending.append((cs, progs))
     if pending:
         try:
-            eng = get_engine()
             t0 = time.perf_counter()
-            flat = [p for _, _, progs in pending for p in progs]
-            loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in flat]
-            hits = iter(eng.batch_search(loaded, SEARCH_SEED, SEARCH_CANDIDATES))
+            eng = get_engine()
+            flat = [p for _, progs in pending for p in progs]
+            n_cand = _n_cand(flat, min(timeout, SEARCH_BUDGET_MS))
+            with _Phase("load"):
+                loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in flat]
+            with _Phase("search"):
+                hits = iter(eng.batch_search(loaded, SEARCH_SEED, n_cand))
             stats.gpu_time += time.perf_counter() - t0
-            for i, cs, progs in pending:
+            for cs, progs in pending:
                 found = [next(hits) for _ in progs]
                 stats.gpu_queries += 1
-                stats.gpu_candidates += sum(SEARCH_CANDIDATES if k < 0 else k + 1 for k, _ in found)
+                stats.gpu_candidates += sum(n_cand if k < 0 else k + 1 for k, _ in found)
                 if any(k < 0 for k, _ in found):
-                    continue
-                a = _merge([unpack(p, w) for p, (_, w) in zip(progs, found)])
-                if _witness_accepted(cs, a, timeout):
-                    stats.gpu_hits += 1
-                    results[i] = True
-        except (EngineUnavailable, EngineError, z3bridge.Z3Unavailable) as e:
+                    _remember(_gpu_missed, cs, True)
+                else:
+                    a = _merge([unpack(p, w) for p, (_, w) in zip(progs, found)])
+                    _remember(_batch_witness, cs, (a, progs))
+        except EngineUnavailable as e:
+            _engine_failed = str(e)
             log.debug("GPU pre-filter unavailable: %s", e)
-    for i, cs in enumerate(sets):
-        if results[i] is None:
-            try:
-                get_model(cs, enforce_execution_time=enforce_execution_time)
-                results[i] = True
-            except UnsatError:
-                results[i] = False
+        except Exception as e:  # noqa: BLE001
+            stats.errors += 1
+            log.debug("GPU pre-filter failed (%s: %s)", type(e).__name__, e)
+    results = []
+    for cs in sets:
+        try:
+            # the call form of Constraints.is_possible (constraints.py:33), so
+            # the lru_cache entry is the one the per-state loop would hit
+            if enforce_execution_time:
+                get_model(cs)
+            else:
+                get_model(cs, enforce_execution_time=False)
+            results.append(True)
+        except UnsatError:
+            results.append(False)
     return results
 
 
@@ -465,15 +598,34 @@ def filter_possible(states, constraints_of=lambda s: s.world_state.constraints):
     return [s for s, k in zip(states, keep) if k]
 
 
+def _patch_statistics(cls) -> None:
+    """Mythril's ``SolverStatistics`` (a singleton, logged by ``fire_lasers``
+    at ``mythril_analyzer.py:181``) prints the pre-filter's counters after
+    its own two lines."""
+    if getattr(cls, "_mythril_amd_patched", False):
+        return
+    base = cls.__repr__
+
+    def __repr__(self):
+        return base(self) + "\n" + stats.gpu_report()
+    cls.__repr__ = __repr__
+    cls._mythril_amd_patched = True
+
+
 def install() -> None:
     """Rebind ``get_model`` in a Mythril installation: the three names bound
     by ``from ... import get_model``, and share Mythril's
-    ``args`` / ``time_handler`` singletons and its ``Optimize`` wrapper."""
+    ``args`` / ``time_handler`` singletons, its ``Optimize`` wrapper, its
+    ``Model`` class and its ``SolverStatistics``."""
     import importlib
-    global args, time_handler, _stock_optimize
+    global args, time_handler, _stock_optimize, _stock_model
     args = importlib.import_module("mythril.support.support_args").args
     time_handler = importlib.import_module("mythril.laser.ethereum.time_handler").time_handler
-    _stock_optimize = importlib.import_module("mythril.laser.smt").Optimize
+    smt = importlib.import_module("mythril.laser.smt")
+    _stock_optimize = smt.Optimize
+    _stock_model = smt.Model
+    _patch_statistics(importlib.import_module(
+        "mythril.laser.smt.solver.solver_statistics").SolverStatistics)
     get_model.cache_clear()
     for mod in ("mythril.support.model", "mythril.analysis.solver",
                 "mythril.laser.ethereum.state.constraints"):
@@ -485,7 +637,7 @@ def install() -> None:
     if hasattr(solver, "_replace_with_actual_sha"):
         from .sha import replace_with_actual_sha
         kfm = importlib.import_module("mythril.laser.ethereum.keccak_function_manager")
-        sf = importlib.import_module("mythril.laser.smt").symbol_factory
+        sf = smt.symbol_factory
 
         def _replace(concrete_transactions, model, code=None):
             replace_with_actual_sha(concrete_transactions, model,

@@ -8,9 +8,11 @@ this image; every function raises :class:`Z3Unavailable` without it).
   falls back to z3.
 * :func:`to_z3` rebuilds a z3 expression from a DAG (stock-solver fallback for
   constraints built with the z3-free mirror).
-* :func:`verify` substitutes a witness into z3 constraints and simplifies
-  (``substitute`` + ``simplify`` must give ``True``), then returns a genuine z3
-  model by checking the constraints with the witness as equalities.
+* :func:`verify` substitutes a whole witness into the z3 constraints (BV and
+  Bool values, arrays as ``K`` + ``Store`` terms, uninterpreted functions as
+  ite chains over their tables), requires ``simplify`` to give ``True``, and
+  only then returns a genuine z3 model from a ``Solver`` check with every
+  symbol pinned.
 """
 
 from __future__ import annotations
@@ -211,34 +213,117 @@ def to_z3(n: N.Node, memo: Dict[int, object] = None):
     return memo[n.id]
 
 
-def witness_terms(assignment, z3_consts: List[object]):
-    """(z3 const, z3 value) pairs for the BV/Bool variables of a witness."""
+def _symbols(z3_constraints):
+    """Free constants (BV / Bool / array) and uninterpreted function decls of
+    the constraints: one visit per hash-consed node (``get_id``), so shared
+    sub-terms (calldata words over one ``size``, long store chains) are
+    walked once, not once per tree path."""
+    z3 = _z3()
+    consts, funcs = {}, {}
+    seen = set()
+    stack = list(z3_constraints)
+    while stack:
+        x = stack.pop()
+        xid = x.get_id()
+        if xid in seen:
+            continue
+        seen.add(xid)
+        if z3.is_app(x) and x.decl().kind() == z3.Z3_OP_UNINTERPRETED:
+            if z3.is_const(x):
+                consts[xid] = x
+            else:
+                funcs[x.decl().name()] = x.decl()
+        stack.extend(x.children())
+    return list(consts.values()), funcs
+
+
+def _table_term(z3, dom_sort, rng_sort, table):
+    """A free array's model table as ``Store(...Store(K(dom, else), k, v)...)``,
+    first entry outermost (first match wins, as the witness reads it)."""
+    entries, default = table
+    t = z3.K(dom_sort, z3.BitVecVal(default, rng_sort.size()))
+    for k, v in reversed(entries):
+        t = z3.Store(t, z3.BitVecVal(k, dom_sort.size()), z3.BitVecVal(v, rng_sort.size()))
+    return t
+
+
+def _uf_term(z3, arg, rng_size, table):
+    entries, default = table
+    t = z3.BitVecVal(default, rng_size)
+    for k, v in reversed(entries):
+        t = z3.If(arg == z3.BitVecVal(k, arg.size()), z3.BitVecVal(v, rng_size), t)
+    return t
+
+
+def interpretation(assignment, consts):
+    """(z3 const, value term) pairs interpreting every free constant of the
+    witness; a symbol the witness does not mention did not influence the
+    device evaluation, so any value is consistent: 0 / false / K(0)."""
     z3 = _z3()
     out = []
-    for c in z3_consts:
+    for c in consts:
         name = c.decl().name()
-        if name in assignment.vars:
-            v = assignment.vars[name]
-            out.append((c, z3.BoolVal(bool(v)) if z3.is_bool(c) else z3.BitVecVal(v, c.size())))
+        s = c.sort()
+        if z3.is_bool(c):
+            out.append((c, z3.BoolVal(bool(assignment.vars.get(name, 0)))))
+        elif z3.is_bv_sort(s):
+            out.append((c, z3.BitVecVal(assignment.vars.get(name, 0), s.size())))
+        elif z3.is_array_sort(s):
+            out.append((c, _table_term(z3, s.domain(), s.range(),
+                                       assignment.arrays.get(name, ([], 0)))))
     return out
 
 
+def _replace_ufs(z3, e, funcs, assignment):
+    """Rebuild ``e`` with every application of an uninterpreted function
+    replaced by the ite chain over the witness's table for it."""
+    if not funcs:
+        return e
+    memo: Dict[int, object] = {}
+    stack = [(e, False)]
+    while stack:
+        x, done = stack.pop()
+        xid = x.get_id()
+        if xid in memo:
+            continue
+        kids = x.children()
+        if not done:
+            stack.append((x, True))
+            stack.extend((k, False) for k in kids if k.get_id() not in memo)
+            continue
+        new = [memo[k.get_id()] for k in kids]
+        if z3.is_app(x) and x.decl().kind() == z3.Z3_OP_UNINTERPRETED and kids:
+            name = x.decl().name()
+            r = _uf_term(z3, new[0], x.size(), assignment.funcs.get(name, ([], 0)))
+        elif kids and any(n.get_id() != k.get_id() for n, k in zip(new, kids)):
+            r = x.decl()(*new)
+        else:
+            r = x
+        memo[xid] = r
+    return memo[e.get_id()]
+
+
 def verify(z3_constraints, assignment, timeout_ms: int):
-    """Re-verify a GPU witness with z3 and return a z3 model, or None."""
+    """Re-verify a GPU witness with z3: substitute the whole
+    witness — BV / Bool values, arrays as ``K`` + ``Store`` terms, UF
+    applications as ite chains over their tables — and require ``simplify``
+    to give ``True``; only then ask a ``Solver`` (every symbol pinned, so the
+    check is immediate) for a genuine z3 model.  None if z3 disagrees."""
     z3 = _z3()
-    consts = set()
-    for c in z3_constraints:
-        stack = [c]
-        while stack:
-            x = stack.pop()
-            if z3.is_const(x) and x.decl().kind() == z3.Z3_OP_UNINTERPRETED:
-                consts.add(x)
-            stack.extend(x.children())
+    consts, funcs = _symbols(z3_constraints)
+    pins = interpretation(assignment, consts)
+    ground = z3.And(*z3_constraints) if len(z3_constraints) != 1 else z3_constraints[0]
+    ground = _replace_ufs(z3, z3.substitute(ground, *pins) if pins else ground, funcs, assignment)
+    if not z3.is_true(z3.simplify(ground)):
+        return None
     s = z3.Solver()
     s.set(timeout=max(1, int(timeout_ms)))
     s.add(*z3_constraints)
-    for c, v in witness_terms(assignment, list(consts)):
+    for c, v in pins:
         s.add(c == v)
+    for name, f in funcs.items():
+        for k, v in assignment.funcs.get(name, ([], 0))[0]:
+            s.add(f(z3.BitVecVal(k, f.domain(0).size())) == z3.BitVecVal(v, f.range().size()))
     if s.check() == z3.sat:
         return s.model()
     return None

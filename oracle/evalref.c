@@ -541,6 +541,38 @@ int ev_run_gen(const uint32_t* nodes, uint32_t n_nodes, const uint64_t* consts,
     return 0;
 }
 
+/* Per-root bits under explicit leaf values: root_out[a * n_roots + r]. */
+int ev_run_leaves_roots(const uint32_t* nodes, uint32_t n_nodes, const uint64_t* consts,
+                        const table_desc* td, uint32_t n_tables, const uint32_t* leafidx,
+                        const uint32_t* roots, uint32_t n_roots, uint32_t n_leaves,
+                        const uint64_t* leaves_in, uint64_t n, uint8_t* root_out, int threads) {
+    table_t tabs[64];
+    if (n_tables > 64) return -1;
+    make_tables(td, n_tables, leafidx, tabs);
+    dag_t g = {nodes, n_nodes, consts, tabs, n_tables};
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+    {
+        V* vals = (V*)malloc(sizeof(V) * (n_nodes ? n_nodes : 1));
+        V* leaves = (V*)malloc(sizeof(V) * (n_leaves ? n_leaves : 1));
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t a = 0; a < (int64_t)n; ++a) {
+            for (uint32_t l = 0; l < n_leaves; ++l) {
+                vzero(&leaves[l]);
+                for (int i = 0; i < 4; ++i) leaves[l].w[i] = leaves_in[((uint64_t)a * n_leaves + l) * 4 + i];
+            }
+            eval_dag(&g, leaves, vals);
+            for (uint32_t r = 0; r < n_roots; ++r)
+                root_out[(uint64_t)a * n_roots + r] = (uint8_t)(vals[roots[r]].w[0] & 1);
+        }
+        free(vals);
+        free(leaves);
+    }
+    return 0;
+}
+
 /* Evaluate under explicit leaf values: leaves [n_leaves][4 x u64] per
  * assignment (AoS, n of them); writes every node value for assignment 0..n-1
  * into vals_out ([n][n_nodes][8 x u64]) when non-NULL, and root bits. */

@@ -68,9 +68,11 @@ def serialize(constraints: Sequence[Node], program, probes: Sequence[Node] = ())
         if name not in table_ix:
             n = program.table_sizes[name]
             koff = len(S.leafidx)
-            S.leafidx += [li["%s#k%d#0" % (name, e)] for e in range(n)]
+            # leaves of entries a program never consults (a table read only
+            # at its constant keys) are absent: index them as leaf 0
+            S.leafidx += [li.get("%s#k%d#0" % (name, e), 0) for e in range(n)]
             voff = len(S.leafidx)
-            S.leafidx += [li["%s#v%d#0" % (name, e)] for e in range(n)]
+            S.leafidx += [li.get("%s#v%d#0" % (name, e), 0) for e in range(n)]
             # constant-keyed entries first (ir.scan_const_keys): key constant
             # indices, then their value leaves (a value leaf a query never
             # reads is absent from the program: index it as leaf 0, which the
@@ -172,6 +174,8 @@ def lib():
                                  p, C.c_int]
         L.ev_run_leaves.argtypes = [p, C.c_uint32, p, p, C.c_uint32, p, p, C.c_uint32, C.c_uint32,
                                     p, C.c_uint64, p, p]
+        L.ev_run_leaves_roots.argtypes = [p, C.c_uint32, p, p, C.c_uint32, p, p, C.c_uint32,
+                                          C.c_uint32, p, C.c_uint64, p, C.c_int]
         _lib = L
     return _lib
 
@@ -227,6 +231,27 @@ def run_leaves(S: Serialized, program, leaf_vals: Sequence[Sequence[int]], want_
                              None if vals_out is None else _p(vals_out), _p(out))
     assert rc == 0
     return out[:n].astype(bool), vals_out
+
+
+def run_leaves_soa(S: Serialized, program, leaves_soa: np.ndarray, per_root: bool = False,
+                   threads: int = 0) -> np.ndarray:
+    """Root bits (``per_root``: (n, n_constraints) bits of every constraint)
+    under the engine's own leaf buffer ((n_leaves, 8, n) u32 limbs, e.g.
+    ``Engine.eval_gen(..., want_leaves=True)``)."""
+    nodes, consts, tabs, leafidx, roots = _arrays(S)
+    nl, _, n = leaves_soa.shape
+    x = np.ascontiguousarray(leaves_soa.transpose(2, 0, 1)).astype(np.uint64)   # (n, nl, 8)
+    lv = np.ascontiguousarray(x[:, :, 0::2] | (x[:, :, 1::2] << np.uint64(32)))  # (n, nl, 4)
+    if nl == 0:
+        lv = np.zeros((max(1, n), 1, 4), dtype=np.uint64)
+    nr = max(1, len(S.roots))
+    out = np.zeros((max(1, n), nr), dtype=np.uint8)
+    rc = lib().ev_run_leaves_roots(_p(nodes), nodes.shape[0], _p(consts),
+                                   C.cast(tabs, C.c_void_p), len(S.tables), _p(leafidx), _p(roots),
+                                   len(S.roots), max(nl, 1), _p(lv), n, _p(out), threads)
+    assert rc == 0
+    bits = out[:n, :len(S.roots)].astype(bool)
+    return bits if per_root else bits.all(axis=1)
 
 
 def node_value(vals_out, a: int, rec_index: int) -> int:

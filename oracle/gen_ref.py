@@ -1,7 +1,7 @@
 """ORACLE — test infrastructure only.
 
 Host restatement of the device candidate generator (``_gen_leaf`` in
-``mythril_amd/asmgen.py``, ``gen_leaf`` in ``mythril_amd/csrc/mg_kernels.hip``; contract in ``include/mythgpu.h``
+``mythril_amd/asmgen.py``; contract in ``include/mythgpu.h``
 ``mg_leafgen``), so tests can rebuild the exact assignment a GPU lane
 evaluated and check the lane against ``oracle/smtlib_ref.py``.
 """

@@ -204,3 +204,111 @@ def test_bucketed_witness_joins_group_assignments(monkeypatch, fresh):
     a, progs = REAL_GPU_SEARCH(nodes, 200)
     assert Eng.calls == 1 and len(progs) == 2
     assert a.vars == {"x": 9, "y": 4}
+
+
+# ---- failure handling, deadline, hand-over, statistics, Model (round 2) ----
+
+@pytest.fixture
+def reset_engine_memo():
+    M._engine_failed = None
+    M._batch_witness.clear()
+    M._gpu_missed.clear()
+    yield
+    M._engine_failed = None
+    M._batch_witness.clear()
+    M._gpu_missed.clear()
+
+
+def test_engine_init_failure_is_remembered(monkeypatch, fresh, reset_engine_memo):
+    from mythril_amd.engine import EngineUnavailable
+    calls = []
+
+    def no_gpu(nodes, budget_ms):
+        calls.append(1)
+        raise EngineUnavailable("mg_init failed")
+    monkeypatch.setattr(M, "gpu_search", no_gpu)
+    x = symbol_factory.BitVecSym("x", 256)
+    for k in range(3):
+        with pytest.raises(M.SolverUnavailable):       # -> z3 (absent here)
+            M.get_model((ULT(x, symbol_factory.BitVecVal(k + 5, 256)),))
+    assert calls == [1]
+
+
+def test_unexpected_prefilter_error_falls_back(monkeypatch, fresh, reset_engine_memo):
+    def broken(nodes, budget_ms):
+        raise AttributeError("bug in a front-end")
+    monkeypatch.setattr(M, "gpu_search", broken)
+    before = M.stats.errors
+    with pytest.raises(M.SolverUnavailable):
+        M.get_model((c_sat(),))
+    assert M.stats.errors == before + 1
+
+
+def test_one_deadline_bounds_search_and_fallback(monkeypatch, fresh, reset_engine_memo):
+    import time
+    seen = {}
+
+    def slow_miss(nodes, budget_ms):
+        seen["budget"] = budget_ms
+        time.sleep(0.15)
+        return None
+
+    def fake_z3(constraints, minimize, maximize, timeout):
+        seen["z3_timeout"] = timeout
+        raise M.UnsatError
+    monkeypatch.setattr(M, "gpu_search", slow_miss)
+    monkeypatch.setattr(M, "_z3_check", fake_z3)
+    M.args.solver_timeout = 400
+    with pytest.raises(M.UnsatError):
+        M.get_model((c_sat(),))
+    assert seen["budget"] <= 200
+    assert seen["z3_timeout"] <= 400 - 150 + 5
+
+
+def test_batch_witness_is_handed_to_get_model(batch_env, monkeypatch, reset_engine_memo):
+    eng, z3_calls = batch_env
+    searches = []
+    monkeypatch.setattr(M, "gpu_search", lambda nodes, budget_ms: searches.append(1))
+    sat, unsat_like = (c_sat(),), (symbol_factory.Bool(False).__class__(symbol_factory.Bool(False).raw),)
+    assert M.batch_is_possible([sat, unsat_like]) == [True, False]
+    assert searches == []                        # neither set searched twice
+    assert len(z3_calls) == 1                    # only the miss reached z3
+    m = M.get_model(sat)                         # cached model of the batch witness
+    assert m.assignment is not None and searches == []
+
+
+def test_statistics_patch_extends_reference_repr():
+    class RefStats:
+        def __init__(self):
+            self.query_count, self.solver_time = 3, 1.5
+
+        def __repr__(self):
+            return "Query count: {} \nSolver time: {}".format(self.query_count, self.solver_time)
+    M._patch_statistics(RefStats)
+    M._patch_statistics(RefStats)               # idempotent
+    text = repr(RefStats())
+    assert text.startswith("Query count: 3 \nSolver time: 1.5\nGPU pre-filter:")
+    assert text.count("GPU pre-filter") == 1
+    for phase in M.PHASES:
+        assert phase in text
+
+
+def test_model_getitem_follows_reference_semantics():
+    class Z3Model:
+        def __init__(self, d, size):
+            self.d, self.size = d, size
+
+        def __getitem__(self, item):
+            if isinstance(item, int) and item >= self.size:
+                raise IndexError(item)
+            return self.d.get(item)
+
+        def decls(self):
+            return list(self.d)
+    m = M.Model([Z3Model({"a": 1}, 1), Z3Model({"b": 2}, 1)])
+    assert m["a"] == 1 and m["b"] == 2 and m["c"] is None
+    with pytest.raises(IndexError):              # the last model's IndexError propagates
+        m[5]
+    assert M.Model([Z3Model({}, 0), Z3Model({"b": 2}, 3)])[1] is None   # earlier one skipped
+    w = M.Model(None, Assignment(vars={"x": 7}))
+    assert w["x"] == 7 and w["y"] is None

@@ -1,10 +1,13 @@
 #!/bin/bash
-# GPU round trip: full -m gpu parity suite, then the bench (no CPU leg).
+# GPU round trip: full -m gpu parity suite, the search bench (per query
+# shape), then the bench (no CPU leg).  Each step has its own time limit and
+# the script stops at the first failure.
 # Usage: tools/gpu_round.sh <tag> [bench args...]
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 TAG=${1:-run}; shift
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; echo "gpu tests failed"; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; echo "gpu tests failed"; exit 1; }
 tail -1 gpurun_out/${TAG}_tests.log
+timeout -k 10 300 python -u tools/search_bench.py > gpurun_out/${TAG}_search.log 2>&1 || { tail -30 gpurun_out/${TAG}_search.log; echo "search bench failed"; exit 1; }
 timeout -k 10 300 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > gpurun_out/${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench.log; echo "bench failed"; exit 1; }
 python -c "
 import json,sys; t=open('gpurun_out/${TAG}_bench.log').read(); d=json.loads(t[t.index('{'):])

@@ -19,7 +19,13 @@ Three numbers, printed as one JSON line:
   check, median of 5 with the lru cache cleared; and ``batch_is_possible``
   over the same queries as sibling states (one batched search).
 
-Usage:  python tools/search_bench.py [--dags 1024]
+* ``shapes`` -- per stand-in query shape C1 / C3 / C4
+  (mythril_amd/workloads.py): one batched search over the shape's queries
+  (hit rate, candidates/s over the candidates needed, wall time) and the
+  drop-in ``get_model`` per query (median latency and the per-phase split:
+  flatten, compile, load, search, verify).
+
+Usage:  python tools/search_bench.py [--dags 1024] [--shape-queries 64]
 """
 
 import argparse
@@ -57,10 +63,68 @@ def reference_sat_queries(engine):
     }
 
 
+def shape_lines(eng, n_queries):
+    import mythril_amd.model as M
+    from mythril_amd import workloads as W
+    from mythril_amd.smt.node import topo_order
+    out = {}
+    M.time_handler.start_execution(3600)
+    for name in ("c1", "c3", "c4"):
+        qs = W.queries(name, n_queries)
+        t0 = time.perf_counter()
+        progs, qmap = [], []
+        for qi, q in enumerate(qs):
+            for b in M.dependence_buckets(q):
+                progs.append(M._compile_search(b))
+                qmap.append(qi)
+        t_compile = time.perf_counter() - t0
+        loaded = [eng.load(p, M.search_leafgen(p), prog_seed=0) for p in progs]
+        n_cand = M.SEARCH_CANDIDATES
+        eng.batch_search(loaded[:2], M.SEARCH_SEED, 1 << 16)       # warm-up
+        t0 = time.perf_counter()
+        hits = eng.batch_search(loaded, M.SEARCH_SEED, n_cand)
+        dt = time.perf_counter() - t0
+        solved = [True] * len(qs)
+        for qi, (i, _) in zip(qmap, hits):
+            solved[qi] = solved[qi] and i >= 0
+        needed = sum(n_cand if i < 0 else i + 1 for i, _ in hits)
+        ins_cand = sum((n_cand if i < 0 else i + 1) * p.n_ins for (i, _), p in zip(hits, progs))
+        # the drop-in get_model, one query at a time (no z3 here: a miss
+        # raises SolverUnavailable after the GPU search)
+        lat, misses = [], 0
+        M.stats.reset_gpu()
+        sample = qs[:16]
+        for q in sample:
+            M.get_model.cache_clear()
+            t1 = time.perf_counter()
+            try:
+                M.get_model(tuple(q), enforce_execution_time=False)
+            except M.SolverUnavailable:
+                misses += 1
+            lat.append((time.perf_counter() - t1) * 1000.0)
+        out[name] = {
+            "queries": len(qs), "programs": len(progs),
+            "source_nodes_mean": statistics.mean(len(topo_order(q)) for q in qs),
+            "ir_ins_mean": statistics.mean(p.n_ins for p in progs),
+            "compile_ms_per_query": t_compile * 1000.0 / len(qs),
+            "batch": {"candidates_per_program": n_cand, "wall_s": dt,
+                      "queries_with_witness": sum(solved), "hit_rate": sum(solved) / len(qs),
+                      "candidates_needed": needed, "candidates_per_s": needed / dt,
+                      "ir_ins_candidates_per_s": ins_cand / dt},
+            "get_model": {"queries": len(sample), "median_ms": statistics.median(lat),
+                          "max_ms": max(lat), "gpu_misses": misses,
+                          "phase_ms_per_query": {k: v * 1000.0 / len(sample)
+                                                 for k, v in M.stats.phase.items()}},
+        }
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dags", type=int, default=1024)
     ap.add_argument("--chunks", type=int, default=8, help="2^20-candidate chunks (unsat query)")
+    ap.add_argument("--shape-queries", type=int, default=64)
+    ap.add_argument("--skip-corpus", action="store_true")
     args = ap.parse_args()
 
     import bench
@@ -91,6 +155,12 @@ def main():
     out["unsat_candidates_per_s"] = args.chunks * chunk / dt
     out["unsat_query"] = {"ir_instructions": int(len(prog.code)), "candidates": args.chunks * chunk,
                           "ms_per_2^20_chunk": dt * 1000.0 / args.chunks}
+
+    out["shapes"] = shape_lines(eng, args.shape_queries)
+    print(json.dumps({"shapes": out["shapes"]}), flush=True)
+    if args.skip_corpus:
+        print(json.dumps(out), flush=True)
+        return
 
     # --- C2 corpus, batched search -----------------------------------------
     loaded = [eng.load(p, M.search_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
