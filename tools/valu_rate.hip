@@ -1,0 +1,132 @@
+// VALU issue rates on gfx950 in one harness, clock-independent: every wave
+// stamps s_memtime (shader clock) around its loop, so the result is SIMD
+// cycles per wave64 instruction = elapsed cycles / (waves on the SIMD x
+// instructions per wave), with no assumed clock; s_memrealtime (100 MHz)
+// gives the clock the chip actually ran at.  Reconciles the int32 ceiling
+// used by mythril_amd/roofline.py with MI355X_MICROARCH.md's "a wave64 VALU
+// instruction issues over 2 cycles" (v_fma_f32) — measured, per instruction.
+//
+// Build: hipcc --offload-arch=gfx950 -O3 tools/valu_rate.hip -o tools/valu_rate
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <vector>
+
+#define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+
+#define ITERS 4000
+#define R4(x) x x x x
+#define R16(x) R4(x) R4(x) R4(x) R4(x)
+
+struct Stamp { uint64_t t0, t1, r0, r1; };
+
+#define BODY8(ins) R16(ins "0\n" ins "1\n" ins "2\n" ins "3\n" ins "4\n" ins "5\n" ins "6\n" ins "7\n")
+
+// 8 independent accumulators v[40..47] (+ v[48..55] for 64-bit ops), 128
+// instructions per iteration; the operand is a second register.
+#define KERNEL(NAME, TEXT)                                                        \
+    __global__ __launch_bounds__(64) void NAME(Stamp* st, uint32_t s) {           \
+        asm volatile("v_mov_b32 v60, %0\n v_mov_b32 v61, %0" ::"v"(threadIdx.x)   \
+                     : "v60", "v61");                                             \
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();                         \
+        const uint64_t r0 = __builtin_amdgcn_s_memrealtime();                     \
+        for (int i = 0; i < ITERS; ++i)                                           \
+            asm volatile(R16(TEXT) ::: "v40", "v41", "v42", "v43", "v44", "v45",   \
+                         "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53",  \
+                         "v54", "v55", "v60", "v61", "vcc");                      \
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();                         \
+        const uint64_t r1 = __builtin_amdgcn_s_memrealtime();                     \
+        if (threadIdx.x == 0) st[blockIdx.x] = Stamp{t0, t1, r0, r1};             \
+    }
+
+KERNEL(k_fma_f32, "v_fma_f32 v40, v40, v60, v61\n v_fma_f32 v41, v41, v60, v61\n"
+                  "v_fma_f32 v42, v42, v60, v61\n v_fma_f32 v43, v43, v60, v61\n"
+                  "v_fma_f32 v44, v44, v60, v61\n v_fma_f32 v45, v45, v60, v61\n"
+                  "v_fma_f32 v46, v46, v60, v61\n v_fma_f32 v47, v47, v60, v61\n")
+KERNEL(k_pk_fma_f32, "v_pk_fma_f32 v[40:41], v[40:41], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[42:43], v[42:43], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[44:45], v[44:45], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[46:47], v[46:47], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[48:49], v[48:49], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[50:51], v[50:51], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[52:53], v[52:53], v[60:61], v[60:61]\n"
+                     "v_pk_fma_f32 v[54:55], v[54:55], v[60:61], v[60:61]\n")
+KERNEL(k_add_u32, "v_add_u32 v40, v40, v60\n v_add_u32 v41, v41, v60\n v_add_u32 v42, v42, v60\n"
+                  "v_add_u32 v43, v43, v60\n v_add_u32 v44, v44, v60\n v_add_u32 v45, v45, v60\n"
+                  "v_add_u32 v46, v46, v60\n v_add_u32 v47, v47, v60\n")
+KERNEL(k_add_f32, "v_add_f32 v40, v40, v60\n v_add_f32 v41, v41, v60\n v_add_f32 v42, v42, v60\n"
+                  "v_add_f32 v43, v43, v60\n v_add_f32 v44, v44, v60\n v_add_f32 v45, v45, v60\n"
+                  "v_add_f32 v46, v46, v60\n v_add_f32 v47, v47, v60\n")
+KERNEL(k_xor_b32, "v_xor_b32 v40, v40, v60\n v_xor_b32 v41, v41, v60\n v_xor_b32 v42, v42, v60\n"
+                  "v_xor_b32 v43, v43, v60\n v_xor_b32 v44, v44, v60\n v_xor_b32 v45, v45, v60\n"
+                  "v_xor_b32 v46, v46, v60\n v_xor_b32 v47, v47, v60\n")
+KERNEL(k_pk_mov_b32, "v_pk_mov_b32 v[40:41], v[60:61], v[40:41] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[42:43], v[60:61], v[42:43] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[44:45], v[60:61], v[44:45] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[46:47], v[60:61], v[46:47] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[48:49], v[60:61], v[48:49] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[50:51], v[60:61], v[50:51] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[52:53], v[60:61], v[52:53] op_sel:[0,1]\n"
+                     "v_pk_mov_b32 v[54:55], v[60:61], v[54:55] op_sel:[0,1]\n")
+KERNEL(k_addc_chain, "v_add_co_u32 v40, vcc, v40, v60\n v_addc_co_u32 v41, vcc, v41, v60, vcc\n"
+                     "v_addc_co_u32 v42, vcc, v42, v60, vcc\n v_addc_co_u32 v43, vcc, v43, v60, vcc\n"
+                     "v_addc_co_u32 v44, vcc, v44, v60, vcc\n v_addc_co_u32 v45, vcc, v45, v60, vcc\n"
+                     "v_addc_co_u32 v46, vcc, v46, v60, vcc\n v_addc_co_u32 v47, vcc, v47, v60, vcc\n")
+KERNEL(k_mad_u64, "v_mad_u64_u32 v[40:41], vcc, v60, v61, v[40:41]\n"
+                  "v_mad_u64_u32 v[42:43], vcc, v60, v61, v[42:43]\n"
+                  "v_mad_u64_u32 v[44:45], vcc, v60, v61, v[44:45]\n"
+                  "v_mad_u64_u32 v[46:47], vcc, v60, v61, v[46:47]\n"
+                  "v_mad_u64_u32 v[48:49], vcc, v60, v61, v[48:49]\n"
+                  "v_mad_u64_u32 v[50:51], vcc, v60, v61, v[50:51]\n"
+                  "v_mad_u64_u32 v[52:53], vcc, v60, v61, v[52:53]\n"
+                  "v_mad_u64_u32 v[54:55], vcc, v60, v61, v[54:55]\n")
+
+struct B { const char* name; void (*fn)(Stamp*, uint32_t); double lane_ops_per_ins; };
+
+int main() {
+    hipDeviceProp_t prop;
+    CHK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    B bs[] = {{"v_fma_f32", k_fma_f32, 1}, {"v_pk_fma_f32", k_pk_fma_f32, 2},
+              {"v_add_f32", k_add_f32, 1}, {"v_add_u32", k_add_u32, 1},
+              {"v_xor_b32", k_xor_b32, 1}, {"v_pk_mov_b32", k_pk_mov_b32, 2},
+              {"v_add/addc_co chain", k_addc_chain, 1}, {"v_mad_u64_u32", k_mad_u64, 1}};
+    const int waves[] = {1, 3, 8};
+    Stamp* d_st;
+    CHK(hipMalloc(&d_st, sizeof(Stamp) * cus * 4 * 8));
+    printf("{\"device\": \"%s\", \"cus\": %d, \"instructions_per_wave\": %d}\n", prop.name, cus,
+           ITERS * 128);
+    for (auto& b : bs) {
+        for (int w : waves) {
+            const int blocks = cus * 4 * w;
+            double cyc = 0, ghz = 0;
+            for (int rep = 0; rep < 3; ++rep) {
+                hipLaunchKernelGGL(b.fn, dim3(blocks), dim3(64), 0, 0, d_st, 3u);
+                CHK(hipGetLastError());
+                CHK(hipDeviceSynchronize());
+            }
+            std::vector<Stamp> st(blocks);
+            CHK(hipMemcpy(st.data(), d_st, sizeof(Stamp) * blocks, hipMemcpyDeviceToHost));
+            std::vector<double> c(blocks), g(blocks);
+            for (int i = 0; i < blocks; ++i) {
+                c[i] = (double)(st[i].t1 - st[i].t0);
+                g[i] = c[i] / (double)(st[i].r1 - st[i].r0) * 0.1;   // GHz
+            }
+            std::sort(c.begin(), c.end());
+            std::sort(g.begin(), g.end());
+            cyc = c[blocks / 2];
+            ghz = g[blocks / 2];
+            // a wave's loop spans all w co-resident waves of its SIMD
+            const double per_ins = cyc / ((double)w * ITERS * 128);
+            const double peak = 256.0 * 4 * 64 * b.lane_ops_per_ins / per_ins * ghz * 1e9;
+            printf("{\"ins\": \"%s\", \"waves_per_simd\": %d, \"simd_cycles_per_ins\": %.3f, "
+                   "\"clock_ghz\": %.3f, \"chip_lane_ops_per_s_T\": %.2f}\n", b.name, w, per_ins,
+                   ghz, peak / 1e12);
+        }
+    }
+    return 0;
+}
