@@ -43,7 +43,9 @@
                                 assembly kernel keeps the first 6 in LDS
                                 (6 x 8 KiB per 256-lane block, 3 blocks per
                                 CU) and the rest in per-lane scratch         */
+#ifndef MG_MAX_PSLOTS        /* (A/B builds may override)                    */
 #define MG_MAX_PSLOTS 112    /* further spill slots in per-lane scratch      */
+#endif
 
 enum mg_op {
     MG_NOP = 0,

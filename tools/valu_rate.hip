@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <map>
 #include <vector>
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
@@ -22,7 +23,7 @@
 #define R4(x) x x x x
 #define R16(x) R4(x) R4(x) R4(x) R4(x)
 
-struct Stamp { uint64_t t0, t1, r0, r1; };
+struct Stamp { uint64_t t0, t1, r0, r1; uint32_t hw, xcc, pad0, pad1; };
 
 #define BODY8(ins) R16(ins "0\n" ins "1\n" ins "2\n" ins "3\n" ins "4\n" ins "5\n" ins "6\n" ins "7\n")
 
@@ -40,7 +41,9 @@ struct Stamp { uint64_t t0, t1, r0, r1; };
                          "v54", "v55", "v60", "v61", "vcc");                      \
         const uint64_t t1 = __builtin_amdgcn_s_memtime();                         \
         const uint64_t r1 = __builtin_amdgcn_s_memrealtime();                     \
-        if (threadIdx.x == 0) st[blockIdx.x] = Stamp{t0, t1, r0, r1};             \
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);            \
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);           \
+        if (threadIdx.x == 0) st[blockIdx.x] = Stamp{t0, t1, r0, r1, hw, xcc, 0, 0}; \
     }
 
 KERNEL(k_fma_f32, "v_fma_f32 v40, v40, v60, v61\n v_fma_f32 v41, v41, v60, v61\n"
@@ -120,12 +123,42 @@ int main() {
             std::sort(g.begin(), g.end());
             cyc = c[blocks / 2];
             ghz = g[blocks / 2];
+            // per SIMD (XCC, SE, SH, CU, SIMD from HW_ID): instructions of all
+            // its waves over the span from the first start to the last end;
+            // independent of how many waves were co-resident
+            std::map<uint64_t, std::pair<std::pair<uint64_t, uint64_t>, int>> simd;
+            for (int i = 0; i < blocks; ++i) {
+                const uint32_t hw = st[i].hw;
+                const uint64_t key = ((uint64_t)(st[i].xcc & 15) << 16) | (((hw >> 13) & 7) << 12) |
+                                     (((hw >> 12) & 1) << 11) | (((hw >> 8) & 15) << 4) |
+                                     ((hw >> 4) & 3);
+                auto it = simd.find(key);
+                if (it == simd.end())
+                    simd[key] = {{st[i].t0, st[i].t1}, 1};
+                else {
+                    it->second.first.first = std::min(it->second.first.first, st[i].t0);
+                    it->second.first.second = std::max(it->second.first.second, st[i].t1);
+                    it->second.second += 1;
+                }
+            }
+            std::vector<double> tput;
+            int maxw = 0;
+            for (auto& kv : simd) {
+                const double span = (double)(kv.second.first.second - kv.second.first.first);
+                tput.push_back(kv.second.second * (double)ITERS * 128 / span);
+                maxw = std::max(maxw, kv.second.second);
+            }
+            std::sort(tput.begin(), tput.end());
+            const double ipc = tput[tput.size() / 2];
             // a wave's loop spans all w co-resident waves of its SIMD
             const double per_ins = cyc / ((double)w * ITERS * 128);
-            const double peak = 256.0 * 4 * 64 * b.lane_ops_per_ins / per_ins * ghz * 1e9;
-            printf("{\"ins\": \"%s\", \"waves_per_simd\": %d, \"simd_cycles_per_ins\": %.3f, "
-                   "\"clock_ghz\": %.3f, \"chip_lane_ops_per_s_T\": %.2f}\n", b.name, w, per_ins,
-                   ghz, peak / 1e12);
+            printf("{\"ins\": \"%s\", \"waves_per_simd\": %d, \"simds_seen\": %zu, "
+                   "\"max_waves_on_a_simd\": %d, \"simd_ins_per_cycle\": %.3f, "
+                   "\"simd_cycles_per_ins\": %.3f, \"wave_cycles_per_ins\": %.3f, "
+                   "\"clock_ghz\": %.3f, \"chip_lane_ops_per_s_T_at_2_4GHz\": %.2f}\n",
+                   b.name, w, simd.size(), maxw, ipc, 1.0 / ipc, cyc / ((double)ITERS * 128), ghz,
+                   256.0 * 4 * 64 * b.lane_ops_per_ins * ipc * 2.4e9 / 1e12);
+            (void)per_ins;
         }
     }
     return 0;
