@@ -9,6 +9,12 @@ ranks with an RCCL all-reduce(MIN) — the search's one exchange step.
 Weak scaling: rank r evaluates candidate indices [r*2^20, (r+1)*2^20) of
 every DAG's stream.
 
+``--shard corpus`` (config C5) shards the corpus axis instead: the corpus is
+``dags x world`` DAGs, split across ranks by longest-processing-time first on
+their node counts (mythril_amd/shard.py), every rank evaluates its own DAGs'
+candidates [s*2^20, (s+1)*2^20) at step s, and nothing is exchanged on the
+data path (still weak scaling: per-rank work is one corpus).
+
 Prints ONE JSON line on rank 0 (contract in the task statement).  Extra
 fields: roofline (INT32 VALU bound, see mythril_amd/roofline.py) and
 cpu_baseline (oracle/evalref.c, the C restatement of z3 model evaluation —
@@ -37,13 +43,73 @@ def _compile_one(dag_id):
     return dag_id, prog, nodes, weight
 
 
-def build_corpus(n_dags, workers):
+def build_corpus(n_dags, workers, dag_ids=None):
+    ids = list(range(n_dags)) if dag_ids is None else list(dag_ids)
     if workers <= 1:
-        return [_compile_one(d) for d in range(n_dags)]
+        return [_compile_one(d) for d in ids]
     import multiprocessing as mp
     ctx = mp.get_context("fork")
     with ctx.Pool(workers) as pool:
-        return sorted(pool.map(_compile_one, range(n_dags), chunksize=16), key=lambda t: t[0])
+        return sorted(pool.map(_compile_one, ids, chunksize=16), key=lambda t: t[0])
+
+
+def my_dags(mode, n_dags, rank, world):
+    """DAG ids this rank evaluates: every DAG (assignment axis) or its LPT
+    share of a ``n_dags x world`` corpus (corpus axis)."""
+    if mode == "assign" or world == 1:
+        return list(range(n_dags))
+    from mythril_amd import shard
+    from mythril_amd.corpus import dag_target_nodes
+    costs = [dag_target_nodes(d, SEED) for d in range(n_dags * world)]
+    return shard.corpus_shard(costs, rank, world)
+
+
+def step_first(mode, step, rank, world, n_assign):
+    """Candidate index of lane 0 at a step: ranks split the candidate space
+    (assignment axis) or all scan the same range of disjoint DAGs (corpus)."""
+    from mythril_amd import shard
+    if mode == "assign":
+        return shard.shard_first(step, rank, world, n_assign)
+    return shard.shard_first(step, 0, 1, n_assign)
+
+
+def timed_run(step, sync, steps, warmup, world, device=None):
+    """The timed region of the contract: W untimed steps, then K steps
+    bracketed by sync + barrier + sync on both sides, elapsed = max over
+    ranks.  ``step(i, k)`` runs step i (k = index among the timed steps, or
+    None in warmup); ``sync`` waits for this rank's device work."""
+    import torch
+    import torch.distributed as dist
+    for i in range(warmup):
+        step(i, None)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(warmup + k, k)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def all_sum(values, world, device=None):
+    """Sum of per-rank numbers (outside the timed region)."""
+    if world == 1:
+        return list(values)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(list(values), dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.tolist()
 
 
 def cpu_baseline(corpus, budget_s=20.0):
@@ -90,6 +156,8 @@ def main():
     ap.add_argument("--dags", type=int, default=4096)
     ap.add_argument("--assign-log2", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", choices=("assign", "corpus"), default="assign",
+                    help="assignment axis (default, C2) or corpus axis (C5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -101,7 +169,7 @@ def main():
     ncpu = os.cpu_count() or 1
     workers = max(1, min(16, ncpu // max(1, world)))
     t0 = time.time()
-    corpus = build_corpus(args.dags, workers)
+    corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world))
     t_compile = time.time() - t0
 
     import torch
@@ -118,8 +186,9 @@ def main():
     batch = eng.batch_create(loaded)
     n_assign = 1 << args.assign_log2
     words = (n_assign + 63) // 64
-    d_bits = torch.empty((args.dags, words), dtype=torch.int64, device="cuda")
-    d_first = torch.empty(args.dags, dtype=torch.int64, device="cuda")
+    n_mine = len(corpus)
+    d_bits = torch.empty((n_mine, words), dtype=torch.int64, device="cuda")
+    d_first = torch.empty(n_mine, dtype=torch.int64, device="cuda")
     # a dedicated (non-default) stream: the library launches on exactly this
     # stream, so the HIP events below bracket the kernel itself (a null
     # handle would make the library fall back to its own internal stream)
@@ -127,45 +196,34 @@ def main():
     torch.cuda.set_stream(stream)
     nodes_per_lane = sum(n for _, _, n, _ in corpus)
     weight_per_lane = sum(w for _, _, _, w in corpus)
-
-    def step(i, ev=None):
-        d_first.fill_(shard.NONE)
-        first = shard.shard_first(i, rank, world, n_assign)
-        if ev:
-            ev[0].record(stream)
-        eng.batch_eval_gen(batch, SEED, first, n_assign, d_bits.data_ptr(), d_first.data_ptr(),
-                           stream.cuda_stream)
-        if ev:
-            ev[1].record(stream)
-        shard.reduce_first_sat(d_first)      # the one exchange step (RCCL MIN)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i, evs[i])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+
+    def step(i, k):
+        d_first.fill_(shard.NONE)
+        first = step_first(args.shard, i, rank, world, n_assign)
+        if k is not None:
+            evs[k][0].record(stream)
+        eng.batch_eval_gen(batch, SEED, first, n_assign, d_bits.data_ptr(), d_first.data_ptr(),
+                           stream.cuda_stream)
+        if k is not None:
+            evs[k][1].record(stream)
+        if args.shard == "assign":
+            shard.reduce_first_sat(d_first)  # the one exchange step (RCCL MIN)
+
+    elapsed = timed_run(step, torch.cuda.synchronize, args.steps, args.warmup, world, "cuda")
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    sat_dags = int((d_first != shard.NONE).sum().item())
+    sat_local = int((d_first != shard.NONE).sum().item())
+    nodes_all, weight_all, sat_all = all_sum([nodes_per_lane, weight_per_lane, sat_local],
+                                             world, "cuda")
+    if args.shard == "assign":
+        nodes_all, sat_all = nodes_per_lane * world, sat_local     # every rank: every DAG
+    sat_dags = int(sat_all)
 
     if rank == 0:
         from mythril_amd.roofline import VALU_PEAK_OPS
         ms_step = elapsed * 1000.0 / args.steps
-        evals = nodes_per_lane * n_assign * world * args.steps
+        evals = nodes_all * n_assign * args.steps
         ops_launch = weight_per_lane * n_assign
         achieved = ops_launch / (kern_ms / 1000.0)
         traffic = None
@@ -190,10 +248,14 @@ def main():
             "vs_baseline": None,
             "dtype": "u32x8 (256-bit bit-vectors)",
             "data": "synthetic (corpus seed 0x6d797468, device-generated candidates)",
-            "config": {"workload": "C2 synthetic corpus: %d random 256-bit DAGs (64-512 nodes) "
-                                   "x 2^%d assignments per GPU" % (args.dags, args.assign_log2),
-                       "dags": args.dags, "assignments_per_gpu": n_assign,
-                       "nodes_total": nodes_per_lane, "parallelism": "dp%d" % world},
+            "config": {"workload": ("C2 synthetic corpus: %d random 256-bit DAGs (64-512 nodes) "
+                                    "x 2^%d assignments per GPU" % (args.dags, args.assign_log2))
+                       if args.shard == "assign" else
+                       ("C5 corpus axis: %d random 256-bit DAGs (64-512 nodes) per GPU, LPT-"
+                        "sharded, x 2^%d assignments each" % (args.dags, args.assign_log2)),
+                       "dags": args.dags * (world if args.shard == "corpus" else 1),
+                       "assignments_per_gpu": n_assign, "nodes_total": int(nodes_all),
+                       "shard": args.shard, "parallelism": "dp%d" % world},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
                          "traffic": traffic, "kernel_ms": kern_ms,

@@ -51,6 +51,13 @@ def dag_seed(seed: int, dag_id: int) -> int:
     return SplitMix64(seed ^ dag_id).next()
 
 
+def dag_target_nodes(dag_id: int, seed: int = SEED) -> int:
+    """The node count DAG ``dag_id`` is generated with (its first draw):
+    the cost estimate the corpus-axis sharding balances on, known without
+    building the DAG (mythril_amd.shard.lpt_assign)."""
+    return 64 + SplitMix64(dag_seed(seed, dag_id)).below(449)
+
+
 def make_dag(dag_id: int, seed: int = SEED, n_nodes: int = 0) -> Tuple[List[N.Node], int]:
     """Return (constraints, source node count) for DAG ``dag_id``."""
     rng = SplitMix64(dag_seed(seed, dag_id))

@@ -591,9 +591,15 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         return u[p] if p < len(u) else 1 << 60
 
     def free_to_drop(v: LNode) -> bool:
-        """Evicting v needs no spill: constants and leaves are
-        rematerialised, a spilled value still has its slot."""
-        return v.op in (I.CONST, I.LEAF) or v.id in lds_of
+        """Evicting v needs no spill: constants are rematerialised, a spilled
+        value still has its slot."""
+        return v.op == I.CONST or v.id in lds_of
+
+    def droppable_when_full(v: LNode) -> bool:
+        """With every spill slot taken a leaf is evicted without a spill
+        too: it is regenerated (or reloaded from the input) at its next use —
+        more VALU than a reload, so only then."""
+        return free_to_drop(v) or v.op == I.LEAF
 
     def alloc_reg(i: int, protect: set, oldest: bool = False) -> int:
         nonlocal n_lds, n_spill
@@ -615,7 +621,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
             # none (a leaf is regenerated / reloaded from the input instead)
             victim, far = None, -1
             for r, v in holder.items():
-                if v.id in protect or not free_to_drop(v):
+                if v.id in protect or not droppable_when_full(v):
                     continue
                 nu = next_use(v, i)
                 if nu > far:
@@ -624,7 +630,8 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
                 raise Unsupported("spill budget exceeded")
         r = reg_of.pop(victim.id)
         del holder[r]
-        if not free_to_drop(victim):
+        slots_left = bool(free_lds) or n_lds < MAX_SPILL
+        if not free_to_drop(victim) and slots_left:
             if free_lds:
                 s = free_lds.pop()
             else:

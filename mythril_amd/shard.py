@@ -1,14 +1,22 @@
 """Multi-GPU sharding of the witness search.
 
-One process per GPU.  The units — (DAG, candidate index) pairs — are
-independent, so the candidate space is partitioned with no data-path
-collective: at step ``s`` rank ``r`` of ``world`` evaluates the candidate
-indices ``[(s*world + r) * n, (s*world + r + 1) * n)`` of every DAG's
-counter-based stream (the device generator regenerates any candidate from
-its index, so witnesses are never gathered).  The single exchange step is
-the per-DAG first satisfying index, reduced with MIN across ranks
-(``torch.distributed`` all-reduce: RCCL over xGMI on GPUs, gloo on CPU).
-``NONE`` (INT64_MAX) means "no witness".
+The units — (DAG, candidate index) pairs — are independent, so both axes
+shard with no data-path collective:
+
+* **assignment axis** (one process per GPU; ``bench.py`` default): at step
+  ``s`` rank ``r`` of ``world`` evaluates the candidate indices
+  ``[(s*world + r) * n, (s*world + r + 1) * n)`` of every DAG's counter-based
+  stream (the device generator regenerates any candidate from its index, so
+  witnesses are never gathered).  The single exchange step is the per-DAG
+  first satisfying index, reduced with MIN across ranks
+  (``torch.distributed`` all-reduce: RCCL over xGMI on GPUs, gloo on CPU).
+  ``NONE`` (INT64_MAX) means "no witness".
+* **corpus axis** (config C5; ``bench.py --shard corpus``, and
+  ``model.batch_is_possible`` over several devices of one process): whole
+  DAGs are assigned to ranks / devices by longest-processing-time first on
+  an estimated cost (:func:`lpt_assign`), each evaluates its DAGs' full
+  candidate range, and nothing is exchanged at all (a DAG's first witness
+  is found on the one device that owns it).
 
 The reference has no distributed code at all (Mythril is
 single-process); this axis is the one the engine creates.
@@ -44,7 +52,9 @@ def reduce_first_sat(first_sat, group=None) -> None:
 
 def lpt_assign(costs: List[float], world: int) -> List[List[int]]:
     """Corpus axis (config C5): longest-processing-time-first assignment of
-    DAGs (estimated cost = weight x candidates) to ``world`` ranks."""
+    DAGs (estimated cost = weight x candidates) to ``world`` ranks; each
+    rank's list is sorted, the lists partition ``range(len(costs))``, and the
+    heaviest rank carries at most the lightest rank's load plus one DAG."""
     import heapq
     if world <= 0:
         raise ValueError("world must be positive")
@@ -57,3 +67,10 @@ def lpt_assign(costs: List[float], world: int) -> List[List[int]]:
     for lst in out:
         lst.sort()
     return out
+
+
+def corpus_shard(costs: List[float], rank: int, world: int) -> List[int]:
+    """The DAG indices rank ``rank`` owns on the corpus axis."""
+    if not (0 <= rank < world):
+        raise ValueError("bad rank %d of %d" % (rank, world))
+    return lpt_assign(costs, world)[rank]

@@ -106,3 +106,80 @@ def test_gloo_world2_first_sat_matches_single_process():
         want = [_local_first(d, r, lo, world * N_ASSIGN) for d, r in enumerate(dags)]
         assert out[0][step] == want
     assert out[0][0][0] != shard.NONE            # the easy DAG is found in every step
+
+
+# ---- corpus axis (C5) and bench.py's world > 1 timed loop -----------------
+
+def test_corpus_shard_partitions_and_balances():
+    from mythril_amd.corpus import dag_target_nodes, make_dag
+    import bench
+    for world in (2, 3, 8):
+        parts = [bench.my_dags("corpus", 64, r, world) for r in range(world)]
+        assert sorted(i for p in parts for i in p) == list(range(64 * world))
+        costs = [dag_target_nodes(d) for d in range(64 * world)]
+        loads = [sum(costs[i] for i in p) for p in parts]
+        assert max(loads) - min(loads) <= max(costs)
+    assert bench.my_dags("assign", 16, 1, 4) == list(range(16))
+    for d in (0, 5, 77):                               # the estimate is the DAG's own draw
+        roots, n = make_dag(d)
+        assert n >= dag_target_nodes(d) and n <= dag_target_nodes(d) + 8
+    # corpus axis: every rank scans the same candidate range of its own DAGs
+    assert bench.step_first("corpus", 3, 1, 4, 1 << 20) == 3 << 20
+    assert bench.step_first("assign", 3, 1, 4, 1 << 20) == (3 * 4 + 1) << 20
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's own timed loop and reductions at world 2 over gloo, with the
+    engine launch replaced by the C oracle on this rank's shard (CPU)."""
+    import time
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dags = _dags()
+        firsts = {}
+        first_sat = torch.full((len(dags),), shard.NONE, dtype=torch.int64)
+
+        def step(i, k):
+            first_sat.fill_(shard.NONE)
+            first = bench.step_first("assign", i, rank, world, N_ASSIGN)
+            first_sat.copy_(torch.tensor([_local_first(d, r, first, N_ASSIGN)
+                                          for d, r in enumerate(dags)], dtype=torch.int64))
+            if rank == 1:
+                time.sleep(0.2)                       # the slow rank sets the clock
+            shard.reduce_first_sat(first_sat)
+            firsts[i] = first_sat.tolist()
+
+        elapsed = bench.timed_run(step, lambda: None, steps=2, warmup=1, world=world)
+        nodes, sat = bench.all_sum([10.0 + rank, float(rank)], world)
+        q.put((rank, elapsed, firsts, nodes, sat))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_timed_loop_world2_gloo():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: (e, f, n, s) for r, e, f, n, s in (q.get(timeout=240) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # elapsed is the max over ranks (the slow rank's two timed steps), on both
+    assert out[0][0] == out[1][0] >= 0.4
+    # warmup step 0 and timed steps 1, 2: reduced first witnesses equal a
+    # single-process sweep over both ranks' ranges
+    dags = _dags()
+    for i in range(3):
+        lo = i * world * N_ASSIGN
+        want = [_local_first(d, r, lo, world * N_ASSIGN) for d, r in enumerate(dags)]
+        assert out[0][1][i] == out[1][1][i] == want
+    assert out[0][2] == out[1][2] == 21.0 and out[0][3] == out[1][3] == 1.0
