@@ -151,6 +151,33 @@ SEARCH_BUDGET_MS = 200
 # used to size a search so it fits its time budget (one device launch
 # sequence cannot be interrupted)
 INS_CAND_PER_S = 3.0e11
+# devices the batched search spreads programs over (corpus axis)
+DEVICES = [0]
+GPU_ENABLED = True
+
+
+def configure_from_env(env=None) -> None:
+    """Pre-filter configuration from the environment:
+    ``MYTHRIL_GPU=0`` turns the GPU path off (every query goes to z3),
+    ``MYTHRIL_GPU_DEVICES=0,1,...`` the devices batched searches use,
+    ``MYTHRIL_GPU_CANDIDATES`` the candidates per query (a power of two),
+    ``MYTHRIL_GPU_BUDGET_MS`` the share of a query's timeout the search may
+    take."""
+    global GPU_ENABLED, DEVICES, SEARCH_CANDIDATES, SEARCH_BUDGET_MS
+    import os
+    env = os.environ if env is None else env
+    GPU_ENABLED = env.get("MYTHRIL_GPU", "1").strip().lower() not in ("0", "off", "false", "no")
+    devs = env.get("MYTHRIL_GPU_DEVICES", "").strip()
+    if devs:
+        DEVICES = [int(d) for d in devs.split(",") if d.strip()]
+    if env.get("MYTHRIL_GPU_CANDIDATES"):
+        n = max(1, int(env["MYTHRIL_GPU_CANDIDATES"]))
+        SEARCH_CANDIDATES = 1 << (n.bit_length() - 1)
+    if env.get("MYTHRIL_GPU_BUDGET_MS"):
+        SEARCH_BUDGET_MS = max(0.0, float(env["MYTHRIL_GPU_BUDGET_MS"]))
+
+
+configure_from_env()
 
 
 class Model:
@@ -317,6 +344,45 @@ def _n_cand(progs: Sequence[Program], budget_ms: float) -> int:
     return 1 << (n.bit_length() - 1)
 
 
+def batch_search_devices(progs: Sequence[Program], n_cand: int):
+    """``Engine.batch_search`` over ``DEVICES``: programs are spread over the
+    devices by longest-processing-time first on their instruction counts
+    (the corpus axis, mythril_amd/shard.py), each device searches its share
+    in its own host thread (the C ABI releases the GIL; one context per
+    device), and the results come back in program order."""
+    from .shard import lpt_assign
+    devices = list(DEVICES) or [0]
+    if len(devices) == 1 or len(progs) < 2:
+        eng = get_engine(devices[0])
+        with _Phase("load"):
+            loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
+        with _Phase("search"):
+            return eng.batch_search(loaded, SEARCH_SEED, n_cand)
+    parts = lpt_assign([float(p.n_ins) for p in progs], len(devices))
+    out: List = [None] * len(progs)
+    errors: List[BaseException] = []
+
+    def run(dev, idx):
+        try:
+            eng = get_engine(dev)
+            loaded = [eng.load(progs[i], search_leafgen(progs[i]), prog_seed=0) for i in idx]
+            for i, h in zip(idx, eng.batch_search(loaded, SEARCH_SEED, n_cand)):
+                out[i] = h
+        except BaseException as e:  # noqa: BLE001 - re-raised in the caller
+            errors.append(e)
+    import threading
+    with _Phase("search"):
+        threads = [threading.Thread(target=run, args=(d, idx)) for d, idx in zip(devices, parts)
+                   if idx]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    if errors:
+        raise errors[0]
+    return out
+
+
 def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     """(assignment, programs) of a satisfying candidate, or None.  Queries
     that split into independent groups (dependence_buckets) search every
@@ -457,7 +523,7 @@ def _prefilter(key, constraints, timeout: int, deadline: float):
     global _engine_failed
     hit = _take(_batch_witness, key)
     if hit is None:
-        if _take(_gpu_missed, key) or _engine_failed is not None:
+        if _take(_gpu_missed, key) or _engine_failed is not None or not GPU_ENABLED:
             return None
         with _Phase("flatten"):
             nodes = _raw_nodes(constraints)
@@ -529,7 +595,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
     if enforce_execution_time:
         timeout = min(timeout, time_handler.time_remaining() - 500)
     pending = []                          # (set, bucket programs)
-    if timeout > 0 and _engine_failed is None:
+    if timeout > 0 and _engine_failed is None and GPU_ENABLED:
         for cs in sets:
             if any(type(c) == bool and not c for c in cs):
                 continue                                   # get_model raises UnsatError
@@ -550,13 +616,9 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
     if pending:
         try:
             t0 = time.perf_counter()
-            eng = get_engine()
             flat = [p for _, progs in pending for p in progs]
             n_cand = _n_cand(flat, min(timeout, SEARCH_BUDGET_MS))
-            with _Phase("load"):
-                loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in flat]
-            with _Phase("search"):
-                hits = iter(eng.batch_search(loaded, SEARCH_SEED, n_cand))
+            hits = iter(batch_search_devices(flat, n_cand))
             stats.gpu_time += time.perf_counter() - t0
             for cs, progs in pending:
                 found = [next(hits) for _ in progs]
@@ -619,6 +681,7 @@ def install() -> None:
     ``Model`` class and its ``SolverStatistics``."""
     import importlib
     global args, time_handler, _stock_optimize, _stock_model
+    configure_from_env()
     args = importlib.import_module("mythril.support.support_args").args
     time_handler = importlib.import_module("mythril.laser.ethereum.time_handler").time_handler
     smt = importlib.import_module("mythril.laser.smt")

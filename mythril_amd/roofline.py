@@ -19,13 +19,23 @@ A w-bit op scales by ceil(w/32)/8 (a 256-bit op is the unit).  Leaves
 (variables, numerals, free and constant arrays) are not nodes; store nodes
 are nodes of weight 0 (they are priced inside the selects that read them).
 
-Peak: MEASURED int32 VALU issue rate on MI355X (``tools/ubench.hip``,
-``profiles/r01/ubench.log``): independent ``v_add_u32`` (and equally
-``v_addc_co_u32`` / ``v_mad_u64_u32``) issue at 4.10 cycles per wave64
-instruction per SIMD at 8 waves/SIMD -> 256 CU x 4 SIMD x 64 lanes / 4.10 cyc
-x 2.4 GHz = 38.4 T int32 lane-ops/s.  (The 157.3 TFLOPS FP32 vector spec
-counts 2-cycle packed FP32 issue; plain int32 VALU does not reach it: the
-nominal int32 rate is 39.3 T at 4 cycles)
+Peak: the SIMD's int32 VALU issue capacity, MEASURED per SIMD
+(``tools/valu_rate.hip``, ``profiles/r02/valu_rate.log``: every wave stamps
+s_memtime and its HW_ID, and each SIMD's instructions are divided by the span
+its waves covered, so co-residency is observed, not assumed).  Plain 32-bit
+VALU (v_add_u32, v_xor_b32, v_add_f32) issues at 2.02 SIMD cycles per wave64
+instruction with 8 waves per SIMD — MI355X_MICROARCH.md's "a wave64 VALU
+instruction issues over 2 cycles" holds for int32 — while one wave alone
+issues every 4.04 cycles (2.67 at 3 waves per SIMD, the interpreter's
+occupancy).  64-bit-operand instructions (v_pk_mov_b32, v_mad_u64_u32,
+v_pk_fma_f32) and carry chains (v_add_co / v_addc_co, carry through VCC) issue
+at 4.0-4.1 cycles per SIMD at any occupancy.  The ceiling for int32 work is
+therefore 256 CU x 4 SIMD x 64 lanes / 2.02 cycles x 2.4 GHz = 77.9 T
+int32 lane-ops/s.  (Round 1 used a single wave's 4-cycle cadence, 38.4 T, as
+the peak, which double-counted the fraction.)  A 256-bit ADD priced 8 ops is
+8 carry-chain instructions at half rate, so the weighted-op definition above
+cannot reach this ceiling for an add-heavy mix; it is the honest upper bound
+for the int32 ops the weights count.
 """
 
 from __future__ import annotations
@@ -34,7 +44,7 @@ from typing import Dict, Iterable, Tuple
 
 from .smt.node import Node, topo_order
 
-VALU_PEAK_OPS = 256 * 4 * 64 / 4.098 * 2.4e9  # measured int32 lane-ops/s (38.4 T)
+VALU_PEAK_OPS = 256 * 4 * 64 / 2.019 * 2.4e9  # measured int32 SIMD issue capacity (77.9 T)
 HBM_PEAK_BPS = 8.0e12
 
 _W8 = {"bvadd", "bvsub", "bvneg", "bvand", "bvor", "bvxor", "bvnot", "=", "distinct",

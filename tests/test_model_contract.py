@@ -113,7 +113,7 @@ class FakeEngine:
 @pytest.fixture
 def batch_env(monkeypatch, fresh):
     eng = FakeEngine()
-    monkeypatch.setattr(M, "get_engine", lambda: eng)
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: eng)
     z3_calls = []
 
     def fake_z3(constraints, minimize, maximize, timeout):
@@ -200,7 +200,7 @@ def test_bucketed_witness_joins_group_assignments(monkeypatch, fresh):
                 w[0, 0] = 9 if p.leaves[0].name == "x" else 4
                 out.append((3, w))
             return out
-    monkeypatch.setattr(M, "get_engine", lambda: Eng())
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: Eng())
     a, progs = REAL_GPU_SEARCH(nodes, 200)
     assert Eng.calls == 1 and len(progs) == 2
     assert a.vars == {"x": 9, "y": 4}
@@ -312,3 +312,58 @@ def test_model_getitem_follows_reference_semantics():
     assert M.Model([Z3Model({}, 0), Z3Model({"b": 2}, 3)])[1] is None   # earlier one skipped
     w = M.Model(None, Assignment(vars={"x": 7}))
     assert w["x"] == 7 and w["y"] is None
+
+
+def test_env_configuration():
+    saved = (M.GPU_ENABLED, list(M.DEVICES), M.SEARCH_CANDIDATES, M.SEARCH_BUDGET_MS)
+    try:
+        M.configure_from_env({"MYTHRIL_GPU": "0", "MYTHRIL_GPU_DEVICES": "0,2,3",
+                              "MYTHRIL_GPU_CANDIDATES": "5000000", "MYTHRIL_GPU_BUDGET_MS": "50"})
+        assert M.GPU_ENABLED is False and M.DEVICES == [0, 2, 3]
+        assert M.SEARCH_CANDIDATES == 1 << 22 and M.SEARCH_BUDGET_MS == 50.0
+        M.configure_from_env({})
+        assert M.GPU_ENABLED is True
+    finally:
+        M.GPU_ENABLED, M.DEVICES, M.SEARCH_CANDIDATES, M.SEARCH_BUDGET_MS = saved
+
+
+def test_gpu_disabled_goes_straight_to_z3(monkeypatch, fresh, reset_engine_memo):
+    monkeypatch.setattr(M, "GPU_ENABLED", False)
+    with pytest.raises(M.SolverUnavailable):
+        M.get_model((c_sat(),))
+    assert fresh == []
+
+
+def test_batch_search_spreads_programs_over_devices(monkeypatch):
+    """Corpus axis inside one process: LPT over instruction counts, one
+    engine (context) per device, results back in program order."""
+    import numpy as np
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.smt import node as N
+
+    class DevEngine:
+        def __init__(self, dev):
+            self.dev, self.seen = dev, []
+
+        def load(self, prog, leafgen, prog_seed=0):
+            return prog
+
+        def batch_search(self, loaded, seed, n_cand, first_index=0):
+            self.seen.extend(loaded)
+            return [(self.dev * 1000 + p.n_ins, np.zeros((len(p.leaves), 8), np.uint32))
+                    for p in loaded]
+    engines = {d: DevEngine(d) for d in (0, 1, 2)}
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "DEVICES", [0, 1, 2])
+    x = N.bv_var("x", 256)
+    progs = [compile_constraints([N.bv_cmp("bvult", N.bv_op("bvmul", *([x] * (k + 2))), x)])
+             for k in range(7)]
+    hits = M.batch_search_devices(progs, 1 << 16)
+    assert len(hits) == len(progs)
+    owner = {}
+    for d, e in engines.items():
+        for p in e.seen:
+            owner[id(p)] = d
+    assert sorted(len(e.seen) for e in engines.values()) != [0, 0, 7]
+    for p, (idx, _) in zip(progs, hits):
+        assert idx == owner[id(p)] * 1000 + p.n_ins       # each program answered by its device
