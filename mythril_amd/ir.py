@@ -42,6 +42,13 @@ from .smt.node import Node, topo_order
 
 CHUNK = 256
 MAX_SPILL = I.MAX_LDS + I.MAX_PSLOTS   # LDS tier first, then per-lane scratch
+LDS_TIER = 6           # spill slots the assembly kernel keeps in LDS (mg_api.cpp)
+# Leaf eviction policy: "spill" (a leaf is spilled like any value), "scratch"
+# (a leaf that would need a per-lane scratch slot is regenerated at its next
+# use instead), "always" (leaves are never spilled).  Regeneration costs the
+# generator's VALU; a scratch spill costs HBM traffic.
+import os as _os
+LEAF_REMAT = _os.environ.get("MYTHRIL_GPU_LEAF_REMAT", "spill")
 
 
 class Unsupported(Exception):
@@ -565,7 +572,8 @@ _INPLACE = {I.ADD, I.SUB, I.AND, I.OR, I.XOR, I.NOT, I.NEG, I.ITE}
 
 
 def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = frozenset(),
-              nreg: int = I.NREG):
+              nreg: int = I.NREG, leaf_remat: Optional[str] = None):
+    leaf_remat = leaf_remat or LEAF_REMAT
     trash = nreg - 1
     uses: Dict[int, List[int]] = {}
     for i, n in enumerate(order):
@@ -631,9 +639,16 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         r = reg_of.pop(victim.id)
         del holder[r]
         slots_left = bool(free_lds) or n_lds < MAX_SPILL
+        if victim.op == I.LEAF and victim.id not in lds_of and leaf_remat != "spill":
+            lds_free = (free_lds and min(free_lds) < LDS_TIER) or n_lds < LDS_TIER
+            if leaf_remat == "always" or not lds_free:
+                slots_left = False                       # regenerated at its next use
         if not free_to_drop(victim) and slots_left:
             if free_lds:
-                s = free_lds.pop()
+                # the lowest free slot: slots below the kernel's LDS tier
+                # live in LDS, the rest in per-lane scratch (HBM traffic)
+                s = min(free_lds)
+                free_lds.remove(s)
             else:
                 s = n_lds
                 n_lds += 1
