@@ -583,7 +583,9 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
     reg_of: Dict[int, int] = {}
     lds_of: Dict[int, int] = {}
     holder: Dict[int, LNode] = {}          # reg -> value
-    free_regs = list(range(nreg - 1))[::-1]
+    # every slot holds values: results nobody reads (fused ROOT conjuncts)
+    # are written to a free slot rather than to a dedicated sink slot
+    free_regs = list(range(nreg))[::-1]
     reg_clean: Dict[int, bool] = {}        # register's last value had <= 32 bits
     free_lds: List[int] = []
     n_lds = 0
@@ -640,8 +642,11 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
         del holder[r]
         slots_left = bool(free_lds) or n_lds < MAX_SPILL
         if victim.op == I.LEAF and victim.id not in lds_of and leaf_remat != "spill":
-            lds_free = (free_lds and min(free_lds) < LDS_TIER) or n_lds < LDS_TIER
-            if leaf_remat == "always" or not lds_free:
+            # "scratch": only LDS-tier slots; "scratchK": also the first K
+            # scratch slots (a footprint the XCD's L2 still holds)
+            tier = LDS_TIER + (int(leaf_remat[7:]) if leaf_remat[7:].isdigit() else 0)
+            cheap_free = (free_lds and min(free_lds) < tier) or n_lds < tier
+            if leaf_remat == "always" or not cheap_free:
                 slots_left = False                       # regenerated at its next use
         if not free_to_drop(victim) and slots_left:
             if free_lds:
@@ -694,7 +699,12 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
             continue
         flags = I.ROOT_FLAG if n.id in fused else 0
         if not uses.get(n.id):
-            d = trash
+            if free_regs:
+                d = free_regs[-1]            # stays free: the value is dead at once
+            else:
+                d = alloc_reg(i, set())
+                free_regs.append(d)
+            reg_clean[d] = n.width <= 32
         else:
             d = None
             # in place: reuse a dying operand's register (the engine then

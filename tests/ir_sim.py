@@ -101,5 +101,6 @@ def run(program, leaf_vals):
             raise AssertionError("op %d" % op)
         if w0 & I.ROOT_FLAG:
             root &= r & 1
-        regs[d] = r
+        if op not in (I.SPILL, I.OUT, I.ROOT, I.NOP):   # these write no slot (mg_host.cpp)
+            regs[d] = r
     return root, [probes.get(i, 0) for i in range(program.n_probes)]
