@@ -86,14 +86,24 @@ def pack(program: Program, assignments: Sequence[Assignment]) -> np.ndarray:
     return out
 
 
-def unpack(program: Program, leaves: np.ndarray) -> Assignment:
-    """Inverse of :func:`pack` for one candidate: leaves is (n_leaves, 8)."""
-    vals = []
-    for i in range(len(program.leaves)):
-        v = 0
-        for j in reversed(range(8)):
-            v = (v << 32) | int(leaves[i, j])
-        vals.append(v)
+def _limbs_int(row) -> int:
+    v = 0
+    for j in reversed(range(8)):
+        v = (v << 32) | int(row[j])
+    return v
+
+
+def unpack(program: Program, leaves: np.ndarray, probes: np.ndarray = None) -> Assignment:
+    """Inverse of :func:`pack` for one candidate: leaves is (n_leaves, 8).  A
+    solve-mode program (``Program.solved``) also needs the candidate's probe
+    values ((n_probes, 8)): the leaves it defines by equalities and the keys
+    of its argument-keyed table entries are computed, not generated."""
+    vals = [_limbs_int(leaves[i]) for i in range(len(program.leaves))]
+    if program.solved:
+        if probes is None:
+            raise ValueError("a solve-mode witness needs its probe values")
+        for li, k in program.derived.items():
+            vals[li] = _limbs_int(probes[k])
     vars_: Dict[str, int] = {}
     tables: Dict[str, dict] = {}
     for leaf, v in zip(program.leaves, vals):
@@ -109,6 +119,10 @@ def unpack(program: Program, leaves: np.ndarray) -> Assignment:
             else:
                 d = t["k" if leaf.kind == "key" else "v"]
                 d[leaf.entry] = d.get(leaf.entry, 0) | part
+    for name, ents in program.entry_keys.items():
+        t = tables.setdefault(name, {"k": {}, "v": {}, "c": {}, "else": 0})
+        for e, chunks in enumerate(ents):
+            t["k"][e] = sum(_limbs_int(probes[k]) << (CHUNK * c) for c, k in enumerate(chunks))
     arrays, funcs = {}, {}
     for name, t in tables.items():
         n = program.table_sizes.get(name, 0)

@@ -206,6 +206,12 @@ class Engine:
             return -1, None
         return first.value, wit[:len(prog.leaves)]
 
+    def witness(self, lp: LoadedProgram, seed: int, index: int):
+        """Leaves and probe values of candidate ``index`` (one lane): what a
+        solve-mode program's model needs besides the generated leaves."""
+        _, probes, leaves = self.eval_gen(lp, seed, index, 1, want_probes=True, want_leaves=True)
+        return leaves[:, :, 0], (probes[:, :, 0] if probes is not None else None)
+
     def keccak256(self, msgs: Sequence[bytes]) -> List[bytes]:
         n = len(msgs)
         if n == 0:

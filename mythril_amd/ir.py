@@ -104,6 +104,18 @@ class Program:
     # per-leaf (offset, count) of its candidate pool in the device constant
     # table (consts); empty unless compiled with leaf_pools
     pool_ranges: List[Tuple[int, int]] = field(default_factory=list)
+    # solve mode: model values the program COMPUTES, reported as probe
+    # chunks after the caller's probes — leaves defined by an equality
+    # (leaf index -> probe index) and the keys of argument-keyed table
+    # entries (table -> entry -> probe index per 256-bit key chunk)
+    derived: Dict[int, int] = field(default_factory=dict)
+    entry_keys: Dict[str, List[List[int]]] = field(default_factory=dict)
+    n_user_probes: int = 0
+
+    @property
+    def solved(self) -> bool:
+        """Witnesses need the probe values too (``assign.unpack``)."""
+        return bool(self.derived or self.entry_keys)
 
     @property
     def n_ins(self) -> int:
@@ -135,6 +147,10 @@ class _Lowerer:
         self.consts_seen: set = set()
         self.birth = 0
         self.table_ckeys: Dict[str, List[int]] = {}
+        # solve mode (search): argument-keyed table entries, in lookup order
+        self.solve = False
+        self.solve_tables: set = set()
+        self.arg_entries: Dict[str, List[Tuple[List[LNode], List[LNode]]]] = {}
 
     # -- hash-consed constructors ------------------------------------------
     def mk(self, op: int, width: int, args=(), imm=None) -> LNode:
@@ -462,6 +478,25 @@ class _Lowerer:
                 kval |= k.imm << (CHUNK * i)
         if kval is not None and kval in ckeys:
             acc = cell("cval", ckeys.index(kval), vw)
+        elif self.solve and name in self.solve_tables:
+            # argument-keyed entries (Ackermann's reduction of a UF / array
+            # to one value per distinct argument): lookup j owns entry j,
+            # whose KEY is its own argument (computed, reported as a probe)
+            # and whose value is a leaf; it reads the first earlier entry
+            # with an equal argument, else its own value.  Entries in lookup
+            # order with first-match semantics are a consistent model table.
+            ents = self.arg_entries.setdefault(name, [])
+            val = cell("val", len(ents), vw)
+            acc = val
+            for k_i, v_i in reversed(ents):
+                acc = self._ite_chunks(self._chunk_eq(key, k_i, kw), v_i, acc)
+            ents.append((list(key), val))
+            self.table_sizes[name] = len(ents)
+            if kval is None:
+                for i in reversed(range(len(ckeys))):
+                    c = [self.const(ckeys[i] >> (CHUNK * k), self.chunk_width(kw, k))
+                         for k in range(self.nchunks(kw))]
+                    acc = self._ite_chunks(self._chunk_eq(key, c, kw), cell("cval", i, vw), acc)
         else:
             acc = cell("else", 0, vw)
             for e in reversed(range(entries)):
@@ -814,10 +849,12 @@ def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
 
 CKEY_CAP = 128          # constant-keyed entries per table
 CKEY_LINKS = 2048       # symbolic-key lookups x constant keys per table
+ARG_ENTRIES_CAP = 32    # solve mode: argument-keyed entries per table (links grow as n^2/2)
 
 
 def scan_const_keys(nodes: Sequence[Node], cap: int = CKEY_CAP,
-                    max_links: int = CKEY_LINKS) -> Dict[str, List[int]]:
+                    max_links: int = CKEY_LINKS,
+                    sym_counts: Optional[Dict[str, int]] = None) -> Dict[str, List[int]]:
     """The constant indices every free array / UF is read at: ``select`` over
     a store / ite chain ending in a free array, and UF applications, whose
     index is a numeral (calldata bytes at fixed offsets, ``calldata.py:219-
@@ -856,15 +893,137 @@ def scan_const_keys(nodes: Sequence[Node], cap: int = CKEY_CAP,
                 note(name, n.args[1])
         elif n.op == "apply":
             note(n.params[0], n.args[0])
-    return {k: sorted(v) for k, v in out.items()
-            if v and len(sym.get(k, ())) * len(v) <= max_links}
+    ck = {k: sorted(v) for k, v in out.items() if v and len(sym.get(k, ())) * len(v) <= max_links}
+    if sym_counts is not None:
+        sym_counts.update({k: len(v) for k, v in sym.items()})
+    return ck
+
+
+def lw_tables(constraints, probes) -> set:
+    """Names of every free array / UF the nodes read."""
+    out = set()
+    for n in topo_order(list(constraints) + list(probes)):
+        if n.op == "array":
+            out.add(n.params[0])
+        elif n.op == "apply":
+            out.add(n.params[0])
+    return out
+
+
+def _resolve(n: LNode, defs: Dict[int, LNode], lw: "_Lowerer", memo: Dict[int, LNode]) -> LNode:
+    """``n`` with every leaf defined by an equality replaced by its
+    definition (the keys of table entries may mention such leaves)."""
+    by_leaf = {}
+    stack = [(n, False)]
+    while stack:
+        x, done = stack.pop()
+        if x.id in memo:
+            continue
+        if x.op == I.LEAF:
+            memo[x.id] = defs.get(x.imm, x)
+            continue
+        if not x.args:
+            memo[x.id] = x
+            continue
+        if not done:
+            stack.append((x, True))
+            stack.extend((a, False) for a in x.args if a.id not in memo)
+            continue
+        args = tuple(memo[a.id] for a in x.args)
+        memo[x.id] = x if all(a is b for a, b in zip(args, x.args)) else lw.mk(x.op, x.width, args,
+                                                                             x.imm)
+    del by_leaf
+    return memo[n.id]
+
+
+def _conjuncts(n: LNode) -> List[LNode]:
+    """The top-level conjuncts of a lowered Bool (AND trees of width 1)."""
+    out, stack = [], [n]
+    while stack:
+        x = stack.pop()
+        if x.op == I.AND and x.width == 1:
+            stack.extend(reversed(x.args))
+        else:
+            out.append(x)
+    return out
+
+
+def _solve_equalities(lw: "_Lowerer", roots: List[LNode]):
+    """Equality substitution (search mode): a top-level conjunct
+    ``leaf = e`` whose ``e`` does not depend on the leaf defines the leaf as
+    ``e`` — every use of the leaf reads ``e`` instead and the conjunct holds
+    by construction (e.g. ``keccak256_N-1(keccak256_N(x)) = x``,
+    ``calldatasize = 64``).  Returns the rewritten roots and the map
+    leaf index -> defining LNode (its model value, reported as a probe)."""
+    repl: Dict[int, LNode] = {}
+    memo: Dict[int, LNode] = {}
+    one = lw.const(1, 1)
+
+    def sub(n: LNode) -> LNode:
+        stack = [(n, False)]
+        while stack:
+            x, done = stack.pop()
+            if x.id in memo:
+                continue
+            if x.id in repl:
+                memo[x.id] = repl[x.id]
+                continue
+            if not x.args:
+                memo[x.id] = x
+                continue
+            if not done:
+                stack.append((x, True))
+                stack.extend((a, False) for a in x.args if a.id not in memo)
+                continue
+            args = tuple(memo[a.id] for a in x.args)
+            if x.op == I.EQ and args[0] is args[1]:
+                r = one
+            elif x.op == I.AND and x.width == 1 and args[0] is one:
+                r = args[1]
+            elif x.op == I.AND and x.width == 1 and args[1] is one:
+                r = args[0]
+            elif all(a is b for a, b in zip(args, x.args)):
+                r = x
+            else:
+                r = lw.mk(x.op, x.width, args, x.imm)
+            memo[x.id] = r
+        return memo[n.id]
+
+    def depends_on(e: LNode, leaf: LNode) -> bool:
+        seen, stack = set(), [e]
+        while stack:
+            x = stack.pop()
+            if x is leaf:
+                return True
+            if x.id in seen:
+                continue
+            seen.add(x.id)
+            stack.extend(x.args)
+        return False
+
+    for r in roots:
+        for c in _conjuncts(r):
+            c = sub(c)
+            if c.op != I.EQ:
+                continue
+            p, q = c.args
+            for leaf, e in ((p, q), (q, p)):
+                if leaf.op == I.LEAF and leaf.id not in repl and not depends_on(e, leaf):
+                    repl[leaf.id] = e
+                    memo.clear()                     # later rewrites see the new definition
+                    break
+    memo.clear()
+    new_roots = [sub(r) for r in roots]
+    defs = {leaf_id: sub(e) for leaf_id, e in repl.items()}
+    by_id = {n.id: n for n in lw.table.values()}
+    return new_roots, {by_id[k].imm: v for k, v in defs.items()}
 
 
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
                         extra_consts: Sequence[int] = (), leaf_pools: bool = False,
-                        const_keys: bool = False) -> Program:
+                        const_keys: bool = False, solve: bool = False) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
     optional probe nodes (256-bit values written per assignment).  ``nreg``
     is the library's register-file size (``Engine.nreg``); ``extra_consts``
@@ -875,17 +1034,38 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
     With ``const_keys`` every free array / UF gets one constant-keyed entry
     per numeral index it is read at (``scan_const_keys``), so reads at fixed
     offsets are plain leaves instead of lookups in a small leaf-keyed table
-    (search mode: every calldata byte a query reads can differ)."""
+    (search mode: every calldata byte a query reads can differ).
+    ``solve`` (search mode) builds a program that also constructs part of
+    the model instead of guessing it: argument-keyed array / UF entries
+    (``_Lowerer._table``) and equality substitution (``_solve_equalities``);
+    the computed model values come out as probes (``Program.derived`` /
+    ``entry_keys``), so such a program is for search, not for evaluating
+    caller-supplied assignments."""
     lw = _Lowerer(table_sizes or {}, default_entries)
-    if const_keys:
-        lw.table_ckeys = scan_const_keys(list(constraints) + list(probes))
-    sinks: List[LNode] = []
+    lw.solve = solve
+    if const_keys or solve:
+        sym_counts: Dict[str, int] = {}
+        ck = scan_const_keys(list(constraints) + list(probes), sym_counts=sym_counts)
+        if const_keys:
+            lw.table_ckeys = ck
+        # tables read at a bounded number of symbolic keys get argument-keyed
+        # entries; the rest keep leaf-keyed ones (calldata at ABI offsets)
+        lw.solve_tables = {k for k in lw_tables(constraints, probes)
+                           if sym_counts.get(k, 0) <= ARG_ENTRIES_CAP} if solve else set()
+    roots: List[LNode] = []
+    births: List[int] = []
     for c in constraints:
         if not c.is_bool():
             raise Unsupported("constraint is not Bool")
-        ch = lw.lower(c)
-        lw.birth = c.id
-        sinks.append(lw.mk(I.ROOT, 1, (ch[0],), None))
+        roots.append(lw.lower(c)[0])
+        births.append(c.id)
+    derived_nodes: Dict[int, LNode] = {}
+    if solve:
+        roots, derived_nodes = _solve_equalities(lw, roots)
+    sinks: List[LNode] = []
+    for r, b in zip(roots, births):
+        lw.birth = b
+        sinks.append(lw.mk(I.ROOT, 1, (r,), None))
     probe_chunks = 0
     for p in probes:
         if p.is_array():
@@ -894,6 +1074,22 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
             lw.birth = p.id
             sinks.append(lw.mk(I.OUT, 1, (ch,), probe_chunks))
             probe_chunks += 1
+    n_user_probes = probe_chunks
+    derived: Dict[int, int] = {}
+    entry_keys: Dict[str, List[List[int]]] = {}
+    if solve:
+        def out(n: LNode) -> int:
+            nonlocal probe_chunks
+            lw.birth = 0                     # right after its operand (short live range)
+            sinks.append(lw.mk(I.OUT, 1, (n,), probe_chunks))
+            probe_chunks += 1
+            return probe_chunks - 1
+        for li, e in sorted(derived_nodes.items()):
+            derived[li] = out(e)
+        memo_e: Dict[int, LNode] = {}
+        for name, ents in lw.arg_entries.items():
+            entry_keys[name] = [[out(_resolve(k, derived_nodes, lw, memo_e)) for k in key]
+                                for key, _ in ents]
     if not sinks:
         sinks.append(lw.mk(I.ROOT, 1, (lw.const(1, 1),), None))
     # comparisons carry their operand width in imm for emission
@@ -928,5 +1124,10 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
     stats = {"lnodes": len(order), "n_ins": len(ins), "spills": n_spill, "reloads": n_reload,
              "hist": hist}
     ckeys = {k: v for k, v in lw.table_ckeys.items() if k in lw.table_kinds}
+    tsizes = dict(lw.table_sizes)
+    for name in lw.solve_tables & set(lw.table_kinds):
+        # no leaf-keyed entries: the model's entries are the argument-keyed ones
+        tsizes[name] = len(lw.arg_entries.get(name, ()))
     return Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
-                   len(constraints), lw.table_sizes, lw.table_kinds, ckeys, stats, pool_ranges)
+                   len(constraints), tsizes, lw.table_kinds, ckeys, stats, pool_ranges,
+                   derived, entry_keys, n_user_probes)

@@ -274,7 +274,18 @@ def search_leafgen(prog: Program) -> List[LeafGen]:
 
 def _compile_search(nodes: Sequence[N.Node]) -> Program:
     return compile_constraints(nodes, extra_consts=harvest_hints(nodes), leaf_pools=True,
-                               const_keys=True)
+                               const_keys=True, solve=True)
+
+
+def _witness(eng, lp, hit) -> Assignment:
+    """The model of a search hit (index, leaves): a solve-mode program also
+    reports the values it computed (probes of one re-evaluated lane)."""
+    idx, leaves = hit
+    prog = getattr(lp, "program", lp)
+    if prog.solved:
+        leaves, probes = eng.witness(lp, SEARCH_SEED, idx)
+        return unpack(prog, leaves, probes)
+    return unpack(prog, leaves)
 
 
 def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
@@ -349,7 +360,8 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
     devices by longest-processing-time first on their instruction counts
     (the corpus axis, mythril_amd/shard.py), each device searches its share
     in its own host thread (the C ABI releases the GIL; one context per
-    device), and the results come back in program order."""
+    device), and the results come back in program order as
+    (first index, witness Assignment) or (-1, None)."""
     from .shard import lpt_assign
     devices = list(DEVICES) or [0]
     if len(devices) == 1 or len(progs) < 2:
@@ -357,7 +369,9 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
         with _Phase("load"):
             loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
         with _Phase("search"):
-            return eng.batch_search(loaded, SEARCH_SEED, n_cand)
+            hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
+            return [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
+                    for lp, h in zip(loaded, hits)]
     parts = lpt_assign([float(p.n_ins) for p in progs], len(devices))
     out: List = [None] * len(progs)
     errors: List[BaseException] = []
@@ -366,8 +380,8 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
         try:
             eng = get_engine(dev)
             loaded = [eng.load(progs[i], search_leafgen(progs[i]), prog_seed=0) for i in idx]
-            for i, h in zip(idx, eng.batch_search(loaded, SEARCH_SEED, n_cand)):
-                out[i] = h
+            for i, lp, h in zip(idx, loaded, eng.batch_search(loaded, SEARCH_SEED, n_cand)):
+                out[i] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
         except BaseException as e:  # noqa: BLE001 - re-raised in the caller
             errors.append(e)
     import threading
@@ -393,19 +407,20 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     buckets = dependence_buckets(nodes)
     with _Phase("compile"):
         progs = [_compile_search(b) for b in buckets]
-    eng = get_engine()
     n_cand = _n_cand(progs, budget_ms)
-    with _Phase("load"):
-        loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
-    with _Phase("search"):
-        if len(progs) > 1:
-            hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
-        else:
-            hits = [eng.search(loaded[0], SEARCH_SEED, n_cand)]
+    if len(progs) > 1:
+        hits = batch_search_devices(progs, n_cand)
+    else:
+        eng = get_engine()
+        with _Phase("load"):
+            lp = eng.load(progs[0], search_leafgen(progs[0]), prog_seed=0)
+        with _Phase("search"):
+            h = eng.search(lp, SEARCH_SEED, n_cand)
+            hits = [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)]
     stats.gpu_candidates += sum(n_cand if i < 0 else i + 1 for i, _ in hits)
     if any(i < 0 for i, _ in hits):
         return None
-    return _merge([unpack(p, w) for p, (_, w) in zip(progs, hits)]), progs
+    return _merge([a for _, a in hits]), progs
 
 
 # Set by install(): the reference's own Optimize wrapper
@@ -627,7 +642,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
                 if any(k < 0 for k, _ in found):
                     _remember(_gpu_missed, cs, True)
                 else:
-                    a = _merge([unpack(p, w) for p, (_, w) in zip(progs, found)])
+                    a = _merge([w for _, w in found])
                     _remember(_batch_witness, cs, (a, progs))
         except EngineUnavailable as e:
             _engine_failed = str(e)

@@ -200,6 +200,17 @@ def test_bucketed_witness_joins_group_assignments(monkeypatch, fresh):
                 w[0, 0] = 9 if p.leaves[0].name == "x" else 4
                 out.append((3, w))
             return out
+
+        def witness(self, p, seed, index):
+            # solve mode defines x / y by their equalities: the program
+            # computes them (probes), as one re-evaluated lane would
+            import ir_sim
+            leaves = np.zeros((len(p.leaves), 8), np.uint32)
+            _, probes = ir_sim.run(p, [0] * len(p.leaves))
+            pr = np.zeros((len(probes), 8), np.uint32)
+            for k, v in enumerate(probes):
+                pr[k] = [(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)]
+            return leaves, pr
     monkeypatch.setattr(M, "get_engine", lambda dev=0: Eng())
     a, progs = REAL_GPU_SEARCH(nodes, 200)
     assert Eng.calls == 1 and len(progs) == 2
