@@ -237,3 +237,21 @@ def test_solve_mode_defines_keccak_inverse_and_size():
     assert R.eval_constraints([q[-2]], asg) == 1        # calldatasize == 64
     inv_eq = [c for c in q if c.op == "and"][-1].args[0]  # inv(f(x)) == x of the keccak condition
     assert R.eval_constraints([inv_eq], asg) == 1
+
+
+def test_reference_keccak_val8_sym256_case_is_satisfiable():
+    """tests/laser/keccak_tests.py:23-27 (reference) expects unsat for
+    keccak(100_8) == keccak(N1_256), but under the encoding the reference's
+    keccak_function_manager builds (its concrete-hash branch compares the
+    8-bit key with N1 zero-padded, keccak_function_manager.py:146-148 and
+    bitvec.py:16-22) the query has a model; the oracle checks it here."""
+    from mythril_amd.smt import And, symbol_factory
+    km = W.KeccakFunctionManager(ref_keccak)
+    o1, c1 = km.create_keccak(symbol_factory.BitVecVal(100, 8))
+    o2, c2 = km.create_keccak(symbol_factory.BitVecSym("N1", 256))
+    q = [And(c1, c2).raw, (o1 == o2).raw]
+    h = int.from_bytes(ref_keccak(bytes([100])), "big")
+    asg = R.Assignment(vars={"N1": 100},
+                       funcs={"keccak256_256": ([(100, h)], 0), "keccak256_256-1": ([(h, 100)], 0),
+                              "keccak256_8": ([(100, h)], 0), "keccak256_8-1": ([(h, 100)], 0)})
+    assert R.eval_constraints(q, asg) == 1
