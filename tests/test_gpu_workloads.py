@@ -122,16 +122,14 @@ def test_workload_batch_entry_point(engine, name):
 def test_workload_search_is_sound(engine, name):
     """Batched witness search over the shape's queries (the drop-in path of
     ``batch_is_possible``): every witness satisfies the query in the oracle."""
-    from mythril_amd.model import SEARCH_SEED, _compile_search
+    from mythril_amd.model import _compile_search, batch_search_devices
     qs = distinct_queries(name)
     progs = [_compile_search(q) for q in qs]
-    loaded = [engine.load(p, search_leafgen(p), prog_seed=0) for p in progs]
-    hits = engine.batch_search(loaded, SEARCH_SEED, 1 << 20)
+    hits = batch_search_devices(progs, 1 << 20)     # witnesses incl. computed values
     n_hit = 0
-    for q, p, (idx, wit) in zip(qs, progs, hits):
+    for q, p, (idx, a) in zip(qs, progs, hits):
         if idx < 0:
             continue
-        a = unpack(p, wit)
         assert R.eval_constraints(q, R.Assignment(a.vars, a.arrays, a.funcs)) == 1, name
         n_hit += 1
     print("%s: %d/%d queries with a GPU witness" % (name, n_hit, len(qs)))
