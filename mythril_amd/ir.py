@@ -727,7 +727,7 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
                 reg_of[a.id] = r
                 holder[r] = a
         slots = [reg_of[a.id] for a in n.args]
-        for a in set(n.args):
+        for a in dict.fromkeys(n.args):        # ordered: compiles are reproducible
             release(a, i)
         if n.op in (I.ROOT, I.OUT):
             ins.append((n.op, 1, trash, slots[0], 0, 0, n.imm or 0))
