@@ -273,8 +273,17 @@ def search_leafgen(prog: Program) -> List[LeafGen]:
 
 
 def _compile_search(nodes: Sequence[N.Node]) -> Program:
-    return compile_constraints(nodes, extra_consts=harvest_hints(nodes), leaf_pools=True,
-                               const_keys=True, solve=True)
+    """Search program: solve mode (part of the model constructed), or — when
+    its argument-keyed entries keep too many values live for the spill
+    budget — the plain search form (every model value generated)."""
+    hints = harvest_hints(nodes)
+    try:
+        return compile_constraints(nodes, extra_consts=hints, leaf_pools=True, const_keys=True,
+                                   solve=True)
+    except Unsupported as e:
+        if "spill budget" not in str(e):
+            raise
+        return compile_constraints(nodes, extra_consts=hints, leaf_pools=True, const_keys=True)
 
 
 def _witness(eng, lp, hit) -> Assignment:
