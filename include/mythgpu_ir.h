@@ -44,7 +44,7 @@
                                 (6 x 8 KiB per 256-lane block, 3 blocks per
                                 CU) and the rest in per-lane scratch         */
 #ifndef MG_MAX_PSLOTS        /* (A/B builds may override)                    */
-#define MG_MAX_PSLOTS 112    /* further spill slots in per-lane scratch      */
+#define MG_MAX_PSLOTS 240    /* further spill slots in per-lane scratch      */
 #endif
 
 enum mg_op {

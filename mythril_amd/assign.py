@@ -58,6 +58,8 @@ def leaf_values(program: Program, asg: Assignment) -> List[int]:
     for leaf in program.leaves:
         if leaf.kind == "var":
             v = asg.vars.get(leaf.source, 0)
+        elif leaf.kind == "aux":          # search-mode selector: not part of a model
+            v = 0
         else:
             tab = asg.table(leaf.source)
             if leaf.kind == "cval":
@@ -108,6 +110,8 @@ def unpack(program: Program, leaves: np.ndarray, probes: np.ndarray = None) -> A
     tables: Dict[str, dict] = {}
     for leaf, v in zip(program.leaves, vals):
         part = v << (CHUNK * leaf.chunk)
+        if leaf.kind == "aux":
+            continue
         if leaf.kind == "var":
             vars_[leaf.source] = vars_.get(leaf.source, 0) | part
         else:

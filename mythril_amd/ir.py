@@ -73,7 +73,8 @@ class LNode:
 
 @dataclass
 class Leaf:
-    """One input slot of an assignment.  ``kind``: var | key | val | else;
+    """One input slot of an assignment.  ``kind``: var | key | val | else |
+    cval | aux (a search-mode selector, ``solve.py``, not part of a model);
     ``source`` is the variable / array / function name, ``chunk`` the 256-bit
     chunk of a wide value, ``entry`` the table entry index."""
     name: str
@@ -913,7 +914,6 @@ def lw_tables(constraints, probes) -> set:
 def _resolve(n: LNode, defs: Dict[int, LNode], lw: "_Lowerer", memo: Dict[int, LNode]) -> LNode:
     """``n`` with every leaf defined by an equality replaced by its
     definition (the keys of table entries may mention such leaves)."""
-    by_leaf = {}
     stack = [(n, False)]
     while stack:
         x, done = stack.pop()
@@ -932,7 +932,6 @@ def _resolve(n: LNode, defs: Dict[int, LNode], lw: "_Lowerer", memo: Dict[int, L
         args = tuple(memo[a.id] for a in x.args)
         memo[x.id] = x if all(a is b for a, b in zip(args, x.args)) else lw.mk(x.op, x.width, args,
                                                                              x.imm)
-    del by_leaf
     return memo[n.id]
 
 
@@ -946,77 +945,6 @@ def _conjuncts(n: LNode) -> List[LNode]:
         else:
             out.append(x)
     return out
-
-
-def _solve_equalities(lw: "_Lowerer", roots: List[LNode]):
-    """Equality substitution (search mode): a top-level conjunct
-    ``leaf = e`` whose ``e`` does not depend on the leaf defines the leaf as
-    ``e`` — every use of the leaf reads ``e`` instead and the conjunct holds
-    by construction (e.g. ``keccak256_N-1(keccak256_N(x)) = x``,
-    ``calldatasize = 64``).  Returns the rewritten roots and the map
-    leaf index -> defining LNode (its model value, reported as a probe)."""
-    repl: Dict[int, LNode] = {}
-    memo: Dict[int, LNode] = {}
-    one = lw.const(1, 1)
-
-    def sub(n: LNode) -> LNode:
-        stack = [(n, False)]
-        while stack:
-            x, done = stack.pop()
-            if x.id in memo:
-                continue
-            if x.id in repl:
-                memo[x.id] = repl[x.id]
-                continue
-            if not x.args:
-                memo[x.id] = x
-                continue
-            if not done:
-                stack.append((x, True))
-                stack.extend((a, False) for a in x.args if a.id not in memo)
-                continue
-            args = tuple(memo[a.id] for a in x.args)
-            if x.op == I.EQ and args[0] is args[1]:
-                r = one
-            elif x.op == I.AND and x.width == 1 and args[0] is one:
-                r = args[1]
-            elif x.op == I.AND and x.width == 1 and args[1] is one:
-                r = args[0]
-            elif all(a is b for a, b in zip(args, x.args)):
-                r = x
-            else:
-                r = lw.mk(x.op, x.width, args, x.imm)
-            memo[x.id] = r
-        return memo[n.id]
-
-    def depends_on(e: LNode, leaf: LNode) -> bool:
-        seen, stack = set(), [e]
-        while stack:
-            x = stack.pop()
-            if x is leaf:
-                return True
-            if x.id in seen:
-                continue
-            seen.add(x.id)
-            stack.extend(x.args)
-        return False
-
-    for r in roots:
-        for c in _conjuncts(r):
-            c = sub(c)
-            if c.op != I.EQ:
-                continue
-            p, q = c.args
-            for leaf, e in ((p, q), (q, p)):
-                if leaf.op == I.LEAF and leaf.id not in repl and not depends_on(e, leaf):
-                    repl[leaf.id] = e
-                    memo.clear()                     # later rewrites see the new definition
-                    break
-    memo.clear()
-    new_roots = [sub(r) for r in roots]
-    defs = {leaf_id: sub(e) for leaf_id, e in repl.items()}
-    by_id = {n.id: n for n in lw.table.values()}
-    return new_roots, {by_id[k].imm: v for k, v in defs.items()}
 
 
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
@@ -1037,7 +965,7 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
     (search mode: every calldata byte a query reads can differ).
     ``solve`` (search mode) builds a program that also constructs part of
     the model instead of guessing it: argument-keyed array / UF entries
-    (``_Lowerer._table``) and equality substitution (``_solve_equalities``);
+    (``_Lowerer._table``) and model construction (``mythril_amd/solve.py``);
     the computed model values come out as probes (``Program.derived`` /
     ``entry_keys``), so such a program is for search, not for evaluating
     caller-supplied assignments."""
@@ -1060,8 +988,12 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
         roots.append(lw.lower(c)[0])
         births.append(c.id)
     derived_nodes: Dict[int, LNode] = {}
+    solver = None
     if solve:
-        roots, derived_nodes = _solve_equalities(lw, roots)
+        from .solve import Solver
+        solver = Solver(lw)
+        roots, derived_nodes = solver.run(roots)
+        probe_memo: Dict[int, LNode] = {}
     sinks: List[LNode] = []
     for r, b in zip(roots, births):
         lw.birth = b
@@ -1071,6 +1003,9 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
         if p.is_array():
             raise Unsupported("array probe")
         for ch in lw.lower(p):
+            if solver is not None:            # the probe's value under the constructed model
+                lw.birth = 0
+                ch = solver.rewrite(ch, probe_memo)
             lw.birth = p.id
             sinks.append(lw.mk(I.OUT, 1, (ch,), probe_chunks))
             probe_chunks += 1

@@ -272,18 +272,20 @@ def search_leafgen(prog: Program) -> List[LeafGen]:
     return [LeafGen(l.width, 0, n_c, 20, 40, 60) for l in prog.leaves]
 
 
-def _compile_search(nodes: Sequence[N.Node]) -> Program:
+def _compile_search(nodes: Sequence[N.Node], probes: Sequence[N.Node] = ()) -> Program:
     """Search program: solve mode (part of the model constructed), or — when
     its argument-keyed entries keep too many values live for the spill
-    budget — the plain search form (every model value generated)."""
+    budget — the plain search form (every model value generated).
+    ``probes`` are evaluated under each candidate's model."""
     hints = harvest_hints(nodes)
     try:
-        return compile_constraints(nodes, extra_consts=hints, leaf_pools=True, const_keys=True,
-                                   solve=True)
+        return compile_constraints(nodes, probes, extra_consts=hints, leaf_pools=True,
+                                   const_keys=True, solve=True)
     except Unsupported as e:
         if "spill budget" not in str(e):
             raise
-        return compile_constraints(nodes, extra_consts=hints, leaf_pools=True, const_keys=True)
+        return compile_constraints(nodes, probes, extra_consts=hints, leaf_pools=True,
+                                   const_keys=True)
 
 
 def _witness(eng, lp, hit) -> Assignment:
