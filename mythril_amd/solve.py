@@ -43,11 +43,15 @@ from typing import Dict, List, Optional
 
 from . import irdefs as I
 
-PASSES = 3
+PASSES = 6
 MAX_DOMAIN = 16          # constants in an ``or`` of equalities made a domain
 MAX_BRANCHES = 4         # disjuncts of an ``or`` split by a selector
 MAX_OR = 64              # such splits per program
+BRANCH_DEPTH = 2
 SELECTOR_WIDTH = 8
+
+
+_PREDICATES = (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO)
 
 
 def _mask(w: int) -> int:
@@ -62,6 +66,10 @@ class Solver:
         self.zero = lw.const(0, 1)
         self.n_aux = 0
         self.n_branch = 0
+        self.selectors: set = set()              # LEAF ids of branch / domain selectors
+        # LEAF id -> generation of a branch's stand-in for an undefined value
+        # (a stand-in may be split again by a later ``or``, to BRANCH_DEPTH)
+        self.depth: Dict[int, int] = {}
         self.unsat = False
 
     # -- rewriting -------------------------------------------------------------
@@ -182,6 +190,10 @@ class Solver:
         if b.op != I.CONST:
             return None
         k = b.imm
+        if a.op in _PREDICATES or (a.op in (I.AND, I.OR, I.NOT) and a.width == 1):
+            if k > 1:
+                return [self.zero]
+            return [a] if k else [self._not(a)]
         if a.op == I.ITE:
             c, p, q = a.args
             if p.op == I.CONST and q.op == I.CONST:
@@ -240,7 +252,11 @@ class Solver:
         a, b = y.args
         if a.op == I.CONST and b.op != I.CONST:
             a, b = b, a
-        if b.op != I.CONST or a.op != I.ITE:
+        if b.op != I.CONST:
+            return None
+        if a.op in _PREDICATES or (a.op in (I.AND, I.OR, I.NOT) and a.width == 1):
+            return self.one if b.imm > 1 else (a if b.imm == 0 else self._not(a))
+        if a.op != I.ITE:
             return None
         c, p, q = a.args
         if p.op != I.CONST or q.op != I.CONST:
@@ -280,12 +296,26 @@ class Solver:
                         stack.append(r)
                         continue
                 out.append(x)
+                if y.op == I.UMULNO and y.args[1].op != I.CONST:
+                    # a * b >= 2^w (BVMulNoOverflow negated): b = 2^w - 1
+                    # suffices for every a > 1
+                    b_ = y.args[1]
+                    stack.append(self.rewrite(self._eq(b_, _mask(b_.width)), memo))
                 continue
             if x.op == I.EQ:
                 parts = self._split_eq(x)
                 if parts is not None:
                     stack.extend(self.rewrite(p, memo) for p in parts)
                     continue
+            if x.op == I.ULT and x.args[0].op == I.ADD and x.args[1] in x.args[0].args:
+                # a + b < a (the carry BVAddNoOverflow tests): b = 2^w - 1
+                # overflows for every a > 0 (a sufficient condition)
+                s_, a_ = x.args[0], x.args[1]
+                other = s_.args[1] if s_.args[0] is a_ else s_.args[0]
+                out.append(x)
+                if other.op != I.CONST:
+                    stack.append(self.rewrite(self._eq(other, _mask(other.width)), memo))
+                continue
             if x.op == I.OR and x.width == 1:
                 le = self._as_ule(x)
                 if le is not None:
@@ -314,16 +344,26 @@ class Solver:
     @staticmethod
     def _bound(x):
         """``x`` as ``lo <= e <= hi`` (unsigned, inclusive) with constant
-        bounds: (e, lo, hi, operand width), or None."""
+        bounds: (e, lo, hi, operand width), or None.  A signed comparison
+        with a non-negative constant gives the non-negative half (exact for
+        ``k < e``, sufficient for ``e < k``: the calldata guards
+        ``offset < calldatasize``)."""
         neg = False
         if x.op == I.NOT and x.width == 1:
             x, neg = x.args[0], True
-        if x.op not in (I.ULT, I.ULE):
+        if x.op not in (I.ULT, I.ULE, I.SLT, I.SLE):
             return None
         a, b = x.args
         w = x.width
         top = _mask(w)
-        strict = x.op == I.ULT
+        strict = x.op in (I.ULT, I.SLT)
+        if x.op in (I.SLT, I.SLE):
+            if neg:
+                return None
+            top = _mask(w - 1)
+            k = b.imm if b.op == I.CONST else (a.imm if a.op == I.CONST else None)
+            if k is None or k > top or (a.op == I.CONST) == (b.op == I.CONST):
+                return None
         if b.op == I.CONST and a.op != I.CONST:
             k = b.imm
             # a < k | a <= k ; negated: a >= k | a > k
@@ -381,6 +421,8 @@ class Solver:
     def _try_define(self, leaf, e) -> bool:
         if leaf.op != I.LEAF or leaf.id in self.repl:
             return False
+        if leaf.id in self.selectors and e.op != I.CONST:
+            return False                         # a selector only commits to a branch
         if e.width > leaf.width and not (e.op == I.CONST and e.imm >> leaf.width == 0):
             return False
         if self._depends(e, leaf):
@@ -415,7 +457,7 @@ class Solver:
         if leaf is None or leaf.id in self.repl:
             return False
         lw = self.lw
-        sel = self._aux(SELECTOR_WIDTH)
+        sel = self._selector()
         span = 1 << SELECTOR_WIDTH
         e = lw.const(ks[-1], leaf.width)
         for i in reversed(range(len(ks) - 1)):
@@ -423,6 +465,11 @@ class Solver:
             e = lw.mk(I.ITE, leaf.width, (lw.mk(I.ULT, SELECTOR_WIDTH, (sel, t)),
                                           lw.const(ks[i], leaf.width), e))
         return self._try_define(leaf, e)
+
+    def _selector(self):
+        sel = self._aux(SELECTOR_WIDTH)
+        self.selectors.add(sel.id)
+        return sel
 
     def _aux(self, width: int):
         self.n_aux += 1
@@ -477,23 +524,22 @@ class Solver:
                         r[3], r[4] = a.width, k.imm
         n = 0
         for leaf, lo, hi, j, res in info.values():
-            if leaf.id in self.repl or lo > hi:
+            if leaf.id in self.repl or lo > hi or (not j and lo == 0 and hi == _mask(leaf.width)):
                 continue
-            if not j and (hi - lo) >> (leaf.width - 4):
-                continue                 # a wide interval: guessing works
             base = ((lo >> j) << j) | res
             if base < lo:
                 base += 1 << j
             if base > hi:
                 continue
-            room = (hi - base) >> j
-            a = min(64, room.bit_length() - 1) if room else 0
+            room = ((hi - base) >> j) + 1       # values base + t * 2^j, t < room
+            # a selector a conjunct confines commits to that branch
+            a = 0 if leaf.id in self.selectors else room.bit_length() - 1
             lw = self.lw
             e = lw.const(base, leaf.width)
             if a > 0:
                 aux = self._aux(a)
                 step = aux if not j else lw.mk(I.CONCAT, a + j, (aux, lw.const(0, j)), j)
-                e = lw.mk(I.ADD, leaf.width, (e, step))
+                e = lw.mk(I.ADD, leaf.width, (e, step)) if base else step
             n += self._try_define(leaf, e)
         return n
 
@@ -532,11 +578,14 @@ class Solver:
         self.n_branch += 1
         lw = self.lw
         by_id = {n.id: n for n in lw.table.values() if n.op == I.LEAF}
-        sel = self._aux(SELECTOR_WIDTH)
+        sel = self._selector()
         span = 1 << SELECTOR_WIDTH
         n = 0
         for k in leaves:
             leaf = by_id[k]
+            d = self.depth.get(k, 0)
+            if d >= BRANCH_DEPTH:
+                continue                         # (else every pass splits the same or)
             free = None
             arms = []
             for defs in per:
@@ -544,6 +593,7 @@ class Solver:
                 if e is None:
                     if free is None:
                         free = self._aux(leaf.width)
+                        self.depth[free.id] = d + 1
                     e = free
                 arms.append(e)
             e = arms[-1]
