@@ -810,6 +810,7 @@ def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
     under_l: Dict[int, frozenset] = {}
     under_c: Dict[int, frozenset] = {}
     pools: List[Dict[int, None]] = [dict() for _ in leaves]
+    done: List[set] = [set() for _ in leaves]         # constants already drawn from
     pv: Dict[Tuple[int, int], List[int]] = {}
     M256 = (1 << 256) - 1
     for n in order:                                   # topological
@@ -832,10 +833,16 @@ def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
                 p = pools[li]
                 if len(p) >= POOL_CAP:
                     continue
+                seen = done[li]
+                if cs <= seen:
+                    continue
                 w = leaves[li].width
                 if ordered is None:
                     ordered = sorted(cs)
                 for c in ordered:
+                    if c in seen:
+                        continue
+                    seen.add(c)
                     vals = pv.get((c, w))
                     if vals is None:
                         vals = pv[(c, w)] = [v & M256 for v in _pool_values(c, w)]

@@ -617,7 +617,7 @@ class Solver:
                 k = self._define(atoms)
                 if k:                   # later roots see the new definitions folded
                     memo = {}
-                    found += k
+                found += k
             # intervals from the bounds of all conjuncts together
             if found:
                 memo = {}
