@@ -196,9 +196,14 @@ def test_solve_mode_constructs_consistent_models(name):
     compute part of the model; under the model unpacked from leaves AND the
     computed probe values, the oracle's verdict on the ORIGINAL query equals
     the program's root bit on every candidate."""
+    from mythril_amd.ir import Unsupported
     solved = 0
     for qi, q in enumerate(W.queries(name, 24)[::3]):
-        prog = compile_constraints(q, const_keys=True, leaf_pools=True, solve=True)
+        try:
+            prog = compile_constraints(q, const_keys=True, leaf_pools=True, solve=True)
+        except Unsupported as e:       # over the spill budget: get_model searches plain
+            assert "spill budget" in str(e)
+            continue
         solved += prog.solved
         table = [sum(int(prog.consts[i, j]) << (32 * j) for j in range(8))
                  for i in range(prog.consts.shape[0])]
