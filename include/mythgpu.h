@@ -40,9 +40,10 @@ typedef struct mg_prog mg_prog;
 typedef struct mg_batch mg_batch;
 
 /* Device candidate generator for one leaf (free variable / table cell).
- * A draw picks a class by (r >> 32) % 100:
- *   < pct_uniform                    uniform random (masked to width)
- *   < pct_small                      random < 2^64
+ * A draw r0 = SplitMix64(seed ^ salt ^ index * golden) picks a class by
+ * mulhi(r0 >> 32, 100):
+ *   < pct_uniform                    r0 + three more SplitMix64 words (masked to width)
+ *   < pct_small                      r0 (< 2^64)
  *   < pct_boundary                   {0, 1, 2^(w-1), 2^w-1, 2^k+1, 2^k-1}
  *   otherwise                        consts[pool_off + e] + {-1, 0, +1}
  * (thresholds are cumulative percentages). */

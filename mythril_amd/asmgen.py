@@ -933,8 +933,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     """dst[0..7] (default X) <- generator value of leaf C for candidate
     first + lane; the boundary / pool lanes arrive by loads into dst, waited
     for unless wait=False (LEAFD: the translator places the WAITVM).
-    Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's four SplitMix64
-    words are computed for every lane (the small class is its first word);
+    Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's words (the
+    class word r0, then three SplitMix64 words) are computed for every lane
+    (the small class is r0);
     the boundary and pool classes then overwrite their lanes under exec.
     Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
     pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
@@ -961,8 +962,11 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     sm64(a, st, z, tt)
     a("s_movk_i32 %s, 100" % s(S_T))
     a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), s(S_T)))
-    # ---- uniform words for every lane; small lanes keep the first 64 bits
-    for j in range(0, 8, 2):
+    # ---- uniform words for every lane: r0 itself, then three SplitMix64
+    # words; small lanes keep the first 64 bits (r0)
+    a("v_mov_b32 %s, %s" % (v(X[0]), v(z[0])))
+    a("v_mov_b32 %s, %s" % (v(X[1]), v(z[1])))
+    for j in range(2, 8, 2):
         sm64(a, st, [X[j], X[j + 1]], tt)
     _class_mask(a, S_T + 2, g + 3, g + 4, cls)                       # small
     lab = exec_begin(a, S_T + 2, S_T + 4)

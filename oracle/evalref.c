@@ -453,7 +453,7 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
     uint32_t cls = mulhi32((uint32_t)(r0 >> 32), 100u), lo = (uint32_t)r0;
     vzero(out);
     if (cls >= pct[0] && cls < pct[1]) {
-        out->w[0] = sm64(&s);
+        out->w[0] = r0;                       /* v3: the class word itself */
     } else if (cls >= pct[1] && cls < pct[2]) {
         uint32_t kind = mulhi32(lo, 6u), k = mulhi32(lo * 0x9E3779B1u, w);
         if (kind == 1) out->w[0] = 1;
@@ -480,7 +480,8 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
         else *out = p;
         for (int i = 4; i < L; ++i) out->w[i] = 0;
     } else {
-        for (int i = 0; i < 4; ++i) out->w[i] = sm64(&s);
+        out->w[0] = r0;                       /* v3: r0, then three words */
+        for (int i = 1; i < 4; ++i) out->w[i] = sm64(&s);
     }
     vmask(out, w);
 }

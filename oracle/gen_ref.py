@@ -31,8 +31,7 @@ def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
     lo = r0 & 0xFFFFFFFF
     mask = (1 << width) - 1
     if pct[0] <= cls < pct[1]:
-        s, r = _sm64(s)
-        v = r
+        v = r0                                # v3: the class word itself
     elif pct[1] <= cls < pct[2]:
         kind = _mulhi(lo, 6)
         k = _mulhi((lo * 0x9E3779B1) & 0xFFFFFFFF, width)
@@ -43,8 +42,8 @@ def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
         delta = _mulhi((lo * 0x85EBCA6B) & 0xFFFFFFFF, 3)
         v = (pool[e] + delta - 1) % (1 << 256)
     else:
-        v = 0
-        for j in range(4):
+        v = r0                                # v3: r0, then three SplitMix64 words
+        for j in range(1, 4):
             s, r = _sm64(s)
             v |= r << (64 * j)
     return v & mask
