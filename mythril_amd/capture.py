@@ -134,7 +134,8 @@ def census(records: List[dict]) -> Dict[str, object]:
 
 def replay_gpu(records: List[dict]) -> Dict[str, object]:
     """Batched GPU search over the optimisation-free captured queries;
-    compares with the recorded outcomes."""
+    compares with the recorded outcomes.  ``witnesses`` maps a query id to
+    the joint model the GPU found (its groups' witnesses merged)."""
     from . import model as M
     from .ir import Unsupported
     sets, idx = [], []
@@ -148,8 +149,6 @@ def replay_gpu(records: List[dict]) -> Dict[str, object]:
                 continue
             sets.append(cs)
             idx.append(r["id"])
-    eng = M.get_engine()
-    from .ir import compile_constraints
     progs, owner = [], []
     for k, cs in enumerate(sets):
         try:
@@ -159,17 +158,18 @@ def replay_gpu(records: List[dict]) -> Dict[str, object]:
         except Unsupported:
             continue
     t0 = time.perf_counter()
-    loaded = [eng.load(p, M.search_leafgen(p), prog_seed=0) for p in progs]
-    hits = eng.batch_search(loaded, M.SEARCH_SEED, M.SEARCH_CANDIDATES)
+    hits = M.batch_search_devices(progs, M.SEARCH_CANDIDATES)   # (index, model) per group
     secs = time.perf_counter() - t0
     found = collections.defaultdict(list)
-    for k, (i, _) in zip(owner, hits):
-        found[k].append(i >= 0)
+    for k, (i, a) in zip(owner, hits):
+        found[k].append(a if i >= 0 else None)
     by_id = {r["id"]: r for r in records}
-    out = {"searched": len(sets), "gpu_found": 0, "seconds": secs, "unsound": []}
+    out = {"searched": len(sets), "gpu_found": 0, "seconds": secs, "unsound": [],
+           "witnesses": {}}
     for k, qid in enumerate(idx):
-        if found.get(k) and all(found[k]):
+        if found.get(k) and all(a is not None for a in found[k]):
             out["gpu_found"] += 1
+            out["witnesses"][qid] = M._merge(found[k])      # the joint model
             if by_id[qid]["result"] == "unsat":
                 out["unsound"].append(qid)
     return out
@@ -186,6 +186,8 @@ def main(argv=None) -> int:
     report = {"census": census(records)}
     if args.gpu:
         report["gpu"] = replay_gpu(records)
+        report["gpu"]["witnesses"] = {str(k): {"vars": {n: hex(v) for n, v in a.vars.items()}}
+                                      for k, a in report["gpu"]["witnesses"].items()}
     print(json.dumps(report, indent=1))
     return 1 if report.get("gpu", {}).get("unsound") else 0
 

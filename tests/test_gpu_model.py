@@ -176,6 +176,13 @@ def test_capture_replay_on_gpu(engine, tmp_path):
                                  "result": res}) + "\n")
     rep = capture.replay_gpu(capture.read(str(path)))
     assert rep["searched"] == 3 and rep["gpu_found"] == 2 and rep["unsound"] == []
+    # every replayed witness satisfies the query as re-parsed from the capture
+    from oracle import smtlib_ref as R
+    recs = {r["id"]: r for r in capture.read(str(path))}
+    assert sorted(rep["witnesses"]) == [0, 1]
+    for qid, a in rep["witnesses"].items():
+        cs = smtlib.parse_query(recs[qid]["smt2"])
+        assert R.eval_constraints(cs, R.Assignment(a.vars, a.arrays, a.funcs)) == 1, qid
 
 
 def test_replace_with_actual_sha_on_gpu(engine):
