@@ -67,6 +67,7 @@ class Solver:
         self.n_aux = 0
         self.n_branch = 0
         self.selectors: set = set()              # LEAF ids of branch / domain selectors
+        self.or_seen: set = set()                # ``or`` atoms already split
         # LEAF id -> generation of a branch's stand-in for an undefined value
         # (a stand-in may be split again by a later ``or``, to BRANCH_DEPTH)
         self.depth: Dict[int, int] = {}
@@ -496,7 +497,8 @@ class Solver:
                         if done:
                             break
                 n += done
-            elif x.op == I.OR and x.width == 1:
+            elif x.op == I.OR and x.width == 1 and x.id not in self.or_seen:
+                self.or_seen.add(x.id)           # the same or splits the same way again
                 n += self._domain(x) or self._branches(x)
         return n
 
