@@ -804,48 +804,61 @@ def _pool_values(c: int, w: int) -> List[int]:
     return out
 
 
+def _bits(x: int):
+    """Indices of the set bits of x, ascending."""
+    while x:
+        low = x & -x
+        yield low.bit_length() - 1
+        x ^= low
+
+
 def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
     """Constraint-guided candidate pools: every comparison (=, <, <=, signed
     or not) makes the constants under it candidates for the leaves under it,
     so a leaf draws the values it is actually tested against instead of any
     constant of the query.  Leaves under no comparison with a constant get
-    an empty list (the caller falls back to the whole constant table)."""
-    under_l: Dict[int, frozenset] = {}
-    under_c: Dict[int, frozenset] = {}
+    an empty list (the caller falls back to the whole constant table).
+    Leaf and constant sets are bit sets (constants indexed in ascending
+    value order, so the POOL_CAP smallest are the lowest bits)."""
+    values = sorted({n.imm for n in order if n.op == I.CONST})
+    cidx = {v: i for i, v in enumerate(values)}
+    under_l: Dict[int, int] = {}
+    under_c: Dict[int, int] = {}
     pools: List[Dict[int, None]] = [dict() for _ in leaves]
-    done: List[set] = [set() for _ in leaves]         # constants already drawn from
+    done: List[int] = [0] * len(leaves)               # constants already drawn from
     pv: Dict[Tuple[int, int], List[int]] = {}
     M256 = (1 << 256) - 1
     for n in order:                                   # topological
         if n.op == I.LEAF:
-            under_l[n.id], under_c[n.id] = frozenset((n.imm,)), frozenset()
+            under_l[n.id], under_c[n.id] = 1 << n.imm, 0
             continue
         if n.op == I.CONST:
-            under_l[n.id], under_c[n.id] = frozenset(), frozenset((n.imm,))
+            under_l[n.id], under_c[n.id] = 0, 1 << cidx[n.imm]
             continue
-        ls, cs = frozenset(), frozenset()
+        ls = cs = 0
         for a in n.args:
-            ls |= under_l.get(a.id, frozenset())
-            cs |= under_c.get(a.id, frozenset())
-        if len(cs) > POOL_CAP:                        # keep the walk linear-ish
-            cs = frozenset(sorted(cs)[:POOL_CAP])
+            ls |= under_l.get(a.id, 0)
+            cs |= under_c.get(a.id, 0)
+        if cs.bit_count() > POOL_CAP:                 # keep the walk linear-ish
+            keep = 0
+            for k, ci in enumerate(_bits(cs)):
+                if k == POOL_CAP:
+                    break
+                keep |= 1 << ci
+            cs = keep
         under_l[n.id], under_c[n.id] = ls, cs
         if n.op in _CMP_OPS and cs:
-            ordered = None
-            for li in ls:
+            for li in _bits(ls):
                 p = pools[li]
                 if len(p) >= POOL_CAP:
                     continue
-                seen = done[li]
-                if cs <= seen:
+                new = cs & ~done[li]
+                if not new:
                     continue
+                done[li] |= new
                 w = leaves[li].width
-                if ordered is None:
-                    ordered = sorted(cs)
-                for c in ordered:
-                    if c in seen:
-                        continue
-                    seen.add(c)
+                for ci in _bits(new):
+                    c = values[ci]
                     vals = pv.get((c, w))
                     if vals is None:
                         vals = pv[(c, w)] = [v & M256 for v in _pool_values(c, w)]
@@ -1062,7 +1075,8 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
                 lw.leaves[li].pool = tuple(p)
             else:
                 pool_ranges.append((0, len(const_values)))
-    consts = np.array([_limbs(v) for v in table], dtype=np.uint32).reshape(-1, 8)
+    consts = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in table),
+                           dtype="<u4").reshape(-1, 8).astype(np.uint32)
     hist: Dict[str, int] = {}
     for n in order:
         hist[I.OPNAME[n.op]] = hist.get(I.OPNAME[n.op], 0) + 1

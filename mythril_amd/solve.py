@@ -68,6 +68,10 @@ class Solver:
         self.n_branch = 0
         self.selectors: set = set()              # LEAF ids of branch / domain selectors
         self.or_seen: set = set()                # ``or`` atoms already split
+        self.dep: Dict[int, int] = {}            # LNode id -> leaf bit set
+        self.clean: set = set()                  # ids of rewrite results
+        self.leaf_imm: Dict[int, int] = {}       # defined LEAF id -> leaf index
+        self._dm = None                          # bit set of the defined leaves
         # LEAF id -> generation of a branch's stand-in for an undefined value
         # (a stand-in may be split again by a later ``or``, to BRANCH_DEPTH)
         self.depth: Dict[int, int] = {}
@@ -116,9 +120,47 @@ class Solver:
             return x
         return lw.mk(op, x.width, args, x.imm)
 
+    def _dep(self, n) -> int:
+        """Bit set (by leaf index) of the leaves under ``n``."""
+        dep = self.dep
+        d = dep.get(n.id)
+        if d is not None:
+            return d
+        stack = [n]
+        while stack:
+            x = stack[-1]
+            if x.id in dep:
+                stack.pop()
+                continue
+            pend = [a for a in x.args if a.id not in dep]
+            if pend:
+                stack.extend(pend)
+                continue
+            stack.pop()
+            if x.op == I.LEAF:
+                v = 1 << x.imm
+            else:
+                v = 0
+                for a in x.args:
+                    v |= dep[a.id]
+            dep[x.id] = v
+        return dep[n.id]
+
+    def _defmask(self) -> int:
+        if self._dm is None:
+            m = 0
+            for k in self.repl:
+                m |= 1 << self.leaf_imm[k]
+            self._dm = m
+        return self._dm
+
     def rewrite(self, n, memo: Dict[int, object]):
         """``n`` with every defined leaf replaced by its definition (followed
-        transitively) and folded."""
+        transitively) and folded.  A node that is already a rewrite result
+        (``clean``: folding cannot change it) over undefined leaves only is
+        its own result — the walk does not enter it."""
+        dm = self._defmask()
+        clean, dep = self.clean, self._dep
         stack = [(n, False)]
         while stack:
             x, done = stack.pop()
@@ -138,10 +180,15 @@ class Solver:
                 memo[x.id] = x
                 continue
             if not done:
+                if x.id in clean and not dep(x) & dm:
+                    memo[x.id] = x
+                    continue
                 stack.append((x, True))
                 stack.extend((a, False) for a in x.args if a.id not in memo)
                 continue
-            memo[x.id] = self._fold(x, tuple(memo[a.id] for a in x.args))
+            r = self._fold(x, tuple(memo[a.id] for a in x.args))
+            clean.add(r.id)
+            memo[x.id] = r
         return memo[n.id]
 
     # -- small constructors ------------------------------------------------------
@@ -429,6 +476,8 @@ class Solver:
         if self._depends(e, leaf):
             return False
         self.repl[leaf.id] = e
+        self.leaf_imm[leaf.id] = leaf.imm
+        self._dm = None
         return True
 
     def _domain(self, x) -> bool:
@@ -570,6 +619,7 @@ class Solver:
             self._ranges(atoms)
             per.append({k: v for k, v in self.repl.items() if k not in saved})
             self.repl = dict(saved)
+            self._dm = None
         self.unsat = unsat
         leaves = {}
         for defs in per:
