@@ -134,4 +134,8 @@ def unpack(program: Program, leaves: np.ndarray, probes: np.ndarray = None) -> A
         tab = ([(c, t["c"].get(i, 0)) for i, c in enumerate(ck)] +
                [(t["k"].get(e, 0), t["v"].get(e, 0)) for e in range(n)], t["else"])
         (funcs if program.table_kinds.get(name) == "func" else arrays)[name] = tab
-    return Assignment(vars_, arrays, funcs)
+    asg = Assignment(vars_, arrays, funcs)
+    if getattr(program, "presets", None) is not None:
+        from .abi import merge
+        merge(asg, program.presets)
+    return asg

@@ -115,11 +115,14 @@ class Program:
     derived: Dict[int, int] = field(default_factory=dict)
     entry_keys: Dict[str, List[List[int]]] = field(default_factory=dict)
     n_user_probes: int = 0
+    # search mode: fixed parts of every candidate model (abi.Plan: the ABI
+    # offset words and calldatasize the query was compiled under)
+    presets: object = None
 
     @property
     def solved(self) -> bool:
         """Witnesses need the probe values too (``assign.unpack``)."""
-        return bool(self.derived or self.entry_keys)
+        return bool(self.derived or self.entry_keys or self.presets)
 
     @property
     def n_ins(self) -> int:
@@ -873,7 +876,7 @@ def _leaf_pools(order: List[LNode], leaves: List["Leaf"]) -> List[List[int]]:
 
 CKEY_CAP = 128          # constant-keyed entries per table
 CKEY_LINKS = 2048       # symbolic-key lookups x constant keys per table
-ARG_ENTRIES_CAP = 32    # solve mode: argument-keyed entries per table (links grow as n^2/2)
+ARG_ENTRIES_CAP = 64    # solve mode: argument-keyed entries per table (links grow as n^2/2)
 
 
 def scan_const_keys(nodes: Sequence[Node], cap: int = CKEY_CAP,
@@ -934,30 +937,6 @@ def lw_tables(constraints, probes) -> set:
     return out
 
 
-def _resolve(n: LNode, defs: Dict[int, LNode], lw: "_Lowerer", memo: Dict[int, LNode]) -> LNode:
-    """``n`` with every leaf defined by an equality replaced by its
-    definition (the keys of table entries may mention such leaves)."""
-    stack = [(n, False)]
-    while stack:
-        x, done = stack.pop()
-        if x.id in memo:
-            continue
-        if x.op == I.LEAF:
-            memo[x.id] = defs.get(x.imm, x)
-            continue
-        if not x.args:
-            memo[x.id] = x
-            continue
-        if not done:
-            stack.append((x, True))
-            stack.extend((a, False) for a in x.args if a.id not in memo)
-            continue
-        args = tuple(memo[a.id] for a in x.args)
-        memo[x.id] = x if all(a is b for a, b in zip(args, x.args)) else lw.mk(x.op, x.width, args,
-                                                                             x.imm)
-    return memo[n.id]
-
-
 def _conjuncts(n: LNode) -> List[LNode]:
     """The top-level conjuncts of a lowered Bool (AND trees of width 1)."""
     out, stack = [], [n]
@@ -996,7 +975,9 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
     lw.solve = solve
     if const_keys or solve:
         sym_counts: Dict[str, int] = {}
-        ck = scan_const_keys(list(constraints) + list(probes), sym_counts=sym_counts)
+        ck = scan_const_keys(list(constraints) + list(probes), sym_counts=sym_counts,
+                             cap=256 if solve else CKEY_CAP,
+                             max_links=8192 if solve else CKEY_LINKS)
         if const_keys:
             lw.table_ckeys = ck
         # tables read at a bounded number of symbolic keys get argument-keyed
@@ -1045,8 +1026,11 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
         for li, e in sorted(derived_nodes.items()):
             derived[li] = out(e)
         memo_e: Dict[int, LNode] = {}
+        lw.birth = 0
         for name, ents in lw.arg_entries.items():
-            entry_keys[name] = [[out(_resolve(k, derived_nodes, lw, memo_e)) for k in key]
+            # keys under the constructed model (folded: an ABI offset the
+            # model pins makes its reads' keys constants)
+            entry_keys[name] = [[out(solver.rewrite(k, memo_e)) for k in key]
                                 for key, _ in ents]
     if not sinks:
         sinks.append(lw.mk(I.ROOT, 1, (lw.const(1, 1),), None))

@@ -277,8 +277,16 @@ def _compile_search(nodes: Sequence[N.Node], probes: Sequence[N.Node] = ()) -> P
     its argument-keyed entries keep too many values live for the spill
     budget — the plain search form (every model value generated).
     ``probes`` are evaluated under each candidate's model."""
+    from . import abi
     hints = harvest_hints(nodes)
+    plan = abi.plan(nodes)
     try:
+        if plan is not None:
+            # ABI offsets pinned (abi.py): a witness carries the presets
+            prog = compile_constraints(plan.apply(nodes), plan.apply(probes), extra_consts=hints,
+                                       leaf_pools=True, const_keys=True, solve=True)
+            prog.presets = plan
+            return prog
         return compile_constraints(nodes, probes, extra_consts=hints, leaf_pools=True,
                                    const_keys=True, solve=True)
     except Unsupported as e:

@@ -54,6 +54,13 @@ SELECTOR_WIDTH = 8
 _PREDICATES = (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO)
 
 
+def _bit_indices(x: int):
+    while x:
+        low = x & -x
+        yield low.bit_length() - 1
+        x ^= low
+
+
 def _mask(w: int) -> int:
     return (1 << w) - 1
 
@@ -69,6 +76,8 @@ class Solver:
         self.selectors: set = set()              # LEAF ids of branch / domain selectors
         self.or_seen: set = set()                # ``or`` atoms already split
         self.dep: Dict[int, int] = {}            # LNode id -> leaf bit set
+        self.ivl: Dict[int, tuple] = {}          # LNode id -> unsigned interval
+        self.joint_done: set = set()             # expressions whose bounds were joined
         self.clean: set = set()                  # ids of rewrite results
         self.leaf_imm: Dict[int, int] = {}       # defined LEAF id -> leaf index
         self._dm = None                          # bit set of the defined leaves
@@ -78,17 +87,119 @@ class Solver:
         self.unsat = False
 
     # -- rewriting -------------------------------------------------------------
+    def _interval(self, n):
+        """Unsigned [lo, hi] of a value (canonical: a node of width w is
+        below 2^w); exact for constants, sums that cannot wrap, ite."""
+        r = self.ivl.get(n.id)
+        if r is not None:
+            return r
+        top = _mask(n.width)
+        if n.op == I.CONST:
+            r = (n.imm, n.imm)
+        elif n.op == I.ADD:
+            (la, ha), (lb, hb) = self._interval(n.args[0]), self._interval(n.args[1])
+            r = (la + lb, ha + hb) if ha + hb <= top else (0, top)
+        elif n.op == I.ITE:
+            (la, ha), (lb, hb) = self._interval(n.args[1]), self._interval(n.args[2])
+            r = (min(la, lb), max(ha, hb))
+        elif n.op in _PREDICATES:
+            r = (0, 1)
+        else:
+            r = (0, top)
+        self.ivl[n.id] = r
+        return r
+
+    def _cmp_fold(self, op, w, a, b):
+        """ULT / ULE / SLT / SLE decided by the operands' intervals, or None."""
+        (la, ha), (lb, hb) = self._interval(a), self._interval(b)
+        if op in (I.SLT, I.SLE):
+            half = 1 << (w - 1)
+            if ha >= half or hb >= half:
+                return None                      # not both non-negative
+        if op in (I.ULT, I.SLT):
+            if ha < lb:
+                return self.one
+            if la >= hb:
+                return self.zero
+        else:
+            if ha <= lb:
+                return self.one
+            if la > hb:
+                return self.zero
+        return None
+
+    def _const_fold(self, x, args):
+        """Bit-vector ops over constants."""
+        w, op = x.width, x.op
+        v = [a.imm for a in args]
+        m = _mask(w)
+        if op == I.CONCAT:
+            return (v[0] << x.imm | v[1]) & m
+        if op == I.EXTRACT:
+            return (v[0] >> x.imm) & m
+        if op == I.AND:
+            return v[0] & v[1] & m
+        if op == I.OR:
+            return (v[0] | v[1]) & m
+        if op == I.XOR:
+            return (v[0] ^ v[1]) & m
+        if op == I.SUB:
+            return (v[0] - v[1]) & m
+        if op == I.MUL:
+            return (v[0] * v[1]) & m
+        if op == I.NOT:
+            return ~v[0] & m
+        return None
+
     def _fold(self, x, args):
         lw, op = self.lw, x.op
+        if op in (I.CONCAT, I.EXTRACT, I.AND, I.OR, I.XOR, I.SUB, I.MUL, I.NOT) and \
+                all(a.op == I.CONST for a in args):
+            c = self._const_fold(x, args)
+            if c is not None:
+                return lw.const(c, x.width)
+        if op in (I.ULT, I.ULE, I.SLT, I.SLE) and not all(a.op == I.CONST for a in args):
+            r = self._cmp_fold(op, x.width, args[0], args[1])
+            if r is not None:
+                return r
         if op == I.EQ:
             a, b = args
             if a is b:
                 return self.one
             if a.op == I.CONST and b.op == I.CONST:
                 return self.one if a.imm == b.imm else self.zero
-        elif op in (I.ULT, I.ULE) and all(a.op == I.CONST for a in args):
+            # y + c1 = y + c2 (and y + c = y): symbolic ABI offsets that differ
+            # by a constant never alias
+            ya, ca = (a.args[0], a.args[1].imm) if a.op == I.ADD and a.args[1].op == I.CONST \
+                else (a, 0)
+            yb, cb = (b.args[0], b.args[1].imm) if b.op == I.ADD and b.args[1].op == I.CONST \
+                else (b, 0)
+            if ya is yb and a.width == b.width and ya.op != I.CONST:
+                return self.one if ca == cb else self.zero
+            (la, ha), (lb, hb) = self._interval(a), self._interval(b)
+            if ha < lb or hb < la:                   # disjoint ranges (a keccak
+                return self.zero                     # interval vs a small slot)
+        elif op == I.ADD:
+            a, b = args
+            if a.op == I.CONST and b.op != I.CONST:
+                a, b = b, a
+            if b.op == I.CONST:
+                w = x.width
+                if a.op == I.CONST:
+                    return lw.const((a.imm + b.imm) & _mask(w), w)
+                if b.imm == 0 and a.width <= w:
+                    return a
+                if a.op == I.ADD and a.width == w and a.args[1].op == I.CONST:
+                    # (y + c1) + c2 = y + (c1 + c2): ABI offsets off + 4 + i
+                    return lw.mk(I.ADD, w, (a.args[0], lw.const((a.args[1].imm + b.imm) & _mask(w), w)))
+                if (a, b) != args:
+                    return lw.mk(I.ADD, w, (a, b))
+        elif op in (I.ULT, I.ULE, I.SLT, I.SLE) and all(a.op == I.CONST for a in args):
             a, b = args[0].imm, args[1].imm
-            return self.one if (a < b if op == I.ULT else a <= b) else self.zero
+            if op in (I.SLT, I.SLE):
+                half = 1 << (x.width - 1)
+                a, b = a - 2 * half if a >= half else a, b - 2 * half if b >= half else b
+            return self.one if (a < b if op in (I.ULT, I.SLT) else a <= b) else self.zero
         elif op == I.ITE:
             c = args[0]
             if c.op == I.CONST:
@@ -288,7 +399,7 @@ class Solver:
                 n_lo = lw_ - off
                 return [self._eq(self._ext(lo, off, n_lo), k & _mask(n_lo)),
                         self._eq(self._ext(hi, 0, w - n_lo), k >> n_lo)]
-            if y.op == I.ITE and (y.args[1].op == I.CONST or y.args[2].op == I.CONST):
+            if y.op == I.ITE:
                 c, p, q = y.args
                 return [self.lw.mk(I.EQ, w, (self.lw.mk(I.ITE, w, (c, self._ext(p, off, w),
                                                                     self._ext(q, off, w))),
@@ -343,13 +454,22 @@ class Solver:
                     if r is not None:
                         stack.append(r)
                         continue
-                out.append(x)
-                if y.op == I.UMULNO and y.args[1].op != I.CONST:
+                if y.op in (I.ULT, I.ULE, I.SLT, I.SLE):
+                    pass                         # a negated bound: handled below
+                else:
+                    out.append(x)
+                if y.op not in (I.ULT, I.ULE, I.SLT, I.SLE) and y.op == I.UMULNO and \
+                        y.args[1].op != I.CONST:
                     # a * b >= 2^w (BVMulNoOverflow negated): b = 2^w - 1
-                    # suffices for every a > 1
+                    # overflows for every a > 1, b = 2^(w-1) for every even a
+                    # with a zero product (what a later balance check needs:
+                    # BECToken's batchTransfer) — a split between the two
                     b_ = y.args[1]
-                    stack.append(self.rewrite(self._eq(b_, _mask(b_.width)), memo))
-                continue
+                    w_ = y.width
+                    stack.append(self.rewrite(self.lw.mk(I.OR, 1, (
+                        self._eq(b_, _mask(b_.width)), self._eq(b_, 1 << (w_ - 1)))), memo))
+                if y.op not in (I.ULT, I.ULE, I.SLT, I.SLE):
+                    continue
             if x.op == I.EQ:
                 parts = self._split_eq(x)
                 if parts is not None:
@@ -370,13 +490,60 @@ class Solver:
                     stack.append(le)
                     continue
             b = self._bound(x)
-            if b is not None and b[0].op == I.ITE:
+            if b is not None and b[0].op in (I.ITE, I.CONCAT, I.MUL):
                 parts = self._split_bound(*b)
                 if parts is not None:
+                    if b[0].op != I.ITE:
+                        out.append(x)            # (a sufficient condition only)
+                    stack.extend(self.rewrite(p, memo) for p in parts)
+                    continue
+            if b is None:
+                parts = self._order_via_arm(x)
+                if parts is not None:
+                    out.append(x)
                     stack.extend(self.rewrite(p, memo) for p in parts)
                     continue
             out.append(x)
         return out
+
+    def _order_via_arm(self, x) -> Optional[list]:
+        """``a <= s`` / ``a < s`` with ``s`` an ite tree of constants (a
+        storage read: known values, else 0): commit to the path that gives
+        ``s`` its largest value and bound ``a`` by it (sufficient)."""
+        neg = x.op == I.NOT and x.width == 1
+        y = x.args[0] if neg else x
+        if y.op not in (I.ULT, I.ULE):
+            return None
+        a, s = y.args
+        strict = y.op == I.ULT
+        if neg:                                    # not (s' < a') = a' <= s'
+            a, s, strict = s, a, not strict
+        if s.op != I.ITE:
+            return None
+        best = self._max_arm(s)
+        if best is None:
+            return None
+        k, conds = best
+        hi = k - 1 if strict else k
+        if hi < 0:
+            return None
+        return conds + self._mk_bound(a, 0, hi, y.width)
+
+    def _max_arm(self, s, depth: int = 8):
+        """(largest constant an ite tree can select, the conditions that
+        select it) over constant arms only."""
+        best = None
+        stack = [(s, [], 0)]
+        while stack:
+            n, conds, d = stack.pop()
+            if n.op == I.CONST:
+                if best is None or n.imm > best[0]:
+                    best = (n.imm, conds)
+            elif n.op == I.ITE and d < depth:
+                c = n.args[0]
+                stack.append((n.args[1], conds + [c], d + 1))
+                stack.append((n.args[2], conds + [self._not(c)], d + 1))
+        return best
 
     def _as_ule(self, x):
         """``a < b or a = b`` (how LASER writes ``ULE`` / ``UGE``) as one
@@ -436,7 +603,7 @@ class Solver:
             out.append(self.lw.mk(I.ULE, w, (e, self.lw.const(hi, w))))
         return out
 
-    def _split_bound(self, e, lo, hi, w) -> Optional[list]:
+    def _split_ite_bound(self, e, lo, hi, w) -> Optional[list]:
         """``lo <= ite(c, k, y) <= hi``: ``y`` in range suffices when ``k`` is
         (else ``not c`` is needed too)."""
         c, p, q = e.args
@@ -446,6 +613,39 @@ class Solver:
         if q.op == I.CONST and p.op != I.CONST:
             inside = lo <= q.imm <= hi
             return self._mk_bound(p, lo, hi, w) + ([] if inside else [c])
+        if p.op != I.CONST and q.op != I.CONST:
+            return self._mk_bound(p, lo, hi, w) + self._mk_bound(q, lo, hi, w)   # sufficient
+        return None
+
+    def _split_bound(self, e, lo, hi, w) -> Optional[list]:
+        if e.op == I.ITE:
+            return self._split_ite_bound(e, lo, hi, w)
+        if e.op == I.CONCAT:
+            # x = h . l in [lo, hi] with hi < 2^|l|: h = 0 and l in [lo, hi]
+            # (exact, down the concat chain); a larger hi: h < hi >> |l|
+            # (any l; sufficient)
+            out = []
+            while e.op == I.CONCAT:
+                _, lw_, l_ = self._concat_parts(e)
+                if hi >> lw_:
+                    break
+                out.append(self._eq(self._hi(e), 0))
+                e = l_
+            if e.op != I.CONCAT:
+                return out + self._mk_bound(e, lo, hi, e.width)
+            if lo:
+                return out or None
+            _, lw_, _ = self._concat_parts(e)
+            h = self._hi(e)
+            return out + self._mk_bound(h, 0, (hi >> lw_) - 1, h.width)
+        if lo:
+            return None
+        if e.op == I.MUL:
+            # a * b <= hi: both factors below 2^(k/2) with 2^k <= hi + 1
+            k = (hi + 1).bit_length() - 1
+            a, b = e.args
+            return (self._mk_bound(a, 0, (1 << (k // 2)) - 1, w) +
+                    self._mk_bound(b, 0, (1 << (k - k // 2)) - 1, w))
         return None
 
     # -- definitions -------------------------------------------------------------
@@ -479,6 +679,20 @@ class Solver:
         self.leaf_imm[leaf.id] = leaf.imm
         self._dm = None
         return True
+
+    @staticmethod
+    def _ite_leaves(x, limit: int = 16) -> list:
+        """Leaves an ite tree (through its arms, not its conditions) can
+        select, innermost-else last."""
+        out, stack = [], [x] if x.op == I.ITE else []
+        while stack and len(out) < limit:
+            y = stack.pop()
+            for arm in (y.args[1], y.args[2]):
+                if arm.op == I.LEAF:
+                    out.append(arm)
+                elif arm.op == I.ITE:
+                    stack.append(arm)
+        return out
 
     def _domain(self, x) -> bool:
         """``leaf = k1 or ... or leaf = kn``: the leaf becomes a selector-picked
@@ -536,13 +750,14 @@ class Solver:
                         done = True
                         break
                 if not done:
-                    # ite(c, leaf, y) = e: the leaf's value e suffices when c
+                    # ite(c, leaf, y) = e (also nested: a first-match table
+                    # read ite(k = k0, v0, ite(k = k1, v1, leaf))): the leaf's
+                    # value e suffices on the path that reaches it
                     for side, e in ((p, q), (q, p)):
-                        if side.op == I.ITE:
-                            for arm in side.args[1:]:
-                                if arm.op == I.LEAF and self._try_define(arm, e):
-                                    done = True
-                                    break
+                        for arm in self._ite_leaves(side):
+                            if self._try_define(arm, e):
+                                done = True
+                                break
                         if done:
                             break
                 n += done
@@ -655,25 +870,114 @@ class Solver:
             n += self._try_define(leaf, e)
         return n
 
+    def _abi_offsets(self) -> list:
+        """Symbolic table keys ``y + c`` whose base ``y`` is not constant
+        (calldata read at an ABI offset that is itself a calldata word:
+        ``calldata.py:219-232`` under a dynamic parameter) get ``y``
+        pinned the way the ABI lays out dynamic data: right after the
+        table's constant-key reads, 32-aligned, in order of first use —
+        ``y = K`` atoms for the definition passes."""
+        out = []
+        for name, ents in self.lw.arg_entries.items():
+            ck = self.lw.table_ckeys.get(name)
+            if not ck or len(ents[0][0]) != 1:
+                continue
+            spans: Dict[int, list] = {}
+            memo: Dict[int, object] = {}
+            for key, _ in ents:
+                k = self.rewrite(key[0], memo)
+                y, c = (k.args[0], k.args[1].imm) if k.op == I.ADD and \
+                    k.args[1].op == I.CONST else (k, 0)
+                if y.op == I.CONST or c >> 32 or not self._reads_own(y, name):
+                    continue
+                r = spans.setdefault(y.id, [y, c, c])
+                r[1], r[2] = min(r[1], c), max(r[2], c)
+            nxt = max(ck) + 1
+            for y, lo, hi in spans.values():
+                base = -(-(nxt - lo) // 32) * 32           # first read lands past nxt
+                out.append(self.lw.mk(I.EQ, y.width, (y, self.lw.const(base, y.width))))
+                nxt = base + hi + 1
+        return out
+
+    def _joint_bounds(self, atoms):
+        """The intersected bounds of every non-leaf expression bounded by
+        two or more atoms, split (atoms to process one by one)."""
+        groups: Dict[int, list] = {}
+        for a in atoms:
+            b = self._bound(a)
+            if b is None or b[0].op in (I.LEAF, I.CONST):
+                continue
+            e, lo, hi, w = b
+            g = groups.setdefault(e.id, [e, 0, _mask(w), w, 0])
+            g[1], g[2], g[4] = max(g[1], lo), min(g[2], hi), g[4] + 1
+        parts = []
+        for e, lo, hi, w, k in groups.values():
+            if k >= 2 and lo <= hi and (e.id, lo, hi) not in self.joint_done:
+                self.joint_done.add((e.id, lo, hi))
+                # split with both limits at once (separate atoms would be
+                # split apart again)
+                sp = self._split_bound(e, lo, hi, w) if e.op in (I.CONCAT, I.ITE, I.MUL) \
+                    else None
+                parts += sp if sp is not None else self._mk_bound(e, lo, hi, w)
+        return parts
+
+    @staticmethod
+    def _is_wrap_test(r) -> bool:
+        """``not bvumul_noovfl(a, b)`` or the carry test ``a + b < a``."""
+        x = r
+        while x.op == I.AND and x.width == 1 and len(x.args) == 2 and x.args[0].op == I.CONST:
+            x = x.args[1]
+        if x.op == I.NOT and x.width == 1 and x.args[0].op == I.UMULNO:
+            return True
+        return x.op == I.ULT and x.args[0].op == I.ADD and x.args[1] in x.args[0].args
+
+    def _reads_own(self, y, name: str) -> bool:
+        """``y`` is built from the table's own cells (and its size): an
+        offset word read from the calldata it indexes."""
+        own = False
+        for li in _bit_indices(self._dep(y)):
+            leaf = self.lw.leaves[li]
+            if leaf.source == name:
+                own = True
+            elif not leaf.name.endswith("calldatasize"):
+                return False
+        return own
+
     def run(self, roots):
         # new nodes are born with their latest operand (ir._schedule places
         # them there), not after the whole query
         saved_birth, self.lw.birth = self.lw.birth, 0
+        pins = self._abi_offsets()
+        if pins:
+            self._define(self._atoms(self.lw.mk(I.AND, 1, tuple(pins)) if len(pins) > 1
+                                     else pins[0], {}))
+        # the overflow tests first (the integer module's check is the
+        # query's last constraint; its wrap-around choice must win over the
+        # bounds the path constraints put on the same operands)
+        order = sorted(roots, key=lambda r: not self._is_wrap_test(r))
         for _ in range(PASSES):
             memo: Dict[int, object] = {}
             found = 0
             every = []
-            for r in roots:
+            for r in order:
                 atoms = self._atoms(r, memo)
                 every += atoms
                 k = self._define(atoms)
                 if k:                   # later roots see the new definitions folded
                     memo = {}
                 found += k
-            # intervals from the bounds of all conjuncts together
+            # intervals from the bounds of all conjuncts together: per
+            # expression (x >= 2 from one constraint, x <= 2 from another make
+            # x = 2 — through a concat, its low byte), then per leaf
             if found:
                 memo = {}
                 every = [self.rewrite(a, memo) for a in every]
+            extra = []
+            for part in self._joint_bounds(every):     # one by one: a violated
+                extra += self._atoms(part, memo)      # part must not hide the rest
+            if extra:
+                found += self._define(extra)
+                every += extra
             found += self._ranges(every)
             if not found:
                 break

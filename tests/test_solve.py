@@ -152,3 +152,60 @@ def test_workload_witnesses_sound(name):
             hits += h
     if name != "c3":
         assert hits > 0
+
+
+def _bec_batch_query(receivers):
+    from mythril_amd.workloads import World, bv, ACTORS, _TOTAL, _BAL, _OWNER_PAUSED, _bec_batch
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    supply = bv(7000000000 * 10 ** 18)
+    c.sstore(bv(_TOTAL), supply)
+    c.sstore(c.mapping(bv(ACTORS[0]), _BAL), supply)
+    c.sstore(bv(_OWNER_PAUSED), bv(ACTORS[0]))
+    t = w.tx()
+    checks = []
+    _bec_batch(t, checks, receivers)
+    return w.query([checks[0]])                # Not(BVMulNoOverflow(cnt, value))
+
+
+def test_abi_offsets_are_preset():
+    """batchTransfer(address[],uint256) reads _receivers at calldata[off + 4
+    + i] with off the word at byte 4 (abi.py): off is pinned right after the
+    head (0x40), calldatasize to the end of the last read, and every read
+    becomes a constant-key read."""
+    from mythril_amd import abi
+    from mythril_amd.smt.node import topo_order
+    q = _bec_batch_query(2)
+    plan = abi.plan(q)
+    assert plan is not None
+    cells = plan.arrays["1_calldata"]
+    assert [cells[4 + i] for i in range(32)] == list((0x40).to_bytes(32, "big"))
+    assert plan.vars["1_calldatasize"] == 4 + 0x40 + 32 * 3        # length + two receivers
+    q2 = plan.apply(q)
+    sym = [n for n in topo_order(q2) if n.op == "select" and n.args[0].op == "array" and
+           n.args[0].params[0] == "1_calldata" and n.args[1].op != "bvnum"]
+    assert sym == []
+
+
+def test_bec_batch_overflow_is_found():
+    """The BECToken batchTransfer overflow (cnt = 2, value = 2^255, amount
+    wraps to 0): the search program pins the ABI offsets, commits to the
+    wrapping value and the joint bounds 2 <= cnt <= 2, and its witnesses
+    are models of the original query (presets merged) in the oracle."""
+    from mythril_amd.model import _compile_search, dependence_buckets
+    q = _bec_batch_query(2)
+    g = max(dependence_buckets(q), key=len)
+    prog = _compile_search(g)
+    assert prog.presets is not None and prog.solved
+    table = [sum(int(prog.consts[i, j]) << (32 * j) for j in range(8))
+             for i in range(prog.consts.shape[0])]
+    hits = 0
+    for idx in range(256):
+        lv = [gen_ref.gen_leaf(11, 0, li, idx, l.width,
+                               table[prog.pool_ranges[li][0]:sum(prog.pool_ranges[li])],
+                               pct=(20, 40, 60)) for li, l in enumerate(prog.leaves)]
+        root, probes = ir_sim.run(prog, lv)
+        a = unpack(prog, _pack1(lv), _pack1(probes))
+        assert root == R.eval_constraints(g, R.Assignment(a.vars, a.arrays, a.funcs)), idx
+        hits += root
+    assert hits > 0
