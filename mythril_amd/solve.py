@@ -364,9 +364,19 @@ class Solver:
                     return [self._not(c)]
                 return [self.zero]
             if q.op == I.CONST:
-                return [c, self._eq(p, k)] if q.imm != k else [self._eq(p, k)]
+                if q.imm != k:
+                    return [c, self._eq(p, k)]
+                # q = k: p = k suffices — unless p can never be k (its range
+                # excludes it), then c must be false
+                lo, hi = self._interval(p)
+                return [self._eq(p, k)] if lo <= k <= hi else [self._not(c)]
             if p.op == I.CONST:
-                return [self._not(c), self._eq(q, k)] if p.imm != k else [self._eq(q, k)]
+                if p.imm != k:
+                    return [self._not(c), self._eq(q, k)]
+                # p = k (a first-match table read ite(x = k0, h0, v) = h0):
+                # v = k suffices — unless v can never be k, then x = k0
+                lo, hi = self._interval(q)
+                return [self._eq(q, k)] if lo <= k <= hi else [c]
             return [self._eq(p, k), self._eq(q, k)]             # sufficient
         if a.op == I.AND and a.width > 1:
             m, z = a.args
