@@ -80,6 +80,7 @@ class Solver:
         self.joint_done: set = set()             # expressions whose bounds were joined
         self.clean: set = set()                  # ids of rewrite results
         self.leaf_imm: Dict[int, int] = {}       # defined LEAF id -> leaf index
+        self.leaf_node: Dict[int, object] = {}   # defined LEAF id -> the LEAF node
         self._dm = None                          # bit set of the defined leaves
         # LEAF id -> generation of a branch's stand-in for an undefined value
         # (a stand-in may be split again by a later ``or``, to BRANCH_DEPTH)
@@ -687,6 +688,7 @@ class Solver:
             return False
         self.repl[leaf.id] = e
         self.leaf_imm[leaf.id] = leaf.imm
+        self.leaf_node[leaf.id] = leaf
         self._dm = None
         return True
 
@@ -854,7 +856,7 @@ class Solver:
             return 0
         self.n_branch += 1
         lw = self.lw
-        by_id = {n.id: n for n in lw.table.values() if n.op == I.LEAF}
+        by_id = self.leaf_node
         sel = self._selector()
         span = 1 << SELECTOR_WIDTH
         n = 0
@@ -993,7 +995,7 @@ class Solver:
                 break
         memo = {}
         new_roots = [self.rewrite(r, memo) for r in roots]
-        by_id = {n.id: n for n in self.lw.table.values() if n.op == I.LEAF}
+        by_id = self.leaf_node
         defs = {by_id[k].imm: self.rewrite(e, memo) for k, e in self.repl.items()}
         self.lw.birth = saved_birth
         return new_roots, defs
