@@ -272,7 +272,33 @@ def search_leafgen(prog: Program) -> List[LeafGen]:
     return [LeafGen(l.width, 0, n_c, 20, 40, 60) for l in prog.leaves]
 
 
+_SEARCH_CACHE: "OrderedDict[tuple, Program]" = None
+SEARCH_CACHE_SIZE = 2048
+
+
 def _compile_search(nodes: Sequence[N.Node], probes: Sequence[N.Node] = ()) -> Program:
+    """Search program of an independent group, cached: LASER's path
+    constraints grow one JUMPI at a time, so sibling and successive
+    ``is_possible`` queries share most of their groups (hash-consed nodes:
+    a group is identified by its node ids).  Compiled by
+    :func:`_compile_search_uncached`."""
+    global _SEARCH_CACHE
+    from collections import OrderedDict
+    if _SEARCH_CACHE is None:
+        _SEARCH_CACHE = OrderedDict()
+    key = (tuple(n.id for n in nodes), tuple(p.id for p in probes))
+    prog = _SEARCH_CACHE.get(key)
+    if prog is not None:
+        _SEARCH_CACHE.move_to_end(key)
+        return prog
+    prog = _compile_search_uncached(nodes, probes)
+    _SEARCH_CACHE[key] = prog
+    if len(_SEARCH_CACHE) > SEARCH_CACHE_SIZE:
+        _SEARCH_CACHE.popitem(last=False)
+    return prog
+
+
+def _compile_search_uncached(nodes: Sequence[N.Node], probes: Sequence[N.Node] = ()) -> Program:
     """Search program: solve mode (part of the model constructed), or — when
     its argument-keyed entries keep too many values live for the spill
     budget — the plain search form (every model value generated).
