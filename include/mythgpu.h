@@ -42,7 +42,9 @@ typedef struct mg_batch mg_batch;
 /* Device candidate generator for one leaf (free variable / table cell).
  * A draw r0 = SplitMix64(seed ^ salt ^ index * golden) picks a class by
  * mulhi(r0 >> 32, 100):
- *   < pct_uniform                    r0 + three more SplitMix64 words (masked to width)
+ *   < pct_uniform                    r0 in limbs 0-1; limb k = 2..7 is m ^ (m >> 16),
+ *                                    m = (x + k * 0x9E3779B9) * 0x85EBCA6B, x = lo(r0) ^ hi(r0)
+ *                                    (mod 2^32; masked to width)
  *   < pct_small                      r0 (< 2^64)
  *   < pct_boundary                   {0, 1, 2^(w-1), 2^w-1, 2^k+1, 2^k-1}
  *   otherwise                        consts[pool_off + e] + {-1, 0, +1}

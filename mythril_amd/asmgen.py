@@ -877,6 +877,7 @@ GOLD = 0x9E3779B97F4A7C15
 
 GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+GOLD32, LIMB_MUL = 0x9E3779B9, 0x85EBCA6B   # uniform limbs 2-7 (generator v4)
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_X, S_X + 6)
 
@@ -933,9 +934,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     """dst[0..7] (default X) <- generator value of leaf C for candidate
     first + lane; the boundary / pool lanes arrive by loads into dst, waited
     for unless wait=False (LEAFD: the translator places the WAITVM).
-    Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's words (the
-    class word r0, then three SplitMix64 words) are computed for every lane
-    (the small class is r0);
+    Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's value (the
+    class word r0 in limbs 0-1, limbs 2-7 mixed from it) is computed for
+    every lane (the small class is r0);
     the boundary and pool classes then overwrite their lanes under exec.
     Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
     pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
@@ -962,12 +963,19 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     sm64(a, st, z, tt)
     a("s_movk_i32 %s, 100" % s(S_T))
     a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), s(S_T)))
-    # ---- uniform words for every lane: r0 itself, then three SplitMix64
-    # words; small lanes keep the first 64 bits (r0)
+    # ---- uniform values for every lane: r0 in limbs 0-1 (small lanes keep
+    # only those), limbs 2-7 one multiply-xorshift each of x = lo ^ hi of r0
+    # plus k * golden32 (v4: 4 VALU per limb instead of a SplitMix64 word
+    # per two limbs)
     a("v_mov_b32 %s, %s" % (v(X[0]), v(z[0])))
     a("v_mov_b32 %s, %s" % (v(X[1]), v(z[1])))
-    for j in range(2, 8, 2):
-        sm64(a, st, [X[j], X[j + 1]], tt)
+    a("v_xor_b32 %s, %s, %s" % (v(tt[0]), v(z[0]), v(z[1])))
+    a("s_mov_b32 %s, 0x%x" % (s(K_M2_LO), LIMB_MUL))
+    for k in range(2, 8):
+        a("v_add_u32 %s, 0x%x, %s" % (v(X[k]), (k * GOLD32) & 0xFFFFFFFF, v(tt[0])))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(X[k]), v(X[k]), s(K_M2_LO)))
+        a("v_lshrrev_b32 %s, 16, %s" % (v(tt[1]), v(X[k])))
+        a("v_xor_b32 %s, %s, %s" % (v(X[k]), v(X[k]), v(tt[1])))
     _class_mask(a, S_T + 2, g + 3, g + 4, cls)                       # small
     lab = exec_begin(a, S_T + 2, S_T + 4)
     moves(a, X[2:], [None] * 6)

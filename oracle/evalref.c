@@ -480,8 +480,13 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
         else *out = p;
         for (int i = 4; i < L; ++i) out->w[i] = 0;
     } else {
-        out->w[0] = r0;                       /* v3: r0, then three words */
-        for (int i = 1; i < 4; ++i) out->w[i] = sm64(&s);
+        out->w[0] = r0;                       /* v4: r0, limbs 2-7 mixed from it */
+        uint32_t x = (uint32_t)r0 ^ (uint32_t)(r0 >> 32);
+        for (int k = 2; k < 8; ++k) {
+            uint32_t y = (x + (uint32_t)k * 0x9E3779B9u) * 0x85EBCA6Bu;
+            y ^= y >> 16;
+            out->w[k / 2] |= (uint64_t)y << (32 * (k & 1));
+        }
     }
     vmask(out, w);
 }

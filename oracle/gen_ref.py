@@ -42,8 +42,9 @@ def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
         delta = _mulhi((lo * 0x85EBCA6B) & 0xFFFFFFFF, 3)
         v = (pool[e] + delta - 1) % (1 << 256)
     else:
-        v = r0                                # v3: r0, then three SplitMix64 words
-        for j in range(1, 4):
-            s, r = _sm64(s)
-            v |= r << (64 * j)
+        v = r0                                # v4: r0, limbs 2-7 mixed from it
+        x = (r0 ^ (r0 >> 32)) & 0xFFFFFFFF
+        for k in range(2, 8):
+            y = (((x + k * 0x9E3779B9) & 0xFFFFFFFF) * 0x85EBCA6B) & 0xFFFFFFFF
+            v |= (y ^ (y >> 16)) << (32 * k)
     return v & mask

@@ -225,3 +225,23 @@ def test_leaf_pools_find_coupled_witness(engine):
     assert check(cs)
     m = M.get_model(tuple(cs), enforce_execution_time=False)
     assert [m[x.raw.params[0]] for x in xs] == vals
+
+
+def test_get_model_finds_the_bec_batch_overflow(engine):
+    """The drop-in get_model on the integer module's query for BECToken's
+    batchTransfer (two receivers: cnt * value wraps): the GPU search with
+    ABI presets and model construction returns a model, and the model —
+    presets included — satisfies the original query in the oracle."""
+    from mythril_amd.workloads import World, bv, ACTORS, _TOTAL, _BAL, _OWNER_PAUSED, _bec_batch
+    from mythril_amd.smt import Bool
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    supply = bv(7000000000 * 10 ** 18)
+    c.sstore(bv(_TOTAL), supply)
+    c.sstore(c.mapping(bv(ACTORS[0]), _BAL), supply)
+    c.sstore(bv(_OWNER_PAUSED), bv(ACTORS[0]))
+    t = w.tx()
+    checks = []
+    _bec_batch(t, checks, 2)
+    q = [Bool(n) for n in w.query([checks[0]])]
+    assert check(q), "GPU search missed the BEC overflow"
