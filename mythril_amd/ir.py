@@ -937,18 +937,6 @@ def lw_tables(constraints, probes) -> set:
     return out
 
 
-def _conjuncts(n: LNode) -> List[LNode]:
-    """The top-level conjuncts of a lowered Bool (AND trees of width 1)."""
-    out, stack = [], [n]
-    while stack:
-        x = stack.pop()
-        if x.op == I.AND and x.width == 1:
-            stack.extend(reversed(x.args))
-        else:
-            out.append(x)
-    return out
-
-
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
