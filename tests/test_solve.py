@@ -209,3 +209,33 @@ def test_bec_batch_overflow_is_found():
         assert root == R.eval_constraints(g, R.Assignment(a.vars, a.arrays, a.funcs)), idx
         hits += root
     assert hits > 0
+
+
+@pytest.mark.parametrize("start", [0, 40, 80])
+def test_solve_mode_sound_on_random_dags(start):
+    """Fuzz: the C2 generator's random DAGs (every operator, arrays, 64-512
+    nodes) compiled in search mode — folding, interval reasoning and every
+    definition rule applied to shapes no workload builder produces.  On
+    every candidate the program's root bit equals the oracle's verdict on
+    the unpacked model of the ORIGINAL constraints."""
+    from mythril_amd.corpus import make_dag
+    from mythril_amd.ir import Unsupported
+    checked = 0
+    for d in range(start, start + 40):
+        roots, _ = make_dag(d)
+        try:
+            prog = compile_constraints(roots, const_keys=True, leaf_pools=True, solve=True)
+        except Unsupported:
+            continue
+        table = [sum(int(prog.consts[i, j]) << (32 * j) for j in range(8))
+                 for i in range(prog.consts.shape[0])]
+        for idx in range(6):
+            lv = [gen_ref.gen_leaf(5, d, li, idx, l.width,
+                                   table[prog.pool_ranges[li][0]:sum(prog.pool_ranges[li])],
+                                   pct=(20, 40, 60)) for li, l in enumerate(prog.leaves)]
+            root, probes = ir_sim.run(prog, lv)
+            a = unpack(prog, _pack1(lv), _pack1(probes))
+            assert root == R.eval_constraints(roots, R.Assignment(a.vars, a.arrays, a.funcs)), \
+                (d, idx)
+        checked += 1
+    assert checked >= 30
