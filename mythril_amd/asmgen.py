@@ -173,12 +173,27 @@ class Asm:
     def __init__(self):
         self.lines: List[str] = []
         self._n = 0
+        self._hot: Optional[List[str]] = None
+        self._cold: List[str] = []
 
     def __call__(self, text: str):
         self.lines.append("    " + text)
 
     def label(self, name: str):
         self.lines.append(name + ":")
+
+    def cold(self):
+        """Following lines go out of line (a rarely taken block), until
+        :meth:`hot`; :meth:`flush_cold` places them after the body's final
+        dispatch, so the common path runs straight through."""
+        self._hot, self.lines = self.lines, self._cold
+
+    def hot(self):
+        self.lines, self._hot = self._hot, None
+
+    def flush_cold(self):
+        self.lines.extend(self._cold)
+        self._cold = []
 
     def uniq(self, stem: str) -> str:
         self._n += 1
@@ -1474,6 +1489,9 @@ def body_shift(a: Asm, kind: str):
 # b/c = T2/T3 (b kept for the remainder); digit temps T4..T11.
 
 DIV_M = {4: 48, 2: 50, 1: 52}   # limb-shift stage masks (bank B: free in heavy bodies)
+DIV_Z6 = 54                     # lanes with vn[0..5] == 0 (bank B)
+DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm:
+                                # unused by division)
 
 
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
@@ -1529,6 +1547,15 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     for st in (4, 2, 1):
         live = _stage(a, un, st, 16, True, DIV_M[st], live)
     bitshift_left(a, un, c, bz, 17, S_T)
+    # lanes whose normalised divisor has its low 4 / 6 digits zero: a
+    # quotient digit's multiply-subtract starts at digit 4 / 6 when every
+    # lane with a nonzero digit is one of them (qh * 0 changes nothing)
+    t = T[4]
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(vn[0]), v(vn[1]), v(vn[2])))
+    a("v_or_b32 %s, %s, %s" % (v(t), v(t), v(vn[3])))
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(DIV_Z4), v(t)))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(vn[4]), v(vn[5])))
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(DIV_Z6), v(t)))
     d = vn[7]
     # dinv = floor((2^64-1)/d) - 2^32 (d >= 2^31): f64 reciprocal, one
     # Newton step (the estimate is then within one of the exact value), then
@@ -1608,30 +1635,48 @@ def _div_digit(a: Asm, un, vn, j, d, dinv):
     # lanes with u2 == d: qhat = b - 1.  qhat is now at most two above the
     # true digit (Knuth's Theorem B, normalised divisor); the add-back below
     # runs at most twice, and only for waves with a lane that needs it
-    lab_nb = a.uniq("dnb")
-    a("s_cmp_eq_u64 %s, -1" % lt)
-    a("s_cbranch_scc1 %s" % lab_nb)
     a("v_cndmask_b32_e64 %s, -1, %s, %s" % (v(QH), v(QH), lt))
-    a.label(lab_nb)
     # multiply-subtract un[j..j+8] -= qh * vn as one borrow chain in vcc:
-    # P = qh * vn[i] + carry (carry pair CR:RH with RH = 0), un[j+i] -= P.lo
-    for i in range(8):
-        add = "0" if i == 0 else "v[%d:%d]" % (CR, RH)
-        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (P0, P1, sp(st + 6), v(QH), v(vn[i]), add))
-        a("v_mov_b32 %s, %s" % (v(CR), v(P1)))
-        if i == 0:
-            a("v_sub_co_u32 %s, vcc, %s, %s" % (v(un[j]), v(un[j]), v(P0)))
-        else:
-            a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
+    # P = qh * vn[i] + carry (carry pair CR:RH with RH = 0), un[j+i] -= P.lo.
+    # In line the chain covers digits 6, 7 only: enough when every lane with
+    # qh != 0 has vn[0..5] == 0 (qh * 0 changes nothing); otherwise an out-of-
+    # line chain from digit 4 (vn[0..3] == 0) or 0 runs instead.
+    lab_wide, lab_full, lab_join = a.uniq("dmw"), a.uniq("dmf"), a.uniq("dmj")
+    a("v_cmp_ne_u32_e64 %s, 0, %s" % (lt, v(QH)))
+    a("s_andn2_b64 %s, %s, %s" % (sp(st + 2), lt, sp(DIV_Z6)))
+    a("s_cbranch_scc1 %s" % lab_wide)
+
+    def chain(first):
+        for i in range(first, 8):
+            add = "0" if i == first else "v[%d:%d]" % (CR, RH)
+            a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (P0, P1, sp(st + 6), v(QH), v(vn[i]), add))
+            a("v_mov_b32 %s, %s" % (v(CR), v(P1)))
+            if i == first:
+                a("v_sub_co_u32 %s, vcc, %s, %s" % (v(un[j + i]), v(un[j + i]), v(P0)))
+            else:
+                a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(un[j + i]), v(un[j + i]), v(P0)))
+    chain(6)
+    a.label(lab_join)
     a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(u2), v(u2), v(CR)))
     # borrow lanes went negative: quotient digit qh - 1 and add vn back under
-    # exec (rare); without Knuth's test qh can be two too big: lanes with no
-    # carry out of the first add-back take a second one
+    # exec (rare, out of line); without Knuth's test qh can be two too big:
+    # lanes with no carry out of the first add-back take a second one
     a("s_mov_b64 %s, vcc" % sp(st + 4))
     a("v_subb_co_u32 %s, vcc, %s, 0, vcc" % (v(u2), v(QH)))       # digit into the dead top
-    lab, lab_x = a.uniq("dab"), a.uniq("dax")
-    a("s_cmp_eq_u64 %s, 0" % sp(st + 4))
-    a("s_cbranch_scc1 %s" % lab)
+    lab_ab, lab_x, lab_ret = a.uniq("dab"), a.uniq("dax"), a.uniq("dar")
+    a("s_cmp_lg_u64 %s, 0" % sp(st + 4))
+    a("s_cbranch_scc1 %s" % lab_ab)
+    a.label(lab_ret)
+    a.cold()
+    a.label(lab_wide)
+    a("s_andn2_b64 %s, %s, %s" % (sp(st + 2), lt, sp(DIV_Z4)))
+    a("s_cbranch_scc1 %s" % lab_full)
+    chain(4)
+    a("s_branch %s" % lab_join)
+    a.label(lab_full)
+    chain(0)
+    a("s_branch %s" % lab_join)
+    a.label(lab_ab)
     a("s_mov_b64 %s, exec" % sp(st + 2))
     a("s_mov_b64 exec, %s" % sp(st + 4))
     for rnd in range(2):
@@ -1644,7 +1689,8 @@ def _div_digit(a: Asm, un, vn, j, d, dinv):
             a("v_add_u32 %s, -1, %s" % (v(u2), v(u2)))
     a.label(lab_x)
     a("s_mov_b64 exec, %s" % sp(st + 2))
-    a.label(lab)
+    a("s_branch %s" % lab_ret)
+    a.hot()
 
 
 def _cond_neg(a: Asm, regs: List[int], m: int):
@@ -1749,6 +1795,7 @@ def body_div(a: Asm):
     exec_end(a, lab, S_T + 2)
     a.label(lab_end)
     heavy_finish(a, R)
+    a.flush_cold()
 
 
 # ---------------------------------------------------------------------------

@@ -128,7 +128,8 @@ class Engine:
     """One HIP device context (one per host thread)."""
 
     def __init__(self, device: int = 0, lib_path: str = _LIB_PATH):
-        self.lib = load_library(lib_path)
+        # an A/B build elsewhere may carry another assembly interpreter
+        self.lib = load_library(lib_path, check_digest=lib_path == _LIB_PATH)
         ctx = C.c_void_p()
         rc = self.lib.mg_init(device, C.byref(ctx))
         if rc != 0:

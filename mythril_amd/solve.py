@@ -270,20 +270,28 @@ class Solver:
         """``n`` with every defined leaf replaced by its definition (followed
         transitively) and folded.  A node that is already a rewrite result
         (``clean``: folding cannot change it) over undefined leaves only is
-        its own result — the walk does not enter it."""
+        its own result — the walk does not enter it.
+
+        ``memo`` may outlive definitions: an entry stays valid while no leaf
+        of its result has been defined since (results hold undefined leaves
+        only), so a pass re-folds just the nodes a new definition reaches."""
         dm = self._defmask()
-        clean, dep = self.clean, self._dep
+        clean, dep, get = self.clean, self._dep, memo.get
         stack = [(n, False)]
         while stack:
             x, done = stack.pop()
-            if x.id in memo:
-                continue
+            if not done:
+                r = get(x.id)
+                if r is not None and not dep(r) & dm:
+                    continue
             if x.op == I.LEAF:
                 e = self.repl.get(x.id)
                 if e is None:
                     memo[x.id] = x
-                elif e.id in memo:
-                    memo[x.id] = memo[e.id]
+                    continue
+                r = get(e.id)
+                if r is not None and not dep(r) & dm:
+                    memo[x.id] = r
                 else:
                     stack.append((x, False))
                     stack.append((e, False))
@@ -296,7 +304,10 @@ class Solver:
                     memo[x.id] = x
                     continue
                 stack.append((x, True))
-                stack.extend((a, False) for a in x.args if a.id not in memo)
+                for a in x.args:
+                    r = get(a.id)
+                    if r is None or dep(r) & dm:
+                        stack.append((a, False))
                 continue
             r = self._fold(x, tuple(memo[a.id] for a in x.args))
             clean.add(r.id)
@@ -967,22 +978,20 @@ class Solver:
         # query's last constraint; its wrap-around choice must win over the
         # bounds the path constraints put on the same operands)
         order = sorted(roots, key=lambda r: not self._is_wrap_test(r))
+        # one memo for the whole run: rewrite drops the entries a new
+        # definition reaches (later roots see the new definitions folded)
+        memo: Dict[int, object] = {}
         for _ in range(PASSES):
-            memo: Dict[int, object] = {}
             found = 0
             every = []
             for r in order:
                 atoms = self._atoms(r, memo)
                 every += atoms
-                k = self._define(atoms)
-                if k:                   # later roots see the new definitions folded
-                    memo = {}
-                found += k
+                found += self._define(atoms)
             # intervals from the bounds of all conjuncts together: per
             # expression (x >= 2 from one constraint, x <= 2 from another make
             # x = 2 — through a concat, its low byte), then per leaf
             if found:
-                memo = {}
                 every = [self.rewrite(a, memo) for a in every]
             extra = []
             for part in self._joint_bounds(every):     # one by one: a violated
@@ -993,7 +1002,6 @@ class Solver:
             found += self._ranges(every)
             if not found:
                 break
-        memo = {}
         new_roots = [self.rewrite(r, memo) for r in roots]
         by_id = self.leaf_node
         defs = {by_id[k].imm: self.rewrite(e, memo) for k, e in self.repl.items()}

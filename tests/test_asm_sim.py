@@ -83,6 +83,30 @@ def test_division_edges_with_reciprocal_noise():
             assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
 
 
+@pytest.mark.parametrize("spans", [(1, 33, 64), (65, 100, 128), (1, 64, 128), (1, 64, 256)])
+def test_division_short_divisor_chains(spans):
+    """Waves whose divisors span few digits (any position, after
+    normalisation: the multiply-subtract enters at digit 6 or 4 when every
+    lane with a nonzero quotient digit allows it), mixed with zero-quotient
+    lanes of wide divisors."""
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    probes = [N.bv_op(op, x, y) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    prog = compile_constraints([], probes)
+    rng = random.Random(sum(spans))
+    for rep in range(2):
+        asgs = []
+        for _ in range(64):
+            span = rng.choice(spans)
+            yv = (rng.getrandbits(span) | 1 << (span - 1)) << rng.randrange(0, 257 - span)
+            xv = rng.getrandbits(256) if rng.random() < 0.8 else rng.getrandbits(rng.randrange(1, 256))
+            asgs.append(PA(vars={"x": xv, "y": yv}))
+        root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+        for a, asg in enumerate(asgs):
+            want = R.evaluate(probes, R.Assignment(asg.vars))
+            got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+            assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
+
+
 def _max_qhat_error(x: int, y: int) -> int:
     """Largest (estimate - true digit) of Knuth D's two-digit quotient
     estimate over the digits of x / y (32-bit digits, normalised)."""
