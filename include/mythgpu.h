@@ -40,7 +40,7 @@ typedef struct mg_prog mg_prog;
 typedef struct mg_batch mg_batch;
 
 /* Device candidate generator for one leaf (free variable / table cell).
- * A draw r0 = SplitMix64(seed ^ salt ^ index * golden) picks a class by
+ * A draw r0 = SplitMix64(seed ^ salt ^ index) picks a class by
  * mulhi(r0 >> 32, 100):
  *   < pct_uniform                    r0 in limbs 0-1; limb k = 2..7 is m ^ (m >> 16),
  *                                    m = (x + k * 0x9E3779B9) * 0x85EBCA6B, x = lo(r0) ^ hi(r0)

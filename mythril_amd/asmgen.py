@@ -892,7 +892,7 @@ GOLD = 0x9E3779B97F4A7C15
 
 GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
-GOLD32, LIMB_MUL = 0x9E3779B9, 0x85EBCA6B   # uniform limbs 2-7 (generator v4)
+GOLD32, LIMB_MUL = 0x9E3779B9, 0x85EBCA6B   # uniform limbs 2-7 (generator v4/v5)
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_X, S_X + 6)
 
@@ -964,12 +964,12 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     load_sm64_consts(a)
     a("s_waitcnt lgkmcnt(0)")
     a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
-    # idx = first + lane ; st = seed ^ salt ^ idx * GOLD
+    # idx = first + lane ; st = seed ^ salt ^ idx (v5: the counter itself,
+    # SplitMix64's finaliser spreads it; no idx * GOLD multiply)
     a("s_mov_b64 %s, %s" % (sp(S_T + 4), IN["first"]))
     a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(S_T + 4), OP_LANE_LO))
     a("v_mov_b32 %s, %s" % (v(st[1]), s(S_T + 5)))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(st[1]), OP_LANE_HI))
-    mul64_const(a, st, K_GOLD_LO, K_GOLD_HI, tt)
     a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
     a("s_waitcnt lgkmcnt(0)")
     a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(g + 6)))
@@ -982,22 +982,20 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     # only those), limbs 2-7 one multiply-xorshift each of x = lo ^ hi of r0
     # plus k * golden32 (v4: 4 VALU per limb instead of a SplitMix64 word
     # per two limbs)
-    a("v_mov_b32 %s, %s" % (v(X[0]), v(z[0])))
-    a("v_mov_b32 %s, %s" % (v(X[1]), v(z[1])))
+    # (built straight in dst: a LEAFD's slot)
+    dst = X if dst is None else dst
+    a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(tt[0]), v(z[0]), v(z[1])))
     a("s_mov_b32 %s, 0x%x" % (s(K_M2_LO), LIMB_MUL))
     for k in range(2, 8):
-        a("v_add_u32 %s, 0x%x, %s" % (v(X[k]), (k * GOLD32) & 0xFFFFFFFF, v(tt[0])))
-        a("v_mul_lo_u32 %s, %s, %s" % (v(X[k]), v(X[k]), s(K_M2_LO)))
-        a("v_lshrrev_b32 %s, 16, %s" % (v(tt[1]), v(X[k])))
-        a("v_xor_b32 %s, %s, %s" % (v(X[k]), v(X[k]), v(tt[1])))
+        a("v_add_u32 %s, 0x%x, %s" % (v(dst[k]), (k * GOLD32) & 0xFFFFFFFF, v(tt[0])))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(dst[k]), v(dst[k]), s(K_M2_LO)))
+        a("v_lshrrev_b32 %s, 16, %s" % (v(tt[1]), v(dst[k])))
+        a("v_xor_b32 %s, %s, %s" % (v(dst[k]), v(dst[k]), v(tt[1])))
     _class_mask(a, S_T + 2, g + 3, g + 4, cls)                       # small
     lab = exec_begin(a, S_T + 2, S_T + 4)
-    moves(a, X[2:], [None] * 6)
+    moves(a, dst[2:], [None] * 6)
     exec_end(a, lab, S_T + 4)
-    dst = X if dst is None else dst
-    if dst != X:
-        moves(a, dst, X)
     # ---- boundary: pct_small <= cls < pct_boundary -------------------------
     _class_mask(a, S_T + 2, g + 4, g + 5, cls)
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))

@@ -447,7 +447,7 @@ static uint64_t sm64(uint64_t* s) {
 static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t idx, uint32_t w,
                      const uint64_t* pool, uint32_t pool_n, const uint32_t pct[3], V* out) {
     uint64_t s = seed ^ (prog_seed * 0xD1B54A32D192ED03ull) ^
-                 ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull) ^ (idx * 0x9E3779B97F4A7C15ull);
+                 ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull) ^ idx;   /* v5 */
     uint64_t r0 = sm64(&s);
     /* v2 range reduction: multiply-high (Lemire) instead of modulo */
     uint32_t cls = mulhi32((uint32_t)(r0 >> 32), 100u), lo = (uint32_t)r0;

@@ -24,7 +24,7 @@ def _sm64(s):
 def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
              pct=(50, 70, 85)) -> int:
     s = (seed ^ ((prog_seed * 0xD1B54A32D192ED03) & M64) ^
-         (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64) ^ ((idx * 0x9E3779B97F4A7C15) & M64)) & M64
+         (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64) ^ idx) & M64    # v5: idx itself
     s, r0 = _sm64(s)
     # v2 range reduction: multiply-high (Lemire), no modulo
     cls = _mulhi(r0 >> 32, 100)
