@@ -854,13 +854,30 @@ def _soa_step(a: Asm):
     a("s_addc_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 1), s(S_T + 5)))
 
 
-def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int, wait_vm: bool = False):
+def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int, wait_vm: bool = False,
+               cold: bool = False):
     """regs -> SoA buffer ptr[(8*row + j) * stride + lane], active lanes only,
-    when ptr != 0 (after the in-flight loads into regs with wait_vm).
-    Clobbers S_T..S_T+7, T[0]."""
+    when ptr != 0 (after the in-flight loads into regs with wait_vm); with
+    ``cold`` the store is out of line (the caller flushes it) and the
+    ptr == 0 case runs straight through.  Clobbers S_T..S_T+7, T[0]."""
     skip = a.uniq("nost")
     a("s_cmp_lg_u64 %s, 0" % ptr_op)
+    if cold:
+        lab = a.uniq("sst")
+        a("s_cbranch_scc1 %s" % lab)
+        a.label(skip)
+        a.cold()
+        a.label(lab)
+        _store_soa_body(a, regs, ptr_op, row_sgpr, wait_vm)
+        a("s_branch %s" % skip)
+        a.hot()
+        return
     a("s_cbranch_scc0 %s" % skip)
+    _store_soa_body(a, regs, ptr_op, row_sgpr, wait_vm)
+    a.label(skip)
+
+
+def _store_soa_body(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int, wait_vm: bool):
     if wait_vm:
         a("s_waitcnt vmcnt(0)")
     _soa_base(a, ptr_op, row_sgpr)
@@ -872,7 +889,6 @@ def _store_soa(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int, wait_vm: boo
         if j < 7:
             _soa_step(a)
     a("s_mov_b64 exec, %s" % sp(S_T + 6))
-    a.label(skip)
 
 
 def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
@@ -1046,9 +1062,19 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     if mask:
         load_masks(a, fld(bank, F_MOFF))
-    lab_gen, lab_done = a.uniq("lgen"), a.uniq("ldone")
+    lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
     a("s_bitcmp1_b32 %s, 0" % IN["mode"])
-    a("s_cbranch_scc1 %s" % lab_gen)
+    a("s_cbranch_scc0 %s" % lab_mem)                 # (generator mode in line)
+    _gen_leaf(a, bank)
+    if mask:
+        a("s_waitcnt lgkmcnt(0)")
+        for j in range(8):
+            a("v_and_b32 %s, %s, %s" % (v(X[j]), s(S_M + j), v(X[j])))
+    _store_soa(a, X, IN["lout"], fld(bank, F_C), cold=True)
+    a.label(lab_done)
+    finish(a, bank, X, root, mask)
+    a.cold()
+    a.label(lab_mem)
     _soa_base(a, IN["leaves"], fld(bank, F_C))
     a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
     for j in range(8):
@@ -1057,15 +1083,8 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
             _soa_step(a)
     a("s_waitcnt vmcnt(0)")
     a("s_branch %s" % lab_done)
-    a.label(lab_gen)
-    _gen_leaf(a, bank)
-    if mask:
-        a("s_waitcnt lgkmcnt(0)")
-        for j in range(8):
-            a("v_and_b32 %s, %s, %s" % (v(X[j]), s(S_M + j), v(X[j])))
-    _store_soa(a, X, IN["lout"], fld(bank, F_C))
-    a.label(lab_done)
-    finish(a, bank, X, root, mask)
+    a.hot()
+    a.flush_cold()
 
 
 def _wait_if_flagged(a: Asm, bank: int):
@@ -1088,9 +1107,16 @@ def h_leafd(a: Asm, bank: int, var: int):
     slot = var
     fd = [FB + 8 * slot + j for j in range(8)]
     prologue(a, bank)
-    lab_gen, lab_done = a.uniq("lgen"), a.uniq("ldone")
+    lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
     a("s_bitcmp1_b32 %s, 0" % IN["mode"])
-    a("s_cbranch_scc1 %s" % lab_gen)
+    a("s_cbranch_scc0 %s" % lab_mem)                 # (generator mode in line)
+    _gen_leaf(a, bank, dst=fd, wait=False)
+    _store_soa(a, fd, IN["lout"], fld(bank, F_C), wait_vm=True, cold=True)
+    a.label(lab_done)
+    _wait_if_flagged(a, bank)
+    dispatch(a, 1 - bank)
+    a.cold()
+    a.label(lab_mem)
     _soa_base(a, IN["leaves"], fld(bank, F_C))
     a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
     for j in range(8):
@@ -1098,12 +1124,8 @@ def h_leafd(a: Asm, bank: int, var: int):
         if j < 7:
             _soa_step(a)
     a("s_branch %s" % lab_done)
-    a.label(lab_gen)
-    _gen_leaf(a, bank, dst=fd, wait=False)
-    _store_soa(a, fd, IN["lout"], fld(bank, F_C), wait_vm=True)
-    a.label(lab_done)
-    _wait_if_flagged(a, bank)
-    dispatch(a, 1 - bank)
+    a.hot()
+    a.flush_cold()
 
 
 def h_reloadd(a: Asm, bank: int, var: int):
@@ -1186,21 +1208,28 @@ def heavy_prologue(a: Asm):
 
 
 def heavy_finish(a: Asm, res: List[int]):
-    """Write (masked when variant bit1), fold ROOT when bit0, dispatch (A)."""
-    lab_nm, lab_done, lab_nr = a.uniq("hnm"), a.uniq("hwd"), a.uniq("hnr")
+    """Write (masked when variant bit1), fold ROOT when bit0, dispatch (A).
+    The unmasked, non-root case runs straight through (no taken branch);
+    the other two are out of line, placed after the dispatch."""
+    lab_m, lab_wd, lab_r, lab_nr = a.uniq("hm"), a.uniq("hwd"), a.uniq("hr"), a.uniq("hnr")
     a("s_waitcnt lgkmcnt(0)")
     a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
-    a("s_cbranch_scc0 %s" % lab_nm)
-    a.write_slot(res, cur(F_D), S_M)
-    a("s_branch %s" % lab_done)
-    a.label(lab_nm)
+    a("s_cbranch_scc1 %s" % lab_m)
     a.write_slot(res, cur(F_D), None)
-    a.label(lab_done)
+    a.label(lab_wd)
     a("s_bitcmp1_b32 %s, 0" % s(S_VAR))
-    a("s_cbranch_scc0 %s" % lab_nr)
-    a.root_and(v(res[0]))
+    a("s_cbranch_scc1 %s" % lab_r)
     a.label(lab_nr)
     dispatch(a, 0)
+    a.cold()
+    a.label(lab_m)
+    a.write_slot(res, cur(F_D), S_M)
+    a("s_branch %s" % lab_wd)
+    a.label(lab_r)
+    a.root_and(v(res[0]))
+    a("s_branch %s" % lab_nr)
+    a.hot()
+    a.flush_cold()
 
 
 def col_product(a: Asm, x: List[int], y: List[int], ncols: int, out: Optional[List[int]] = None,
@@ -1267,13 +1296,17 @@ def low_product(a: Asm, x: List[int], y: List[int], out: List[int]):
                 A0, A1, out[c], out[c + 1], "0" if c == 0 else "v[%d:%d]" % (A2, A2 + 1)))
 
 
-def body_mul(a: Asm):
-    a.label(".Lbody_MUL_%=")
-    heavy_prologue(a)
-    a.read_slot(X, cur(F_A))
-    a.read_slot(Y, cur(F_B))
+def h_mul(a, bank, root, mask, dc=False, w32=False, ip=False):
+    """MUL in line in each (variant, bank) handler, unlike the other heavy
+    ops: no record copy, no branch to a shared body, no run-time variant
+    tests (the most frequent heavy op; ~100 instructions per copy)."""
+    prologue(a, bank)
+    if mask:
+        load_masks(a, fld(bank, F_MOFF))
+    a.read_slot(X, fld(bank, F_A))
+    a.read_slot(Y, fld(bank, F_B))
     low_product(a, X, Y, R)
-    heavy_finish(a, R)
+    finish(a, bank, R, root, mask)
 
 
 def clz256(a: Asm, vals: List[int], out: int, t: List[int]):
@@ -1420,29 +1453,37 @@ def bitshift_left(a: Asm, t: List[int], c: int, bz: int, nl: int, save: int):
     exec_end(a, lab, save)
 
 
-def body_shift(a: Asm, kind: str):
-    """SHL / LSHR / ASHR of F[a] by F[b] at width W."""
-    a.label(".Lbody_%s_%%=" % kind)
-    heavy_prologue(a)
-    a.read_slot(X, cur(F_A))
-    a.read_slot(Y, cur(F_B))
-    a("s_waitcnt lgkmcnt(0)")
+def h_shift(kind: str):
+    """SHL / LSHR / ASHR of F[a] by F[b] at width W, in line in each
+    (variant, bank) handler (like MUL: no shared body, static variant)."""
+    def h(a, bank, root, mask, dc=False, w32=False, ip=False):
+        prologue(a, bank)
+        if mask:
+            load_masks(a, fld(bank, F_MOFF))
+        shift_core(a, kind, fld(bank, F_A), fld(bank, F_B), fld(bank, F_W), mask)
+        finish(a, bank, X, root, mask and kind != "LSHR")   # LSHR: canonical
+    return h
+
+
+def shift_core(a: Asm, kind: str, fa: int, fb: int, fw: int, masked: bool):
+    """X = F[fa] shifted by F[fb] at the width in s[fw]; ASHR sign-extends
+    from that width first when ``masked`` (the masks S_M are loading)."""
+    a.read_slot(X, fa)
+    a.read_slot(Y, fb)
     over = S_X                     # s[88:89] lanes shifting by >= W
     a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(Y[1]), v(Y[2]), v(Y[3])))
     a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(T[0]), v(Y[4]), v(Y[5])))
     a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(T[0]), v(Y[6]), v(Y[7])))
     a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(over), v(T[0])))
-    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), s(cur(F_W)), v(Y[0])))
+    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), s(fw), v(Y[0])))
     a("s_or_b64 %s, %s, %s" % (sp(over), sp(over), sp(S_T)))
     a("v_bfe_u32 %s, %s, 5, 3" % (v(T[2]), v(Y[0])))         # q (over lanes masked later)
     a("v_and_b32 %s, 31, %s" % (v(T[3]), v(Y[0])))          # b
     fill = None
     if kind == "ASHR":
-        lab = a.uniq("asx")
-        a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
-        a("s_cbranch_scc0 %s" % lab)
-        sext(a, X, cur(F_W), S_M, T[4], S_T)
-        a.label(lab)
+        if masked:
+            a("s_waitcnt lgkmcnt(0)")
+            sext(a, X, fw, S_M, T[4], S_T)
         a("v_ashrrev_i32 %s, 31, %s" % (v(T[4]), v(X[7])))
         for j in range(8):
             a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[4])))
@@ -1469,9 +1510,6 @@ def body_shift(a: Asm, kind: str):
     lab = exec_begin(a, over, S_T)                   # shift >= W: 0 or sign fill
     moves(a, X, [None if fill is None else T[4 + (j & 1)] for j in range(8)])
     exec_end(a, lab, S_T)
-    if kind == "LSHR":
-        a("s_and_b32 %s, %s, 1" % (s(S_VAR), s(S_VAR)))     # canonical: no mask needed
-    heavy_finish(a, X)
 
 
 # ---- division ---------------------------------------------------------------
@@ -1806,10 +1844,11 @@ CHEAP = {
     "XOR": h_xor, "NOT": h_not, "EQ": h_eq, "ULT": h_ult, "ULE": h_ule, "SLT": h_slt,
     "SLE": h_sle, "ITE": h_ite, "CONCAT": h_concat, "EXTRACT": h_extract, "SEXT": h_sext,
     "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov, "SUBR": h_subr, "ITEN": h_iten,
-    "WAITVM": h_waitvm,
+    "WAITVM": h_waitvm, "MUL": h_mul,
+    "SHL": h_shift("SHL"), "LSHR": h_shift("LSHR"), "ASHR": h_shift("ASHR"),
 }
 SLOT_HANDLERS = {"SPILL_LDS": h_spill_lds, "SPILL_SCR": h_spill_scr, "RELOAD_LDS": h_reload_lds}
-HEAVY = {"MUL": "MUL", "UMULNO": "UMULNO", "SHL": "SHL", "LSHR": "LSHR", "ASHR": "ASHR",
+HEAVY = {"UMULNO": "UMULNO",
          "UDIV": "DIV", "UREM": "DIV", "SDIV": "DIV", "SREM": "DIV", "SMOD": "DIV"}
 HEAVY_AOPS = sorted(AOP[n] for n in HEAVY)
 
@@ -1867,10 +1906,7 @@ def generate() -> List[str]:
                 else:
                     bits = var | (DIV_CODE.get(name, 0) << 4)
                     heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
-    body_mul(a)
     body_umulno(a)
-    for k in ("SHL", "LSHR", "ASHR"):
-        body_shift(a, k)
     body_div(a)
     a.label(".Lexit_%=")
     a("s_set_gpr_idx_off")
