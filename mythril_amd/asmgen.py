@@ -63,6 +63,10 @@ S_M0 = S_X + 7             # m0 (GPR-index register) saved across the asm
 S_LAST = S_X + 7
 
 F_OFF, F_D, F_A, F_B, F_C, F_IMM, F_W, F_MOFF = range(8)
+# LEAFD records carry the leaf's generator parameters (mg_load_program
+# patches them in): pool offset, salt pair, pool size, thresholds
+# (uniform | small << 8 | boundary << 16); C is the leaf index, W the wait flag
+LEAFD_POFF, LEAFD_SALT, LEAFD_PN, LEAFD_PCT = 1, 2, 5, 7
 
 AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", "RELOAD_SCR",
         "ADD", "SUB", "MUL", "UDIV", "UREM", "SDIV", "SREM", "SMOD", "AND", "OR", "XOR",
@@ -970,16 +974,32 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     every lane (the small class is r0);
     the boundary and pool classes then overwrite their lanes under exec.
     Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
-    pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi."""
+    pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi.  A
+    LEAFD (``in_record``: 256 bits) finds them in its own record instead
+    (mg_load_program: pool_off, salt, pool_n, packed thresholds), so no
+    descriptor load sits between dispatch and the generator."""
     st, z, tt = [T[0], T[1]], [T[2], T[3]], [T[4], T[5], T[6], T[7]]
     cls, lo = T[8], z[0]
     g = S_CUR
-    a("s_load_dwordx2 %s, %s, 0x10" % (sp(S_T), IN["desc"]))       # gen table
+    in_record = dst is not None and dst != X
     a("s_load_dwordx2 %s, %s, 0x38" % (sp(S_T + 6), IN["desc"]))   # boundary table
-    a("s_lshl_b32 %s, %s, 5" % (s(S_T + 2), s(fld(bank, F_C))))
-    load_sm64_consts(a)
-    a("s_waitcnt lgkmcnt(0)")
-    a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
+    if in_record:
+        f = {"w": g + 0, "poff": fld(bank, LEAFD_POFF), "pn": fld(bank, LEAFD_PN),
+             "pu": g + 3, "ps": g + 4, "pb": g + 5, "salt": fld(bank, LEAFD_SALT)}
+        a("s_movk_i32 %s, 0x100" % s(f["w"]))
+        pk = fld(bank, LEAFD_PCT)
+        a("s_and_b32 %s, %s, 0xff" % (s(f["pu"]), s(pk)))
+        a("s_bfe_u32 %s, %s, 0x80008" % (s(f["ps"]), s(pk)))
+        a("s_bfe_u32 %s, %s, 0x80010" % (s(f["pb"]), s(pk)))
+        load_sm64_consts(a)
+    else:
+        f = {"w": g + 0, "poff": g + 1, "pn": g + 2, "pu": g + 3, "ps": g + 4, "pb": g + 5,
+             "salt": g + 6}
+        a("s_load_dwordx2 %s, %s, 0x10" % (sp(S_T), IN["desc"]))       # gen table
+        a("s_lshl_b32 %s, %s, 5" % (s(S_T + 2), s(fld(bank, F_C))))
+        load_sm64_consts(a)
+        a("s_waitcnt lgkmcnt(0)")
+        a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
     # idx = first + lane ; st = seed ^ salt ^ idx (v5: the counter itself,
     # SplitMix64's finaliser spreads it; no idx * GOLD multiply)
     a("s_mov_b64 %s, %s" % (sp(S_T + 4), IN["first"]))
@@ -987,8 +1007,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_mov_b32 %s, %s" % (v(st[1]), s(S_T + 5)))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(st[1]), OP_LANE_HI))
     a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
-    a("s_waitcnt lgkmcnt(0)")
-    a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(g + 6)))
+    if not in_record:
+        a("s_waitcnt lgkmcnt(0)")
+    a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(f["salt"])))
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), v(st[0])))
     a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), v(st[1])))
     sm64(a, st, z, tt)
@@ -1008,15 +1029,17 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a("v_mul_lo_u32 %s, %s, %s" % (v(dst[k]), v(dst[k]), s(K_M2_LO)))
         a("v_lshrrev_b32 %s, 16, %s" % (v(tt[1]), v(dst[k])))
         a("v_xor_b32 %s, %s, %s" % (v(dst[k]), v(dst[k]), v(tt[1])))
-    _class_mask(a, S_T + 2, g + 3, g + 4, cls)                       # small
+    _class_mask(a, S_T + 2, f["pu"], f["ps"], cls)                   # small
     lab = exec_begin(a, S_T + 2, S_T + 4)
     moves(a, dst[2:], [None] * 6)
     exec_end(a, lab, S_T + 4)
     # ---- boundary: pct_small <= cls < pct_boundary -------------------------
-    _class_mask(a, S_T + 2, g + 4, g + 5, cls)
+    _class_mask(a, S_T + 2, f["ps"], f["pb"], cls)
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     lab = a.uniq("gbd")
     a("s_cbranch_execz %s" % lab)
+    if in_record:
+        a("s_waitcnt lgkmcnt(0)")                  # the boundary table pointer
     # one load from the context's boundary table (mg_api.cpp
     # mg_boundary_table): entry kind * 256 + p, p = width - 1 for kind 2
     # (1 << (w-1)) and k otherwise; masked to the width by the handler
@@ -1024,8 +1047,8 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_mul_hi_u32 %s, %s, 6" % (v(kind), v(lo)))
     a("s_mov_b32 %s, 0x9e3779b1" % s(S_T))
     a("v_mul_lo_u32 %s, %s, %s" % (v(k), v(lo), s(S_T)))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(k), v(k), s(g + 0)))
-    a("s_sub_u32 %s, %s, 1" % (s(S_T + 1), s(g + 0)))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(k), v(k), s(f["w"])))
+    a("s_sub_u32 %s, %s, 1" % (s(S_T + 1), s(f["w"])))
     a("v_mov_b32 %s, %s" % (v(bit), s(S_T + 1)))
     a("v_cmp_eq_u32 vcc, 2, %s" % v(kind))
     a("v_cndmask_b32 %s, %s, %s, vcc" % (v(k), v(k), v(bit)))
@@ -1037,19 +1060,19 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
     # the pool is stored as (v-1, v, v+1) triples: entry e * 3 + delta
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
-    _class_mask(a, S_T + 2, g + 5, None, cls)
-    a("s_cmp_lg_u32 %s, 0" % s(g + 2))
+    _class_mask(a, S_T + 2, f["pb"], None, cls)
+    a("s_cmp_lg_u32 %s, 0" % s(f["pn"]))
     a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(S_T + 2)))
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     lab = a.uniq("gpl")
     a("s_cbranch_execz %s" % lab)
     e, delta = tt[0], tt[1]
-    a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(g + 2)))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(f["pn"])))
     a("s_mov_b32 %s, 0x85ebca6b" % s(S_T))
     a("v_mul_lo_u32 %s, %s, %s" % (v(delta), v(lo), s(S_T)))
     a("v_mul_hi_u32 %s, %s, 3" % (v(delta), v(delta)))
     a("v_mad_u32_u24 %s, %s, 3, %s" % (v(e), v(e), v(delta)))
-    a("v_lshl_add_u32 %s, %s, 5, %s" % (v(e), v(e), s(g + 1)))
+    a("v_lshl_add_u32 %s, %s, 5, %s" % (v(e), v(e), s(f["poff"])))
     a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(e), sp(S_CONST)))
     a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(e), sp(S_CONST)))
     a.label(lab)

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include <cstdlib>
@@ -256,6 +257,26 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
                    leaves[i].pool_n,
                    leaves[i].pct_uniform, leaves[i].pct_small, leaves[i].pct_boundary,
                    (uint32_t)salt, (uint32_t)(salt >> 32)};
+    }
+    // LEAFD records carry their leaf's generator parameters (asmgen.py
+    // LEAFD_*: no descriptor load in the handler): pool offset, salt, pool
+    // size and the class thresholds packed one per byte
+    {
+        std::vector<uint32_t> leafd_off;
+        for (uint32_t var = 0; var < MG_NREG; ++var)
+            for (int bank = 0; bank < 2; ++bank)
+                leafd_off.push_back(ctx->hoff[MGA_HID(MGA_LEAFD, var, bank)]);
+        for (size_t r = 0; r + 8 <= rec.size(); r += 8) {
+            if (std::find(leafd_off.begin(), leafd_off.end(), rec[r]) == leafd_off.end()) continue;
+            const uint32_t li = rec[r + 4];
+            if (li >= n_leaves) continue;            // eval mode only (no generator)
+            const mg_leafgen_dev& g = gdev[li];
+            rec[r + 1] = g.pool_off_b;
+            rec[r + 2] = g.salt_lo;
+            rec[r + 3] = g.salt_hi;
+            rec[r + 5] = g.pool_n;
+            rec[r + 7] = g.pct_uniform | g.pct_small << 8 | g.pct_boundary << 16;
+        }
     }
     // 8 zeroed NOPs after the IR code: the C++ interpreter prefetches ahead
     const size_t code_b = (size_t)(n_ins + 8) * 16, const_b = (size_t)n_const_all * 32,

@@ -351,6 +351,10 @@ class Wave:
     def i_s_and_b32(self, a, pc):
         self._sop2(a, lambda x, y: x & y)
 
+    def i_s_bfe_u32(self, a, pc):
+        # S1[4:0] = offset, S1[22:16] = width
+        self._sop2(a, lambda x, y: (x >> (y & 31)) & ((1 << ((y >> 16) & 0x7F)) - 1))
+
     def i_s_and_b64(self, a, pc):
         self._sop2(a, lambda x, y: x & y, 64)
 
@@ -898,6 +902,19 @@ def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
             salt = ((prog_seed * 0xD1B54A32D192ED03) ^ ((i + 1) * 0x8CB92BA72F3D8DD7)) & M64
             gdev[i] = [g.width, (pool_base + 3 * g.pool_off) * 32, g.pool_n, g.pct_uniform,
                        g.pct_small, g.pct_boundary, salt & M32, salt >> 32]
+        # LEAFD records carry the generator parameters (mg_load_program)
+        from mythril_amd import asmgen
+        _, table = body_and_table()
+        leafd = {table[asmgen.hid(asmgen.AOP["LEAFD"], var, bank)]
+                 for var in range(asmgen.NREG) for bank in (0, 1)}
+        rec = rec.copy()
+        for r in range(0, len(rec) - 7, 8):
+            li = int(rec[r + 4])
+            if int(rec[r]) in leafd and li < n_leaves:
+                g = gdev[li]
+                rec[r + 1], rec[r + 2], rec[r + 3], rec[r + 5] = g[1], g[6], g[7], g[2]
+                rec[r + 7] = int(g[3]) | int(g[4]) << 8 | int(g[5]) << 16
+        x_base = mem.alloc(rec.astype(np.uint32).tobytes(), "records")
     g_base = mem.alloc(gdev.tobytes(), "gen")
     b_base = mem.alloc(boundary_table().tobytes(), "btab")
     desc = struct.pack("<QQQIIIIQQQ", 0, c_base, g_base, prog.n_ins, n_leaves, 0, 0,
