@@ -179,6 +179,7 @@ class Asm:
         self._n = 0
         self._hot: Optional[List[str]] = None
         self._cold: List[str] = []
+        self._idx_state = None
 
     def __call__(self, text: str):
         self.lines.append("    " + text)
@@ -204,10 +205,35 @@ class Asm:
         return ".L%s%d_%%=" % (stem, self._n)
 
     def idx_on(self, sreg: int, mode: str):
+        """GPR-index mode on.  Right after an idx_off whose on-state is
+        known, the pair becomes one instruction: s_set_gpr_idx_idx (same
+        mode, another index) or s_set_gpr_idx_mode (same index)."""
+        prev = self._idx_state if self.lines and \
+            self.lines[-1].strip() == "s_set_gpr_idx_off" else None
+        self._idx_state = None
+        if prev is not None and (prev[1] == mode or prev[0] == sreg):
+            self.lines.pop()
+            if prev[1] != mode:
+                self("s_set_gpr_idx_mode gpr_idx(%s)" % mode)
+            elif prev[0] != sreg:
+                self("s_set_gpr_idx_idx %s" % s(sreg))
+            return
         self("s_set_gpr_idx_on %s, gpr_idx(%s)" % (s(sreg), mode))
 
     def idx_off(self):
+        # the on-state being closed, if no label or other index change
+        # came after the s_set_gpr_idx_on (a following idx_on may merge)
+        st = None
+        for line in reversed(self.lines):
+            t = line.strip()
+            m = re.fullmatch(r"s_set_gpr_idx_on s(\d+), gpr_idx\(([A-Z0-9,]+)\)", t)
+            if m:
+                st = (int(m.group(1)), m.group(2))
+                break
+            if t.startswith("s_set_gpr_idx_") or t.endswith(":"):
+                break
         self("s_set_gpr_idx_off")
+        self._idx_state = st
 
     def read_slot(self, dst: List[int], fld_sgpr: int):
         """dst[0..7] <- F[slot] with four 64-bit moves (full rate on gfx950,
@@ -1358,7 +1384,6 @@ def body_umulno(a: Asm):
     heavy_prologue(a)
     a.read_slot(X, cur(F_A))
     a.read_slot(Y, cur(F_B))
-    a("s_waitcnt lgkmcnt(0)")
     sz = T[8]                                   # clz(x) + clz(y) = 512 - (p + q)
     clz256(a, X, sz, [T[8], T[9], T[10], T[11], T[0], T[1], T[2], T[3]])
     clz256(a, Y, T[4], [T[4], T[5], T[6], T[7], T[0], T[1], T[2], T[3]])
@@ -1369,6 +1394,7 @@ def body_umulno(a: Asm):
     lab = a.uniq("unf")
     a("s_cmp_eq_u64 %s, 0" % sp(S_X + 2))
     a("s_cbranch_scc1 %s" % lab)
+    a("s_waitcnt lgkmcnt(0)")                   # the width masks
     col_product(a, X, Y, 16, hi_or=T[7])
     a("v_cmp_eq_u32 vcc, 0, %s" % v(T[7]))
     a("s_and_b64 vcc, vcc, %s" % sp(S_X + 2))
@@ -1771,7 +1797,6 @@ def body_div(a: Asm):
     heavy_prologue(a)
     a.read_slot(X, cur(F_A))
     a.read_slot(Y, cur(F_B))
-    a("s_waitcnt lgkmcnt(0)")
     a("s_lshr_b32 %s, %s, 4" % (s(OPR), s(S_VAR)))
     lab_u = a.uniq("du")
     a("s_cmp_lt_u32 %s, 2" % s(OPR))
@@ -1779,6 +1804,7 @@ def body_div(a: Asm):
     lab_ns = a.uniq("dns")
     a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
     a("s_cbranch_scc0 %s" % lab_ns)
+    a("s_waitcnt lgkmcnt(0)")                          # the width masks (sext)
     sext(a, X, cur(F_W), S_M, T[0], S_T)
     sext(a, Y, cur(F_W), S_M, T[0], S_T)
     a.label(lab_ns)
