@@ -934,11 +934,8 @@ def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
 # ---------------------------------------------------------------------------
 
 GOLD = 0x9E3779B97F4A7C15
-
-
-GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
-GOLD32, LIMB_MUL = 0x9E3779B9, 0x85EBCA6B   # uniform limbs 2-7 (generator v4/v5)
+PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_X, S_X + 6)
 
@@ -1042,19 +1039,18 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("s_movk_i32 %s, 100" % s(S_T))
     a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), s(S_T)))
     # ---- uniform values for every lane: r0 in limbs 0-1 (small lanes keep
-    # only those), limbs 2-7 one multiply-xorshift each of x = lo ^ hi of r0
-    # plus k * golden32 (v4: 4 VALU per limb instead of a SplitMix64 word
-    # per two limbs)
+    # only those), limb pair k = 1..3 is x * C_k + r0 (mod 2^64) with
+    # x = lo ^ hi of r0: one v_mad_u64_u32 per two limbs (v6; v4 spent a
+    # 4-VALU multiply-xorshift per limb)
     # (built straight in dst: a LEAFD's slot)
     dst = X if dst is None else dst
     a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(tt[0]), v(z[0]), v(z[1])))
-    a("s_mov_b32 %s, 0x%x" % (s(K_M2_LO), LIMB_MUL))
-    for k in range(2, 8):
-        a("v_add_u32 %s, 0x%x, %s" % (v(dst[k]), (k * GOLD32) & 0xFFFFFFFF, v(tt[0])))
-        a("v_mul_lo_u32 %s, %s, %s" % (v(dst[k]), v(dst[k]), s(K_M2_LO)))
-        a("v_lshrrev_b32 %s, 16, %s" % (v(tt[1]), v(dst[k])))
-        a("v_xor_b32 %s, %s, %s" % (v(dst[k]), v(dst[k]), v(tt[1])))
+    for k, c in enumerate(PAIR_MUL):
+        a("s_mov_b32 %s, 0x%x" % (s(K_M1_LO + k), c))
+    for k in range(3):
+        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(tt[0]), s(K_M1_LO + k),
+                                                 vp(z[0])))
     _class_mask(a, S_T + 2, f["pu"], f["ps"], cls)                   # small
     lab = exec_begin(a, S_T + 2, S_T + 4)
     moves(a, dst[2:], [None] * 6)

@@ -480,13 +480,11 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
         else *out = p;
         for (int i = 4; i < L; ++i) out->w[i] = 0;
     } else {
-        out->w[0] = r0;                       /* v4: r0, limbs 2-7 mixed from it */
-        uint32_t x = (uint32_t)r0 ^ (uint32_t)(r0 >> 32);
-        for (int k = 2; k < 8; ++k) {
-            uint32_t y = (x + (uint32_t)k * 0x9E3779B9u) * 0x85EBCA6Bu;
-            y ^= y >> 16;
-            out->w[k / 2] |= (uint64_t)y << (32 * (k & 1));
-        }
+        /* v6: r0, limb pair k = x * C_k + r0 with x = lo ^ hi of r0 */
+        static const uint64_t pair_mul[3] = {0x85EBCA6Bull, 0xC2B2AE35ull, 0x27D4EB2Full};
+        uint64_t x = (uint32_t)r0 ^ (uint32_t)(r0 >> 32);
+        out->w[0] = r0;
+        for (int k = 0; k < 3; ++k) out->w[k + 1] = x * pair_mul[k] + r0;
     }
     vmask(out, w);
 }

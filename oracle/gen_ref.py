@@ -42,9 +42,8 @@ def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
         delta = _mulhi((lo * 0x85EBCA6B) & 0xFFFFFFFF, 3)
         v = (pool[e] + delta - 1) % (1 << 256)
     else:
-        v = r0                                # v4: r0, limbs 2-7 mixed from it
+        v = r0                                # v6: limb pair k = x * C_k + r0
         x = (r0 ^ (r0 >> 32)) & 0xFFFFFFFF
-        for k in range(2, 8):
-            y = (((x + k * 0x9E3779B9) & 0xFFFFFFFF) * 0x85EBCA6B) & 0xFFFFFFFF
-            v |= (y ^ (y >> 16)) << (32 * k)
+        for k, c in enumerate((0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)):
+            v |= ((x * c + r0) & M64) << (64 * (k + 1))
     return v & mask
