@@ -1594,8 +1594,8 @@ def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
 
 def udivrem(a: Asm, want_rem: bool, z: int):
     """X / Y: quotient -> R; remainder (want_rem) -> X; s[z:z+1] <- lanes
-    with Y == 0, which divide by 1 instead (the caller applies SMT-LIB's
-    x/0 rules).  Normalisation shifts Y left until its top limb is nonzero,
+    with Y == 0, which compute 0 / 1 instead (quotient and remainder 0; the
+    caller applies SMT-LIB's x/0 rules).  Normalisation shifts Y left until its top limb is nonzero,
     4, 2 then 1 limbs at a time in the lanes whose top limbs are zero (the
     stage masks stay in s[48:53] for the dividend and the remainder), then
     by b = clz(top limb) bits.  Registers: un = X ++ R ++ [T0]; vn = Y;
@@ -1624,6 +1624,12 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     a("v_sub_u32 %s, 32, %s" % (v(c), v(b)))
     a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(bz), v(b)))
     bitshift_left(a, vn, c, bz, 8, S_T)
+    # lanes dividing by zero divide 0 instead (quotient and remainder 0; the
+    # caller gives them their SMT-LIB result), so they never keep a quotient
+    # digit of the wave alive (a divisor of 1 would need all eight)
+    lab = exec_begin(a, z, S_T)
+    moves(a, X, [None] * 8)
+    exec_end(a, lab, S_T)
     live = 8
     for st in (4, 2, 1):
         live = _stage(a, un, st, 16, True, DIV_M[st], live)
@@ -1819,7 +1825,7 @@ def body_div(a: Asm):
     a.label(lab_q)
     udivrem(a, want_rem=False, z=Z)
     a.label(lab_dd)
-    # R = q (== |u| where the divisor was forced to 1), X = remainder
+    # R = q, X = remainder (both 0 where the divisor is 0)
     labs = {k: a.uniq("dr%d" % k) for k in range(5)}
     lab_end = a.uniq("dre")
     for k in range(1, 5):
@@ -1836,11 +1842,17 @@ def body_div(a: Asm):
         moves(a, dst, src)
         exec_end(a, lab, S_T + 2)
 
+    def dividend_where_zero():                         # urem/srem/smod x/0 = x
+        lab = exec_begin(a, Z, S_T + 2)
+        a.read_slot(R, cur(F_A))                       # canonical at the width
+        exec_end(a, lab, S_T + 2)
+
     a.label(labs[0])                                   # udiv: z ? ~0 : q
     ones_where_zero()
     a("s_branch %s" % lab_end)
-    a.label(labs[1])                                   # urem: z ? q : rem
+    a.label(labs[1])                                   # urem: z ? x : rem
     rem_unless_zero(R, X)
+    dividend_where_zero()
     a("s_branch %s" % lab_end)
     a.label(labs[2])                                   # sdiv
     ones_where_zero()
@@ -1850,11 +1862,9 @@ def body_div(a: Asm):
     a.label(labs[3])                                   # srem: sign of the dividend
     rem_unless_zero(R, X)
     _cond_neg(a, R, NS)
+    dividend_where_zero()
     a("s_branch %s" % lab_end)
-    a.label(labs[4])                                   # smod
-    lab = exec_begin(a, Z, S_T + 2)                    # m = z ? q : rem  -> X
-    moves(a, X, R)
-    exec_end(a, lab, S_T + 2)
+    a.label(labs[4])                                   # smod: m = rem (X)
     a.read_slot(Y, cur(F_B))                           # t again
     lab_nx = a.uniq("dsx")
     a("s_bitcmp1_b32 %s, 1" % s(S_VAR))
@@ -1874,6 +1884,7 @@ def body_div(a: Asm):
     lab = exec_begin(a, None, S_T + 2)
     moves(a, R, [None] * 8)
     exec_end(a, lab, S_T + 2)
+    dividend_where_zero()
     a.label(lab_end)
     heavy_finish(a, R)
     a.flush_cold()
