@@ -98,7 +98,7 @@ int main() {
               {"v_add_f32", k_add_f32, 1}, {"v_add_u32", k_add_u32, 1},
               {"v_xor_b32", k_xor_b32, 1}, {"v_pk_mov_b32", k_pk_mov_b32, 2},
               {"v_add/addc_co chain", k_addc_chain, 1}, {"v_mad_u64_u32", k_mad_u64, 1}};
-    const int waves[] = {1, 3, 8};
+    const int waves[] = {1, 2, 3, 4, 5, 6, 8};
     Stamp* d_st;
     CHK(hipMalloc(&d_st, sizeof(Stamp) * cus * 4 * 8));
     printf("{\"device\": \"%s\", \"cus\": %d, \"instructions_per_wave\": %d}\n", prop.name, cus,
