@@ -82,7 +82,10 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "CONCATQ"]  # CONCAT: variant = limb shift q | 8 if a bit shift remains
 AOP = {n: i for i, n in enumerate(AOPS)}
 V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
-NVAR = 32
+# NW = a ROOT-fused result nobody reads: only the root is updated, the slot
+# is not written (chosen by the translator, mg_host.cpp)
+V_NW = 32
+NVAR = 64
 # variant bits each handler family implements (the query maps the others to
 # the nearest implemented handler): DC = destination's upper limbs are known
 # zero (write limb 0 only), W32 = operands and result fit one limb
@@ -95,6 +98,8 @@ SUPPORT.update({n: _RM | V_DC for n in ("SLT", "SLE")})
 # IP = the destination is operand a's slot: the ALU op writes the file in place
 SUPPORT.update({n: SUPPORT[n] | V_IP for n in ("ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG",
                                                "ITE")})
+for _n in ("EQ", "ULT", "ULE", "SLT", "SLE", "AND", "OR", "XOR"):
+    SUPPORT[_n] |= V_NW
 SUPPORT["SUBR"] = _RM | V_IP
 SUPPORT["ITEN"] = V_ROOT | V_IP
 SUPPORT["WAITVM"] = 0
@@ -126,6 +131,12 @@ def canon_var(name: str, var: int) -> int:
         var &= ~V_DC
     if var & V_W32:
         var &= ~V_IP                 # one limb: nothing to save
+    if not var & V_ROOT:
+        var &= ~V_NW                 # only a ROOT-fused result can go unwritten
+    if var & V_NW:
+        var &= ~V_DC
+        if name in ("AND", "OR", "XOR") and not var & V_W32:
+            var &= ~V_NW             # Bool logic is one limb
     return var
 
 
@@ -134,6 +145,8 @@ def hid(aop: int, variant: int, bank: int) -> int:
 
 
 NUM_HANDLERS = len(AOPS) * NVAR * 2
+# log2 of the byte alignment of every handler entry (0: packed)
+HANDLER_ALIGN = int(os.environ.get("MYTHGPU_HANDLER_ALIGN", "0"))
 
 
 def canonical(h: int) -> int:
@@ -180,6 +193,7 @@ class Asm:
         self._hot: Optional[List[str]] = None
         self._cold: List[str] = []
         self._idx_state = None
+        self.nw = False              # the handler being generated is an NW variant
 
     def __call__(self, text: str):
         self.lines.append("    " + text)
@@ -316,7 +330,12 @@ def write_narrow(a: Asm, bank: int, r0: str, dc: bool):
 
 
 def finish_narrow(a: Asm, bank: int, root: bool, mask: bool, dc: bool):
-    """R0 (one limb) -> F[D], masked to W bits if requested, ROOT, dispatch."""
+    """R0 (one limb) -> F[D], masked to W bits if requested, ROOT, dispatch.
+    NW (a dead ROOT-fused Bool): the root only."""
+    if a.nw:
+        a.root_and(v(R[0]))
+        dispatch(a, 1 - bank)
+        return
     if mask:
         a("s_waitcnt lgkmcnt(0)")
         a("v_and_b32 %s, %s, %s" % (v(R[0]), s(S_M), v(R[0])))
@@ -373,7 +392,10 @@ def h_nop(a, bank, root, mask, dc=False, w32=False, ip=False):
 
 def h_halt(a, bank, root, mask, dc=False, w32=False, ip=False):
     a("s_waitcnt lgkmcnt(0)")
-    a("s_branch .Lexit_%=")
+    if HANDLER_ALIGN:
+        far_jump(a, ".Lexit_%=")       # padded handlers outgrow s_branch's range
+    else:
+        a("s_branch .Lexit_%=")
 
 
 def h_const(a, bank, root, mask, dc=False, w32=False, ip=False):
@@ -564,6 +586,13 @@ def h_root(a, bank, root, mask, dc=False, w32=False, ip=False):
 
 
 def _bool_result(a, bank, root, true_if_vcc=True, dc=False):
+    if a.nw:                          # dead ROOT-fused Bool: root &= result
+        if true_if_vcc:
+            a("v_cndmask_b32_e64 %s, 0, %s, vcc" % (OP_ROOT, OP_ROOT))
+        else:
+            a("v_cndmask_b32_e64 %s, %s, 0, vcc" % (OP_ROOT, OP_ROOT))
+        dispatch(a, 1 - bank)
+        return
     a("v_cndmask_b32 %s, %s, %s, vcc" % (v(R[0]), "0" if true_if_vcc else "1",
                                          "1" if true_if_vcc else "0"))
     write_narrow(a, bank, v(R[0]), dc)
@@ -1916,6 +1945,10 @@ def generate() -> List[str]:
     a("s_load_dwordx2 %s, %s, 0x8" % (sp(S_CONST), IN["desc"]))
     a("s_load_dwordx2 %s, %s, 0x30" % (sp(S_CODE), IN["desc"]))
     a("v_mov_b32 %s, 1" % OP_ROOT)
+    if HANDLER_ALIGN:
+        # .Lbase at the same offset modulo the alignment in both kernel
+        # instantiations (the query launch's offsets must fit the other)
+        a(".p2align %d" % HANDLER_ALIGN)
     a("s_getpc_b64 %s" % sp(S_BASE))
     a.label(".Lbase_%=")
     a("s_bitcmp1_b32 %s, 1" % IN["mode"])
@@ -1943,7 +1976,10 @@ def generate() -> List[str]:
                 continue
             root_v, mask_v = bool(var & V_ROOT), bool(var & V_MASK)
             dc_v, w32_v, ip_v = bool(var & V_DC), bool(var & V_W32), bool(var & V_IP)
+            a.nw = bool(var & V_NW)
             for bank in (0, 1):
+                if HANDLER_ALIGN:
+                    a(".p2align %d" % HANDLER_ALIGN)
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
                 if name == "LEAFD":
                     h_leafd(a, bank, var)
@@ -1962,6 +1998,7 @@ def generate() -> List[str]:
                 else:
                     bits = var | (DIV_CODE.get(name, 0) << 4)
                     heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
+    a.nw = False
     body_umulno(a)
     body_div(a)
     a.label(".Lexit_%=")
@@ -1999,7 +2036,7 @@ def write_outputs(csrc: str) -> None:
            "#define MGA_NVAR %d" % NVAR,
            "#define MGA_V_ROOT %d" % V_ROOT, "#define MGA_V_MASK %d" % V_MASK,
            "#define MGA_V_DC %d" % V_DC, "#define MGA_V_W32 %d" % V_W32,
-           "#define MGA_V_IP %d" % V_IP,
+           "#define MGA_V_IP %d" % V_IP, "#define MGA_V_NW %d" % V_NW,
            "#define MGA_V_NEG %d" % V_NEG, "#define MGA_V_GEN %d" % V_GEN,
            "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
            "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,

@@ -299,12 +299,28 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
                 var |= MGA_V_IP;
             }
         }
+        // a ROOT-fused Bool nobody reads (the common case: a path condition):
+        // the NW variant only updates the root and leaves the slot alone
+        bool nw = false;
+        if ((in[0] & MG_ROOT_FLAG) &&
+            (aop == MGA_EQ || aop == MGA_ULT || aop == MGA_ULE || aop == MGA_SLT || aop == MGA_SLE ||
+             ((aop == MGA_AND || aop == MGA_OR || aop == MGA_XOR) && (var & MGA_V_W32)))) {
+            nw = true;
+            for (uint32_t q = pc + 1; q < n_ins; ++q) {
+                const uint32_t* f = code + 4 * order[q];
+                const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
+                               fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
+                if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) { nw = false; break; }
+                if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
+            }
+            if (nw) var = (var | MGA_V_NW) & ~MGA_V_DC;
+        }
         r[0] = hoff[MGA_HID(aop, var, bank)];
         if (aop == MGA_LEAFD || aop == MGA_RELOADD) {
             r[6] = 0;
             last_ld = (size_t)(r - rec.data());
         }
-        if (writes) clean[d] = narrow;
+        if (writes && !nw) clean[d] = narrow;
         bank = mga_is_heavy(aop) ? 0 : 1 - bank;
     }
 }

@@ -114,7 +114,7 @@ class Wave:
             for k, val in subst.items():
                 text = text.replace(k, val)
             text = text.replace("%=", "0")
-            if not text:
+            if not text or text.startswith(".p2align"):   # layout only
                 continue
             if text.endswith(":"):
                 self.labels[text[:-1]] = len(self.instrs)
