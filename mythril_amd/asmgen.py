@@ -701,10 +701,11 @@ def h_subr(a, bank, root, mask, dc=False, w32=False, ip=False):
 
 
 def _ite_cond(a: Asm, bank: int, negate: bool):
+    """vcc = (c != 0), or (c == 0) when negated; c is a canonical Bool
+    (limb 0 is 0 or 1), compared straight from the file."""
     a.idx_on(fld(bank, F_C), "SRC0")
-    a("v_and_b32_e64 %s, %s, 1" % (v(T[0]), v(F[0])))
+    a("v_cmp_%s_u32_e64 vcc, %s, 0" % ("eq" if negate else "ne", v(F[0])))
     a.idx_off()
-    a("v_cmp_%s_u32 vcc, 0, %s" % ("eq" if negate else "ne", v(T[0])))
 
 
 def _ite_inplace(a: Asm, bank: int, root: bool, negate: bool):
@@ -727,11 +728,11 @@ def _ite_inplace(a: Asm, bank: int, root: bool, negate: bool):
 
 
 def _ite_select(a: Asm, bank: int, first: int, other: int):
-    """R = F[first], then F[other] copied into R where vcc is set."""
+    """R = F[first], then F[other] read straight into R in the lanes where
+    vcc is set (an indexed read under exec: no staging copy)."""
     a.read_slot(R, fld(bank, first))
-    a.read_slot(Y, fld(bank, other))
     lab = exec_begin(a, None, S_T)
-    moves(a, R, Y)
+    a.read_slot(R, fld(bank, other))
     exec_end(a, lab, S_T)
 
 
@@ -1233,13 +1234,12 @@ def h_eqsel(a: Asm, bank: int, var: int):
     a("s_and_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 4)))
     if var & V_GEN:
         a.read_slot(R, fld(bank, F_IMM))          # else value
-    a.read_slot(Y, fld(bank, F_C))                # value taken
-    if var & V_GEN:
         lab = exec_begin(a, None, S_T)
-        moves(a, R, Y)
+        a.read_slot(R, fld(bank, F_C))            # value taken, where equal
         exec_end(a, lab, S_T)
         a.write_slot(R, fld(bank, F_D))
     else:
+        a.read_slot(Y, fld(bank, F_C))            # value taken
         lab = exec_begin(a, None, S_T, invert=bool(var & V_NEG))
         a.idx_on(fld(bank, F_D), "DST")
         moves(a, F, Y)
@@ -1482,7 +1482,7 @@ def moves(a: Asm, dsts: List[int], srcs: List[Optional[int]]):
 
 
 def _barrel(a: Asm, t: List[int], q: int, nl: int, left: bool, save: int,
-            live: Optional[int] = None):
+            live: Optional[int] = None, fill: Optional[int] = None):
     hi = nl if live is None else live
     for st in (1, 2, 4):
         a("v_and_b32 %s, %d, %s" % (v(TMP), st, v(q)))
@@ -1494,14 +1494,16 @@ def _barrel(a: Asm, t: List[int], q: int, nl: int, left: bool, save: int,
             moves(a, [t[j] for j in js], [t[j - st] if j - st >= 0 else None for j in js])
             hi = top
         else:
-            moves(a, [t[j] for j in range(nl)], [t[j + st] if j + st < nl else None for j in range(nl)])
+            moves(a, [t[j] for j in range(nl)], [t[j + st] if j + st < nl else fill
+                                                 for j in range(nl)])
         exec_end(a, lab, save)
 
 
-def barrel_right(a: Asm, t: List[int], q: int, nl: int, save: int):
-    """t[0..nl-1] = t >> (32*q) limbs (q per lane in v[q] < 8), zero fill;
-    each stage moves only the lanes that take it (under exec)."""
-    _barrel(a, t, q, nl, False, save)
+def barrel_right(a: Asm, t: List[int], q: int, nl: int, save: int, fill: Optional[int] = None):
+    """t[0..nl-1] = t >> (32*q) limbs (q per lane in v[q] < 8), filled with
+    zeros or with v[fill] (the sign word of an arithmetic shift); each stage
+    moves only the lanes that take it (under exec)."""
+    _barrel(a, t, q, nl, False, save, fill=fill)
 
 
 def barrel_left(a: Asm, t: List[int], q: int, nl: int, save: int, live: Optional[int] = None):
@@ -1543,24 +1545,26 @@ def shift_core(a: Asm, kind: str, fa: int, fb: int, fw: int, masked: bool):
     """X = F[fa] shifted by F[fb] at the width in s[fw]; ASHR sign-extends
     from that width first when ``masked`` (the masks S_M are loading)."""
     a.read_slot(X, fa)
-    a.read_slot(Y, fb)
     over = S_X                     # s[88:89] lanes shifting by >= W
-    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(Y[1]), v(Y[2]), v(Y[3])))
-    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(T[0]), v(Y[4]), v(Y[5])))
-    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(T[0]), v(Y[6]), v(Y[7])))
+    # the shift amount is used straight from the file (all three sources of
+    # the or3 indexed: limbs 1..6 of F[b]), no staging copy
+    a.idx_on(fb, "SRC0,SRC1,SRC2")
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(F[1]), v(F[2]), v(F[3])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(F[4]), v(F[5]), v(F[6])))
+    a("s_set_gpr_idx_mode gpr_idx(SRC0)")
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(F[7]), v(T[0]), v(T[1])))
+    a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T), v(F[0]), s(fw)))
+    a("v_bfe_u32 %s, %s, 5, 3" % (v(T[2]), v(F[0])))         # q (over lanes masked later)
+    a("v_and_b32_e64 %s, %s, 31" % (v(T[3]), v(F[0])))      # b
+    a.idx_off()
     a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(over), v(T[0])))
-    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T), s(fw), v(Y[0])))
     a("s_or_b64 %s, %s, %s" % (sp(over), sp(over), sp(S_T)))
-    a("v_bfe_u32 %s, %s, 5, 3" % (v(T[2]), v(Y[0])))         # q (over lanes masked later)
-    a("v_and_b32 %s, 31, %s" % (v(T[3]), v(Y[0])))          # b
     fill = None
     if kind == "ASHR":
         if masked:
             a("s_waitcnt lgkmcnt(0)")
             sext(a, X, fw, S_M, T[4], S_T)
-        a("v_ashrrev_i32 %s, 31, %s" % (v(T[4]), v(X[7])))
-        for j in range(8):
-            a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[4])))
+        a("v_ashrrev_i32 %s, 31, %s" % (v(T[4]), v(X[7])))   # the sign word
         fill = T[4]
     lab_all = a.uniq("sho")
     a("s_andn2_b64 %s, exec, %s" % (sp(S_T), sp(over)))
@@ -1570,14 +1574,11 @@ def shift_core(a: Asm, kind: str, fa: int, fb: int, fw: int, masked: bool):
         a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_X + 2), v(T[3])))
         barrel_left(a, X, T[2], 8, S_T)
         bitshift_left(a, X, T[5], S_X + 2, 8, S_T)
-    else:
-        a("v_mov_b32 %s, 0" % v(R[0]))
+    else:                          # ASHR fills with the sign word directly
+        a("v_mov_b32 %s, %s" % (v(R[0]), "0" if fill is None else v(fill)))
         t = X + [R[0]]
-        barrel_right(a, t, T[2], 8, S_T)
+        barrel_right(a, t, T[2], 8, S_T, fill)
         bitshift_right(a, t, T[3], 8)
-    if fill is not None:
-        for j in range(8):
-            a("v_xor_b32 %s, %s, %s" % (v(X[j]), v(X[j]), v(fill)))
     a.label(lab_all)
     if fill is not None:
         a("v_mov_b32 %s, %s" % (v(T[5]), v(fill)))
