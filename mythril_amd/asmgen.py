@@ -194,11 +194,28 @@ class Asm:
         self._cold: List[str] = []
         self._idx_state = None
         self.nw = False              # the handler being generated is an NW variant
+        # GPR-index mode may still be on at a handler's entry (a handler
+        # leaves it on when its last VGPR access was indexed: dispatch drops
+        # the trailing s_set_gpr_idx_off); the first instruction that touches
+        # VGPRs before the handler sets the mode itself gets the off first
+        self._entry_idx_unknown = False
 
     def __call__(self, text: str):
+        if self._entry_idx_unknown:
+            op = text.split(None, 1)[0]
+            if op.startswith("s_set_gpr_idx_on") or op == "s_set_gpr_idx_off":
+                self._entry_idx_unknown = False
+            elif (not op.startswith("s_") and not op.startswith(".")) or \
+                    op.startswith("s_cbranch") or op == "s_branch":
+                # before the first VGPR access, or before a branch (a path
+                # that leaves the straight line must not miss it)
+                self._entry_idx_unknown = False
+                self.lines.append("    s_set_gpr_idx_off")
         self.lines.append("    " + text)
 
     def label(self, name: str):
+        if name.startswith(".Lh") or name.startswith(".Lbody_"):
+            self._entry_idx_unknown = True       # entered from any handler's dispatch
         self.lines.append(name + ":")
 
     def cold(self):
@@ -288,8 +305,21 @@ def prologue(a: Asm, bank: int):
     a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
 
 
+_PROBE = os.environ.get("MYTHGPU_PROBE", "")     # sensitivity probes (A/B builds only)
+
+
 def dispatch(a: Asm, next_bank: int):
     nb = BANK[next_bank]
+    if a.lines and a.lines[-1].strip() == "s_set_gpr_idx_off":
+        a.lines.pop()                  # the next handler turns it off if it must
+    if _PROBE == "salu2":
+        a("s_mov_b32 s85, s85")
+        a("s_mov_b32 s85, s85")
+    elif _PROBE == "valu2":
+        a("v_mov_b32 %s, %s" % (v(TMP), v(TMP)))
+        a("v_mov_b32 %s, %s" % (v(TMP), v(TMP)))
+    elif _PROBE == "valu4c":
+        a("v_mov_b64 %s, %s" % (vp(T[8]), vp(T[8])))
     a("s_waitcnt lgkmcnt(0)")
     a("s_add_u32 %s, %s, %s" % (s(S_JMP), s(S_BASE), s(nb + F_OFF)))
     a("s_addc_u32 %s, %s, 0" % (s(S_JMP + 1), s(S_BASE + 1)))
@@ -1443,8 +1473,9 @@ def exec_begin(a: Asm, mask: Optional[int], save: int, invert: bool = False) -> 
     a conditional update costs one plain instruction instead of a compute +
     v_cndmask pair.  Clobbers s[save:save+1] and scc."""
     lab = a.uniq("xm")
-    a("s_mov_b64 %s, exec" % sp(save))
-    a("s_%s_b64 exec, exec, %s" % ("andn2" if invert else "and", "vcc" if mask is None else sp(mask)))
+    # one instruction saves exec and narrows it (andn1: exec &= ~mask)
+    a("s_%s_saveexec_b64 %s, %s" % ("andn1" if invert else "and", sp(save),
+                                    "vcc" if mask is None else sp(mask)))
     a("s_cbranch_execz %s" % lab)
     return lab
 

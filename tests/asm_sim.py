@@ -367,6 +367,18 @@ class Wave:
     def i_s_andn2_b64(self, a, pc):
         self._sop2(a, lambda x, y: x & ~y, 64)
 
+    def i_s_and_saveexec_b64(self, a, pc):
+        m = self.sread(a[1], 64)
+        self.swrite(a[0], self.exec)
+        self.exec = m & self.exec
+        self.scc = int(self.exec != 0)
+
+    def i_s_andn1_saveexec_b64(self, a, pc):
+        m = self.sread(a[1], 64)
+        self.swrite(a[0], self.exec)
+        self.exec = ~m & self.exec & M64
+        self.scc = int(self.exec != 0)
+
     def i_s_lshl_b32(self, a, pc):
         self._sop2(a, lambda x, y: x << (y & 31))
 
