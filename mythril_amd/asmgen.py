@@ -239,11 +239,14 @@ class Asm:
         """GPR-index mode on.  Right after an idx_off whose on-state is
         known, the pair becomes one instruction: s_set_gpr_idx_idx (same
         mode, another index) or s_set_gpr_idx_mode (same index)."""
-        prev = self._idx_state if self.lines and \
-            self.lines[-1].strip() == "s_set_gpr_idx_off" else None
+        after_off = bool(self.lines) and self.lines[-1].strip() == "s_set_gpr_idx_off"
+        prev = self._idx_state if after_off else None
         self._idx_state = None
-        if prev is not None and (prev[1] == mode or prev[0] == sreg):
+        if after_off:
+            # s_set_gpr_idx_on sets index and mode whatever the state: an off
+            # right before it is redundant
             self.lines.pop()
+        if prev is not None and (prev[1] == mode or prev[0] == sreg):
             if prev[1] != mode:
                 self("s_set_gpr_idx_mode gpr_idx(%s)" % mode)
             elif prev[0] != sreg:
@@ -2036,7 +2039,56 @@ def generate() -> List[str]:
     a.label(".Lexit_%=")
     a("s_set_gpr_idx_off")
     a("s_mov_b32 m0, %s" % s(S_M0))
-    return a.lines
+    return drop_redundant_idx_off(a.lines)
+
+
+def drop_redundant_idx_off(lines: List[str]) -> List[str]:
+    """Remove every s_set_gpr_idx_off after which each path reaches an
+    s_set_gpr_idx_on (it sets index and mode in any state) or a dispatch
+    (the next handler turns the mode off lazily, Asm.__call__) before any
+    instruction that touches VGPRs.  A path reaching another off, an
+    s_set_gpr_idx_idx / _mode or the end keeps the off (conservative)."""
+    body = [l.strip() for l in lines]
+    label_at = {t[:-1]: i for i, t in enumerate(body) if t.endswith(":")}
+
+    def succ(i: int) -> List[int]:
+        t = body[i]
+        op = t.split(None, 1)[0] if t else ""
+        if op == "s_setpc_b64":
+            return []
+        if op == "s_branch":
+            return [label_at[t.split()[1]]]
+        if op.startswith("s_cbranch"):
+            return [label_at[t.split()[1]], i + 1]
+        return [i + 1]
+
+    def redundant(i: int) -> bool:
+        stack, seen = [i + 1], set()
+        while stack:
+            j = stack.pop()
+            if j in seen:
+                continue
+            seen.add(j)
+            if j >= len(body):
+                return False
+            t = body[j]
+            if not t or t.endswith(":") or t.startswith("."):
+                stack.append(j + 1)
+                continue
+            op = t.split(None, 1)[0]
+            if op.startswith("s_set_gpr_idx_on"):
+                continue
+            if op.startswith("s_set_gpr_idx_"):
+                return False
+            if op == "s_setpc_b64":
+                continue                          # next handler: lazy off
+            if not op.startswith("s_"):
+                return False                      # a VGPR access
+            stack.extend(succ(j))
+        return True
+
+    drop = {i for i, t in enumerate(body) if t == "s_set_gpr_idx_off" and redundant(i)}
+    return [l for i, l in enumerate(lines) if i not in drop]
 
 
 def clobbers() -> List[str]:
