@@ -60,7 +60,8 @@ S_T = 80                   # s[80:87] temps; s[86:87] is also the jump target
 S_X = 88                   # s[88:95] division lane masks (ns, nt, z) + op
 S_JMP = S_T + 6
 S_M0 = S_X + 7             # m0 (GPR-index register) saved across the asm
-S_LAST = S_X + 7
+S_K = 96                   # s[96:101] SplitMix64 constants, set once at entry
+S_LAST = S_K + 5
 
 F_OFF, F_D, F_A, F_B, F_C, F_IMM, F_W, F_MOFF = range(8)
 # LEAFD records carry the leaf's generator parameters (mg_load_program
@@ -181,7 +182,8 @@ G = [FB - 8 + j for j in range(10)]     # funnel base (index = 8*slot + limb shi
 TMP = T[11]
 
 # inline-asm operand names
-OP_ROOT, OP_LANE_LO, OP_LANE_HI, OP_LDS = "%[root]", "%[lane_lo]", "%[lane_hi]", "%[lds]"
+# idx = the lane's candidate index (first + lane, 64-bit; the C++ shell)
+OP_ROOT, OP_IDX_LO, OP_IDX_HI, OP_LDS = "%[root]", "%[idx_lo]", "%[idx_hi]", "%[lds]"
 IN = {k: "%%[%s]" % k for k in ("desc", "seed", "first", "leaves", "stride", "lout", "probes",
                                 "mode", "scr", "active", "table")}
 
@@ -942,6 +944,14 @@ def _soa_base(a: Asm, ptr_op: str, row_sgpr: int):
     a("s_addc_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 1), s(S_T + 3)))
 
 
+def lane_offset(a: Asm, dst: int):
+    """v[dst] = 4 * lane (the lane's row in an SoA buffer) from idx - first.
+    Clobbers s[S_T+6:S_T+7]."""
+    a("s_mov_b64 %s, %s" % (sp(S_T + 6), IN["first"]))
+    a("v_subrev_u32 %s, %s, %s" % (v(dst), s(S_T + 6), OP_IDX_LO))
+    a("v_lshlrev_b32 %s, 2, %s" % (v(dst), v(dst)))
+
+
 def _soa_step(a: Asm):
     a("s_add_u32 %s, %s, %s" % (s(S_T), s(S_T), s(S_T + 4)))
     a("s_addc_u32 %s, %s, %s" % (s(S_T + 1), s(S_T + 1), s(S_T + 5)))
@@ -974,7 +984,7 @@ def _store_soa_body(a: Asm, regs: List[int], ptr_op: str, row_sgpr: int, wait_vm
     if wait_vm:
         a("s_waitcnt vmcnt(0)")
     _soa_base(a, ptr_op, row_sgpr)
-    a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
+    lane_offset(a, T[0])
     a("s_mov_b64 %s, exec" % sp(S_T + 6))
     a("s_mov_b64 exec, %s" % IN["active"])
     for j in range(8):
@@ -1000,7 +1010,8 @@ GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
 PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
-K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_X, S_X + 6)
+K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
+S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
 
 
 def load_sm64_consts(a: Asm):
@@ -1077,27 +1088,21 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a("s_and_b32 %s, %s, 0xff" % (s(f["pu"]), s(pk)))
         a("s_bfe_u32 %s, %s, 0x80008" % (s(f["ps"]), s(pk)))
         a("s_bfe_u32 %s, %s, 0x80010" % (s(f["pb"]), s(pk)))
-        load_sm64_consts(a)
     else:
         f = {"w": g + 0, "poff": g + 1, "pn": g + 2, "pu": g + 3, "ps": g + 4, "pb": g + 5,
              "salt": g + 6}
         a("s_load_dwordx2 %s, %s, 0x10" % (sp(S_T), IN["desc"]))       # gen table
         a("s_lshl_b32 %s, %s, 5" % (s(S_T + 2), s(fld(bank, F_C))))
-        load_sm64_consts(a)
         a("s_waitcnt lgkmcnt(0)")
         a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
-    # idx = first + lane ; st = seed ^ salt ^ idx (v5: the counter itself,
-    # SplitMix64's finaliser spreads it; no idx * GOLD multiply)
-    a("s_mov_b64 %s, %s" % (sp(S_T + 4), IN["first"]))
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(S_T + 4), OP_LANE_LO))
-    a("v_mov_b32 %s, %s" % (v(st[1]), s(S_T + 5)))
-    a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(st[1]), OP_LANE_HI))
+    # st = seed ^ salt ^ idx (v5: the counter itself, SplitMix64's finaliser
+    # spreads it; no idx * GOLD multiply); idx = first + lane arrives ready
     a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
     if not in_record:
         a("s_waitcnt lgkmcnt(0)")
     a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(f["salt"])))
-    a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), v(st[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), v(st[1])))
+    a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), OP_IDX_LO))
+    a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), OP_IDX_HI))
     sm64(a, st, z, tt)
     a("s_movk_i32 %s, 100" % s(S_T))
     a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), s(S_T)))
@@ -1110,9 +1115,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(tt[0]), v(z[0]), v(z[1])))
     for k, c in enumerate(PAIR_MUL):
-        a("s_mov_b32 %s, 0x%x" % (s(K_M1_LO + k), c))
+        a("s_mov_b32 %s, 0x%x" % (s(S_PAIR + k), c))
     for k in range(3):
-        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(tt[0]), s(K_M1_LO + k),
+        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(tt[0]), s(S_PAIR + k),
                                                  vp(z[0])))
     _class_mask(a, S_T + 2, f["pu"], f["ps"], cls)                   # small
     lab = exec_begin(a, S_T + 2, S_T + 4)
@@ -1184,7 +1189,7 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     a.cold()
     a.label(lab_mem)
     _soa_base(a, IN["leaves"], fld(bank, F_C))
-    a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
+    lane_offset(a, T[0])
     for j in range(8):
         a("global_load_dword %s, %s, %s" % (v(X[j]), v(T[0]), sp(S_T)))
         if j < 7:
@@ -1226,7 +1231,7 @@ def h_leafd(a: Asm, bank: int, var: int):
     a.cold()
     a.label(lab_mem)
     _soa_base(a, IN["leaves"], fld(bank, F_C))
-    a("v_lshlrev_b32 %s, 2, %s" % (v(T[0]), OP_LANE_LO))
+    lane_offset(a, T[0])
     for j in range(8):
         a("global_load_dword %s, %s, %s" % (v(fd[j]), v(T[0]), sp(S_T)))
         if j < 7:
@@ -1976,6 +1981,7 @@ HEAVY_AOPS = sorted(AOP[n] for n in HEAVY)
 def generate() -> List[str]:
     a = Asm()
     a("s_mov_b32 %s, m0" % s(S_M0))
+    load_sm64_consts(a)
     # mg_pdesc: code@0 consts@8 gen@16 ... xcode@48
     a("s_load_dwordx2 %s, %s, 0x8" % (sp(S_CONST), IN["desc"]))
     a("s_load_dwordx2 %s, %s, 0x30" % (sp(S_CODE), IN["desc"]))

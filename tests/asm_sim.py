@@ -508,6 +508,9 @@ class Wave:
     def i_v_sub_u32(self, a, pc):
         self._vop2(a, lambda x, y: x - y)
 
+    def i_v_subrev_u32(self, a, pc):
+        self._vop2(a, lambda x, y: y - x)
+
     def i_v_mul_lo_u32(self, a, pc):
         self._vop2(a, lambda x, y: (x * y) & np.uint64(M32))
 
@@ -808,7 +811,7 @@ class Wave:
 # ---------------------------------------------------------------------------
 
 OPERANDS = {  # inline-asm operands -> registers the simulator uses
-    "%[root]": "v200", "%[lane_lo]": "v201", "%[lane_hi]": "v202", "%[lds]": "v203",
+    "%[root]": "v200", "%[idx_lo]": "v201", "%[idx_hi]": "v202", "%[lds]": "v203",
     "%[desc]": "s[0:1]", "%[seed]": "s[2:3]", "%[first]": "s[4:5]", "%[leaves]": "s[6:7]",
     "%[stride]": "s[8:9]", "%[lout]": "s[10:11]", "%[probes]": "s[12:13]", "%[mode]": "s14",
     "%[scr]": "s15", "%[active]": "s[16:17]", "%[table]": "s[18:19]",
@@ -943,8 +946,9 @@ def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
         w.s[reg], w.s[reg + 1] = val & M32, (val >> 32) & M32
     w.s[14] = 1 if gen is not None else 0
     w.s[15] = 0
-    w.v[201] = np.arange(NL, dtype=np.uint64)
-    w.v[202] = 0
+    idx = [(first + lane) & M64 for lane in range(NL)]      # the shell's first + lane
+    w.v[201] = np.array([i & M32 for i in idx], dtype=np.uint64)
+    w.v[202] = np.array([i >> 32 for i in idx], dtype=np.uint64)
     w.v[203] = np.arange(NL, dtype=np.uint64) * 16
     w.run()
     if w.pending:
