@@ -118,7 +118,14 @@ DC_NEEDS_W32 = {"ADD", "SUB", "AND", "OR", "XOR", "NOT", "NEG", "ITE", "EXTRACT"
 SLOT_VARIANT = {"LEAFD", "RELOADD", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS"}
 
 
+# LEAFD / RELOADD: variant = slot | WAITD when the handler waits for its own
+# loads (its consumer is the very next record; the translator folds the wait)
+V_WAITD = 16
+
+
 def canon_var(name: str, var: int) -> int:
+    if name in ("LEAFD", "RELOADD"):
+        return var & (V_WAITD | 15) if (var & 15) < NREG else 0
     if name in SLOT_VARIANT:
         return var if var < NREG else 0      # the variant is the register slot
     if name == "EXTRACTN":
@@ -427,10 +434,7 @@ def h_nop(a, bank, root, mask, dc=False, w32=False, ip=False):
 
 def h_halt(a, bank, root, mask, dc=False, w32=False, ip=False):
     a("s_waitcnt lgkmcnt(0)")
-    if HANDLER_ALIGN:
-        far_jump(a, ".Lexit_%=")       # padded handlers outgrow s_branch's range
-    else:
-        a("s_branch .Lexit_%=")
+    far_jump(a, ".Lexit_%=")           # the handlers outgrow s_branch's range
 
 
 def h_const(a, bank, root, mask, dc=False, w32=False, ip=False):
@@ -1125,9 +1129,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     exec_end(a, lab, S_T + 4)
     # ---- boundary: pct_small <= cls < pct_boundary -------------------------
     _class_mask(a, S_T + 2, f["ps"], f["pb"], cls)
+    # (no skip branch: with 64 lanes some lane nearly always is in the class;
+    # with exec = 0 the loads access nothing)
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
-    lab = a.uniq("gbd")
-    a("s_cbranch_execz %s" % lab)
     if in_record:
         a("s_waitcnt lgkmcnt(0)")                  # the boundary table pointer
     # one load from the context's boundary table (mg_api.cpp
@@ -1146,7 +1150,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_lshlrev_b32 %s, 5, %s" % (v(k), v(k)))
     a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(k), sp(S_T + 6)))
     a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(k), sp(S_T + 6)))
-    a.label(lab)
     # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
     # the pool is stored as (v-1, v, v+1) triples: entry e * 3 + delta
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
@@ -1154,8 +1157,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("s_cmp_lg_u32 %s, 0" % s(f["pn"]))
     a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(S_T + 2)))
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
-    lab = a.uniq("gpl")
-    a("s_cbranch_execz %s" % lab)
     e, delta = tt[0], tt[1]
     a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(f["pn"])))
     a("s_mov_b32 %s, 0x85ebca6b" % s(S_T))
@@ -1165,7 +1166,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_lshl_add_u32 %s, %s, 5, %s" % (v(e), v(e), s(f["poff"])))
     a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(e), sp(S_CONST)))
     a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(e), sp(S_CONST)))
-    a.label(lab)
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
     if wait:
         a("s_waitcnt vmcnt(0)")                   # boundary and pool loads
@@ -1200,15 +1200,12 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     a.flush_cold()
 
 
-def _wait_if_flagged(a: Asm, bank: int):
-    """LEAFD / RELOADD whose consumer is the very next record: the translator
-    sets word W of the record, and the handler waits for its loads itself
-    instead of a separate WAITVM record."""
-    lab = a.uniq("nw")
-    a("s_cmp_eq_u32 %s, 0" % s(fld(bank, F_W)))
-    a("s_cbranch_scc1 %s" % lab)
-    a("s_waitcnt vmcnt(0)")
-    a.label(lab)
+def _wait_if_flagged(a: Asm, var: int):
+    """LEAFD / RELOADD whose consumer is the very next record (the WAITD
+    variant, chosen by the translator): the handler waits for its loads
+    itself instead of a separate WAITVM record; static, no test."""
+    if var & V_WAITD:
+        a("s_waitcnt vmcnt(0)")
 
 
 def h_leafd(a: Asm, bank: int, var: int):
@@ -1217,7 +1214,7 @@ def h_leafd(a: Asm, bank: int, var: int):
     generator's boundary / pool lanes) are left in flight, so a run of leaves
     pays one memory latency at the WAITVM the translator puts before the
     first instruction that touches a pending slot."""
-    slot = var
+    slot = var & 15
     fd = [FB + 8 * slot + j for j in range(8)]
     prologue(a, bank)
     lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
@@ -1226,7 +1223,7 @@ def h_leafd(a: Asm, bank: int, var: int):
     _gen_leaf(a, bank, dst=fd, wait=False)
     _store_soa(a, fd, IN["lout"], fld(bank, F_C), wait_vm=True, cold=True)
     a.label(lab_done)
-    _wait_if_flagged(a, bank)
+    _wait_if_flagged(a, var)
     dispatch(a, 1 - bank)
     a.cold()
     a.label(lab_mem)
@@ -1246,12 +1243,12 @@ def h_reloadd(a: Asm, bank: int, var: int):
     flight; the translator hoists it above earlier instructions that leave
     the slot and the spill slot alone, and puts a WAITVM before the first
     instruction that touches the slot."""
-    fd = FB + 8 * var
+    fd = FB + 8 * (var & 15)
     prologue(a, bank)
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
     a("scratch_load_dwordx4 v[%d:%d], off, %s" % (fd, fd + 3, s(S_T)))
     a("scratch_load_dwordx4 v[%d:%d], off, %s offset:16" % (fd + 4, fd + 7, s(S_T)))
-    _wait_if_flagged(a, bank)
+    _wait_if_flagged(a, var)
     dispatch(a, 1 - bank)
 
 
@@ -1473,18 +1470,22 @@ def body_umulno(a: Asm):
 
 # ---- per-lane shifts ------------------------------------------------------
 
-def exec_begin(a: Asm, mask: Optional[int], save: int, invert: bool = False) -> str:
+def exec_begin(a: Asm, mask: Optional[int], save: int, invert: bool = False,
+               skip: bool = False) -> str:
     """Narrow exec to the lanes of s[mask:mask+1] (vcc if None; or the
-    complement) and
-    branch over the block when none is left; returns the label that
-    exec_end places.  VALU under a narrowed exec writes only those lanes, so
-    a conditional update costs one plain instruction instead of a compute +
-    v_cndmask pair.  Clobbers s[save:save+1] and scc."""
+    complement); returns the label that exec_end places.  VALU under a
+    narrowed exec writes only those lanes, so a conditional update costs one
+    plain instruction instead of a compute + v_cndmask pair.  The blocks are
+    short, so by default there is no branch over an empty one: a taken
+    branch (an instruction-fetch redirect) costs more than a few
+    instructions issued with exec = 0 (+1.5 % corpus, profiles/r02/
+    ab_noskip.log); ``skip`` adds it.  Clobbers s[save:save+1] and scc."""
     lab = a.uniq("xm")
     # one instruction saves exec and narrows it (andn1: exec &= ~mask)
     a("s_%s_saveexec_b64 %s, %s" % ("andn1" if invert else "and", sp(save),
                                     "vcc" if mask is None else sp(mask)))
-    a("s_cbranch_execz %s" % lab)
+    if skip:
+        a("s_cbranch_execz %s" % lab)
     return lab
 
 
@@ -2127,6 +2128,7 @@ def write_outputs(csrc: str) -> None:
            "#define MGA_V_ROOT %d" % V_ROOT, "#define MGA_V_MASK %d" % V_MASK,
            "#define MGA_V_DC %d" % V_DC, "#define MGA_V_W32 %d" % V_W32,
            "#define MGA_V_IP %d" % V_IP, "#define MGA_V_NW %d" % V_NW,
+           "#define MGA_V_WAITD %d" % V_WAITD,
            "#define MGA_V_NEG %d" % V_NEG, "#define MGA_V_GEN %d" % V_GEN,
            "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
            "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,

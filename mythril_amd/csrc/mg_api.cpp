@@ -264,8 +264,9 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     {
         std::vector<uint32_t> leafd_off;
         for (uint32_t var = 0; var < MG_NREG; ++var)
-            for (int bank = 0; bank < 2; ++bank)
-                leafd_off.push_back(ctx->hoff[MGA_HID(MGA_LEAFD, var, bank)]);
+            for (uint32_t w = 0; w < 2; ++w)
+                for (int bank = 0; bank < 2; ++bank)
+                    leafd_off.push_back(ctx->hoff[MGA_HID(MGA_LEAFD, var | (w ? MGA_V_WAITD : 0), bank)]);
         for (size_t r = 0; r + 8 <= rec.size(); r += 8) {
             if (std::find(leafd_off.begin(), leafd_off.end(), rec[r]) == leafd_off.end()) continue;
             const uint32_t li = rec[r + 4];

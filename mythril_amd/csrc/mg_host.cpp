@@ -116,9 +116,12 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
     // the last record emitted, when it is a LEAFD / RELOADD: a wait right
     // after it folds into that record (word W = 1, the handler waits)
     size_t last_ld = SIZE_MAX;
+    uint32_t last_ld_hid = 0;               // its handler id, WAITD bit clear
     auto wait_vm = [&]() {
         if (last_ld != SIZE_MAX && last_ld + 8 == rec.size()) {
-            rec[last_ld + 6] = 1;           // the LEAFD / RELOADD waits itself
+            // the LEAFD / RELOADD waits itself: its WAITD variant
+            rec[last_ld] = hoff[last_ld_hid + 2 * MGA_V_WAITD];
+            rec[last_ld + 6] = 1;
         } else {
             emit()[0] = hoff[MGA_HID(MGA_WAITVM, 0, bank)];
             bank = 1 - bank;
@@ -319,6 +322,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         if (aop == MGA_LEAFD || aop == MGA_RELOADD) {
             r[6] = 0;
             last_ld = (size_t)(r - rec.data());
+            last_ld_hid = MGA_HID(aop, var, bank);
         }
         if (writes && !nw) clean[d] = narrow;
         bank = mga_is_heavy(aop) ? 0 : 1 - bank;

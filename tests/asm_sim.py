@@ -920,8 +920,8 @@ def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
         # LEAFD records carry the generator parameters (mg_load_program)
         from mythril_amd import asmgen
         _, table = body_and_table()
-        leafd = {table[asmgen.hid(asmgen.AOP["LEAFD"], var, bank)]
-                 for var in range(asmgen.NREG) for bank in (0, 1)}
+        leafd = {table[asmgen.hid(asmgen.AOP["LEAFD"], var | w, bank)]
+                 for var in range(asmgen.NREG) for w in (0, asmgen.V_WAITD) for bank in (0, 1)}
         rec = rec.copy()
         for r in range(0, len(rec) - 7, 8):
             li = int(rec[r + 4])
