@@ -746,7 +746,11 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
             else:
                 d = alloc_reg(i, set())
                 free_regs.append(d)
-            reg_clean[d] = n.width <= 32
+            # a dead ROOT-fused Bool is not written at all (the translator's NW
+            # variants, mg_host.cpp): the register keeps its previous state
+            if not (n.id in fused and (n.op in _CMP_OPS or
+                                       (n.op in (I.AND, I.OR, I.XOR) and n.width <= 32))):
+                reg_clean[d] = n.width <= 32
         else:
             d = None
             # in place: reuse a dying operand's register (the engine then
@@ -762,6 +766,15 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
             if d is None and n.width <= 32:
                 for r in reversed(free_regs):
                     if reg_clean.get(r):
+                        free_regs.remove(r)
+                        d = r
+                        break
+            # wide results prefer a register whose upper limbs are dirty
+            # anyway, keeping the clean ones for one-limb results (their
+            # writes then skip the upper limbs: the translator's DC variants)
+            if d is None and n.width > 32 and KEEP_CLEAN:
+                for r in reversed(free_regs):
+                    if not reg_clean.get(r):
                         free_regs.remove(r)
                         d = r
                         break
@@ -791,6 +804,8 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
 
 
 _CMP_OPS = (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE)
+# wide results avoid clean registers (A/B knob: MYTHRIL_GPU_KEEP_CLEAN=0)
+KEEP_CLEAN = _os.environ.get("MYTHRIL_GPU_KEEP_CLEAN", "1") != "0"
 POOL_CAP = 128          # candidate values per leaf pool
 
 
