@@ -182,3 +182,59 @@ def test_inactive_lanes_do_not_store():
     _, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs), active=active)
     for a in range(64):
         assert limbs_to_int(pr[0, :, a]) == (2 * (a + 1) if a < 40 else 0)
+
+
+def _record_handlers(prog):
+    """(family, variant) of every translated record of prog."""
+    _, table = asm_sim.body_and_table()
+    off2 = {}
+    for h, off in enumerate(table):
+        bank, var, aop = h % 2, (h // 2) % asmgen.NVAR, h // (2 * asmgen.NVAR)
+        off2.setdefault(off, (asmgen.AOPS[aop], var))
+    rec, _ = asm_sim.translate(prog, 6)
+    return [off2.get(int(r[0]), ("PAD", 0)) for r in rec.reshape(-1, 8)]   # + zeroed pad
+
+
+def test_nw_variant_only_for_dead_root_conjuncts():
+    """A ROOT-fused compare nobody reads later takes the no-write variant
+    (only the root is updated); one whose value is read again (here by an
+    ITE) keeps writing its slot.  Both roots stay right (simulated)."""
+    x, y, z = N.bv_var("x", 256), N.bv_var("y", 256), N.bv_var("z", 256)
+    live = N.bv_cmp("bvule", x, y)                  # also the ITE's condition
+    dead = N.bv_cmp("bvult", z, x)                  # a root only
+    pick = N.ite(live, z, y)
+    roots = [live, dead, N.distinct(pick, N.bv_num(7, 256))]
+    prog = compile_constraints(roots)
+    fams = _record_handlers(prog)
+    ule = [var for f, var in fams if f == "ULE"]
+    ult = [var for f, var in fams if f == "ULT"]
+    assert ule and not any(var & asmgen.V_NW for var in ule)
+    assert ult and all(var & asmgen.V_NW for var in ult)
+    rng = random.Random(5)
+    asgs = [PA(vars={k: rng.choice([0, 1, 7, (1 << 256) - 1, rng.getrandbits(256)])
+                     for k in ("x", "y", "z")}) for _ in range(64)]
+    root, _, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+    for a, asg in enumerate(asgs):
+        assert bool(root[a]) == bool(R.eval_constraints(roots, asg)), a
+
+
+def test_index_mode_text_invariants():
+    """GPR-index mode is state, not brackets: an off never
+    directly precedes an on (s_set_gpr_idx_on sets index and mode in any
+    state), and in every handler the first instruction that touches VGPRs,
+    or the first branch, comes after the handler set the mode itself (a
+    handler may be entered with the mode left on by the previous one)."""
+    lines = [l.strip() for l in asmgen.generate()]
+    for a, b in zip(lines, lines[1:]):
+        assert not (a == "s_set_gpr_idx_off" and b.startswith("s_set_gpr_idx_on")), (a, b)
+    for i, t in enumerate(lines):
+        if not (t.startswith(".Lh") and t.endswith(":")):
+            continue
+        for u in lines[i + 1:]:
+            op = u.split(None, 1)[0] if u else ""
+            if op.startswith("s_set_gpr_idx_on") or op == "s_set_gpr_idx_off" or \
+                    op == "s_setpc_b64" or u.startswith("s_branch .Lbody_"):
+                break                 # (a heavy body sets the mode itself)
+            assert not (op.startswith("v_") or op.startswith("ds_") or
+                        op.startswith("global_") or op.startswith("scratch_") or
+                        op.startswith("s_cbranch") or op == "s_branch"), (t, u)
