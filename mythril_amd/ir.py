@@ -48,10 +48,11 @@ LDS_TIER = 6           # spill slots the assembly kernel keeps in LDS (mg_api.cp
 # use instead), "scratchK" (regenerated unless one of the first K scratch
 # slots is free), "always" (leaves are never spilled).  Regeneration costs
 # the generator's VALU; a scratch spill costs HBM traffic.  Default
-# "scratch4": 2.9x less HBM traffic than "spill" for 0.5 % of kernel time
-# (profiles/r02/leaf_remat_ab.json).
+# "scratch2": with the round-2 generator (49 VALU per leaf) as fast as
+# "scratch4" and "scratch6"/LDS-only slower (profiles/r02/remat_final/),
+# at well under half the HBM traffic.
 import os as _os
-LEAF_REMAT = _os.environ.get("MYTHRIL_GPU_LEAF_REMAT", "scratch4")
+LEAF_REMAT = _os.environ.get("MYTHRIL_GPU_LEAF_REMAT", "scratch2")
 
 
 class Unsupported(Exception):
