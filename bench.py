@@ -31,36 +31,76 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 SEED = 0x6D797468
+# stand-in query streams (mythril_amd/workloads.py): distinct queries per step
+STREAM_QUERIES = 256
+_STREAM = None
 
 
-def _compile_one(dag_id):
-    from mythril_amd.corpus import make_dag
+def workload_roots(workload, dag_id):
+    """The source DAG (list of root Bools) of unit ``dag_id``: a corpus DAG
+    (c2) or the dag_id-th distinct query of a stand-in stream (c3 / c4)."""
+    global _STREAM
+    if workload == "c2":
+        from mythril_amd.corpus import make_dag
+        return make_dag(dag_id, SEED)[0]
+    if _STREAM is None or _STREAM[0] != workload:
+        from mythril_amd import workloads as W
+        seen, out = set(), []
+        for q in W.queries(workload, 8 * STREAM_QUERIES):
+            key = tuple(c.id for c in q)
+            if key not in seen:
+                seen.add(key)
+                out.append(q)
+        _STREAM = (workload, out)
+    qs = _STREAM[1]
+    return qs[dag_id % len(qs)]
+
+
+def compile_unit(item):
+    """(workload, dag_id) -> (dag_id, Program, node count, int32-op weight)."""
     from mythril_amd.ir import compile_constraints
     from mythril_amd.roofline import dag_work
-    roots, _ = make_dag(dag_id, SEED)
+    workload, dag_id = item
+    roots = workload_roots(workload, dag_id)
     prog = compile_constraints(roots)
     nodes, weight = dag_work(roots, prog.table_sizes)
     return dag_id, prog, nodes, weight
 
 
-def build_corpus(n_dags, workers, dag_ids=None):
+def build_corpus(n_dags, workers, dag_ids=None, workload="c2", start="fork"):
+    """Compile the step's DAGs on ``workers`` host processes (fork before
+    any GPU initialisation; ``start="spawn"`` from a process that already
+    uses the GPU)."""
     ids = list(range(n_dags)) if dag_ids is None else list(dag_ids)
+    items = [(workload, d) for d in ids]
     if workers <= 1:
-        return [_compile_one(d) for d in ids]
+        return [compile_unit(it) for it in items]
     import multiprocessing as mp
-    ctx = mp.get_context("fork")
+    ctx = mp.get_context(start)
     with ctx.Pool(workers) as pool:
-        return sorted(pool.map(_compile_one, ids, chunksize=16), key=lambda t: t[0])
+        return sorted(pool.map(compile_unit, items, chunksize=16), key=lambda t: t[0])
 
 
-def my_dags(mode, n_dags, rank, world):
+def kernel_key(lib_digest, workload, dags, assign_log2, jit):
+    """What a traffic measurement (profiles/traffic.json) is valid for: the
+    generated assembly, the allocator's leaf policy, the code path and the
+    workload.  bench.py reports ``traffic`` only when every field matches."""
+    from mythril_amd import ir
+    return {"asm_digest": lib_digest, "leaf_remat": ir.LEAF_REMAT, "jit": bool(jit),
+            "workload": workload, "dags": dags, "assign_log2": assign_log2}
+
+
+def my_dags(mode, n_dags, rank, world, workload="c2"):
     """DAG ids this rank evaluates: every DAG (assignment axis) or its LPT
     share of a ``n_dags x world`` corpus (corpus axis)."""
     if mode == "assign" or world == 1:
         return list(range(n_dags))
     from mythril_amd import shard
     from mythril_amd.corpus import dag_target_nodes
-    costs = [dag_target_nodes(d, SEED) for d in range(n_dags * world)]
+    if workload == "c2":
+        costs = [dag_target_nodes(d, SEED) for d in range(n_dags * world)]
+    else:
+        costs = [1] * (n_dags * world)
     return shard.corpus_shard(costs, rank, world)
 
 
@@ -112,10 +152,9 @@ def all_sum(values, world, device=None):
     return t.tolist()
 
 
-def cpu_baseline(corpus, budget_s=20.0):
+def cpu_baseline(corpus, budget_s=20.0, workload="c2"):
     """Time the C restatement oracle on a bounded sample of the same workload
     (same DAGs, same generator) with all host cores."""
-    from mythril_amd.corpus import make_dag
     from oracle import build as obuild
     from oracle import evalref
     obuild.build()
@@ -129,7 +168,7 @@ def cpu_baseline(corpus, budget_s=20.0):
     t_total = 0.0
     per_dag = None
     for dag_id, prog, nodes, _ in sample:
-        roots, _ = make_dag(dag_id, SEED)
+        roots = workload_roots(workload, dag_id)
         S = evalref.serialize(roots, prog)
         if per_dag is None:
             n_cal = 16384
@@ -143,9 +182,9 @@ def cpu_baseline(corpus, budget_s=20.0):
         total_nodes += nodes * per_dag
     return {"value": total_nodes / t_total, "unit": "node-evals/s", "cores": threads,
             "kind": "port",
-            "sample": "%d corpus DAGs x %d generated assignments (%.3g node-evals, %.1f s); "
+            "sample": "%d %s DAGs x %d generated assignments (%.3g node-evals, %.1f s); "
                       "oracle/evalref.c restates z3 model evaluation (z3 not installed)"
-                      % (len(sample), per_dag, total_nodes, t_total)}
+                      % (len(sample), workload, per_dag, total_nodes, t_total)}
 
 
 def main():
@@ -153,13 +192,20 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--dags", type=int, default=4096)
+    ap.add_argument("--workload", choices=("c2", "c3", "c4"), default="c2",
+                    help="c2: synthetic corpus (default, BASELINE configs[1]); c3 / c4: the "
+                         "BECToken / token+WalletLibrary stand-in query streams")
+    ap.add_argument("--dags", type=int, default=None,
+                    help="DAGs per step (default 4096 for c2, %d distinct queries for c3/c4)"
+                         % STREAM_QUERIES)
     ap.add_argument("--assign-log2", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", choices=("assign", "corpus"), default="assign",
                     help="assignment axis (default, C2) or corpus axis (C5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
+    if args.dags is None:
+        args.dags = 4096 if args.workload == "c2" else STREAM_QUERIES
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,7 +215,8 @@ def main():
     ncpu = os.cpu_count() or 1
     workers = max(1, min(16, ncpu // max(1, world)))
     t0 = time.time()
-    corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world))
+    corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world, args.workload),
+                          args.workload)
     t_compile = time.time() - t0
 
     import torch
@@ -226,15 +273,30 @@ def main():
         evals = nodes_all * n_assign * args.steps
         ops_launch = weight_per_lane * n_assign
         achieved = ops_launch / (kern_ms / 1000.0)
-        traffic = None
+        key = kernel_key(eng.lib.mg_asm_digest().decode(), args.workload, args.dags,
+                         args.assign_log2, False)
+        traffic, traffic_note = None, "no profiles/traffic.json"
         if os.path.exists(args.traffic_json):
             try:
                 with open(args.traffic_json) as fh:
                     tj = json.load(fh)
-                if tj.get("dags") == args.dags and tj.get("assign_log2") == args.assign_log2:
+                got = tj.get("kernel_key")
+                if got == key:
                     traffic = tj.get("hbm_bytes_per_launch")
-            except (OSError, ValueError):
-                traffic = None
+                    traffic_note = ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch of this "
+                                    "kernel (profiles/traffic.json, same kernel_key)")
+                else:
+                    diff = sorted(k for k in key if (got or {}).get(k) != key[k])
+                    traffic_note = "profiles/traffic.json is for another kernel (%s differ)" % \
+                        ", ".join(diff)
+            except (OSError, ValueError) as e:
+                traffic_note = "profiles/traffic.json unreadable: %s" % e
+        workload_txt = {
+            "c2": "C2 synthetic corpus: %d random 256-bit DAGs (64-512 nodes)" % args.dags,
+            "c3": "C3 stand-in stream: %d distinct BECToken-shaped integer-overflow queries "
+                  "(mythril_amd/workloads.py)" % args.dags,
+            "c4": "C4 stand-in stream: %d distinct token + WalletLibrary keccak/mapping queries "
+                  "(mythril_amd/workloads.py)" % args.dags}[args.workload]
         out = {
             "metric": "constraint-node evals/sec",
             "value": evals / elapsed,
@@ -248,8 +310,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u32x8 (256-bit bit-vectors)",
             "data": "synthetic (corpus seed 0x6d797468, device-generated candidates)",
-            "config": {"workload": ("C2 synthetic corpus: %d random 256-bit DAGs (64-512 nodes) "
-                                    "x 2^%d assignments per GPU" % (args.dags, args.assign_log2))
+            "config": {"workload": ("%s x 2^%d assignments per GPU" % (workload_txt, args.assign_log2))
                        if args.shard == "assign" else
                        ("C5 corpus axis: %d random 256-bit DAGs (64-512 nodes) per GPU, LPT-"
                         "sharded, x 2^%d assignments each" % (args.dags, args.assign_log2)),
@@ -258,13 +319,14 @@ def main():
                        "shard": args.shard, "parallelism": "dp%d" % world},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
-                         "traffic": traffic, "kernel_ms": kern_ms,
+                         "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kern_ms,
                          "int32_ops_per_launch": ops_launch},
+            "kernel_key": key,
             "sat_dags": sat_dags,
             "compile_s": round(t_compile, 2),
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(corpus)
+            out["cpu_baseline"] = cpu_baseline(corpus, workload=args.workload)
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -39,16 +39,22 @@ typedef struct mg_ctx mg_ctx;
 typedef struct mg_prog mg_prog;
 typedef struct mg_batch mg_batch;
 
-/* Device candidate generator for one leaf (free variable / table cell).
- * A draw r0 = SplitMix64(seed ^ salt ^ index) picks a class by
- * mulhi(r0 >> 32, 100):
- *   < pct_uniform                    r0 in limbs 0-1; limb k = 2..7 is m ^ (m >> 16),
- *                                    m = (x + k * 0x9E3779B9) * 0x85EBCA6B, x = lo(r0) ^ hi(r0)
- *                                    (mod 2^32; masked to width)
- *   < pct_small                      r0 (< 2^64)
- *   < pct_boundary                   {0, 1, 2^(w-1), 2^w-1, 2^k+1, 2^k-1}
- *   otherwise                        consts[pool_off + e] + {-1, 0, +1}
- * (thresholds are cumulative percentages). */
+/* Device candidate generator for one leaf (free variable / table cell),
+ * generator v7 (restated bit-exactly by oracle/gen_ref.py):
+ *   salt = prog_seed * 0xD1B54A32D192ED03 ^ (leaf + 1) * 0x8CB92BA72F3D8DD7
+ *   r0   = SplitMix64(seed ^ salt ^ index)          (one step, state += golden)
+ *   x    = lo(r0) ^ hi(r0)                          (32 bits)
+ *   cls  = mulhi(x * 0x2545F491 mod 2^32, 100)      (not from emitted value bits)
+ * and by class (thresholds are cumulative percentages):
+ *   pct_uniform <= cls < pct_small   r0 (< 2^64)
+ *   pct_small <= cls < pct_boundary  {0, 1, 2^(w-1), 2^256-1, 2^k+1, 2^k-1},
+ *                                    kind = mulhi(lo, 6), k = mulhi(lo * 0x9E3779B1, w)
+ *   cls >= pct_boundary, pool_n > 0  consts[pool_off + e] + delta - 1,
+ *                                    e = mulhi(lo, pool_n), delta = mulhi(lo * 0x85EBCA6B, 3)
+ *   otherwise (uniform)              r0 in limbs 0-1; limb pair k = 1..3 is
+ *                                    x * C_k + r0 (mod 2^64), C = 0x85EBCA6B,
+ *                                    0xC2B2AE35, 0x27D4EB2F
+ * every value masked to the leaf's width. */
 typedef struct mg_leafgen {
     uint32_t width;
     uint32_t pool_off;
@@ -66,6 +72,11 @@ typedef struct mg_gen {
 int mg_init(int device, mg_ctx** out);
 void mg_free(mg_ctx* ctx);
 const char* mg_last_error(const mg_ctx* ctx);
+/* Device time (ms, HIP events on the context stream) of the last synchronous
+ * mg_eval / mg_eval_gen / mg_search / mg_batch_search: the evaluation or
+ * search launches only (no copies, no witness regeneration).  Feeds
+ * SolverStatistics' kernel time (reference solver_statistics.py:29-43). */
+float mg_last_kernel_ms(const mg_ctx* ctx);
 /* CU count, device name; available after mg_init. */
 int mg_device_info(mg_ctx* ctx, char* name, size_t name_len, int* n_cus);
 

@@ -153,8 +153,6 @@ def hid(aop: int, variant: int, bank: int) -> int:
 
 
 NUM_HANDLERS = len(AOPS) * NVAR * 2
-# log2 of the byte alignment of every handler entry (0: packed)
-HANDLER_ALIGN = int(os.environ.get("MYTHGPU_HANDLER_ALIGN", "0"))
 
 
 def canonical(h: int) -> int:
@@ -1013,6 +1011,7 @@ def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
 GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
 PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
+CLS_MUL = 0x2545F491                              # class remix (generator v7)
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
 S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
@@ -1108,8 +1107,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), OP_IDX_LO))
     a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), OP_IDX_HI))
     sm64(a, st, z, tt)
-    a("s_movk_i32 %s, 100" % s(S_T))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(z[1]), s(S_T)))
     # ---- uniform values for every lane: r0 in limbs 0-1 (small lanes keep
     # only those), limb pair k = 1..3 is x * C_k + r0 (mod 2^64) with
     # x = lo ^ hi of r0: one v_mad_u64_u32 per two limbs (v6; v4 spent a
@@ -1118,6 +1115,12 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     dst = X if dst is None else dst
     a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(tt[0]), v(z[0]), v(z[1])))
+    # v7: class = mulhi(x * CLS_MUL, 100) — from a remix of x, not from bits
+    # that are emitted as value bits (oracle/gen_ref.py gen_class)
+    a("s_mov_b32 %s, 0x%x" % (s(S_T), CLS_MUL))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(tt[0]), s(S_T)))
+    a("s_movk_i32 %s, 100" % s(S_T + 1))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(S_T + 1)))
     for k, c in enumerate(PAIR_MUL):
         a("s_mov_b32 %s, 0x%x" % (s(S_PAIR + k), c))
     for k in range(3):
@@ -1987,10 +1990,6 @@ def generate() -> List[str]:
     a("s_load_dwordx2 %s, %s, 0x8" % (sp(S_CONST), IN["desc"]))
     a("s_load_dwordx2 %s, %s, 0x30" % (sp(S_CODE), IN["desc"]))
     a("v_mov_b32 %s, 1" % OP_ROOT)
-    if HANDLER_ALIGN:
-        # .Lbase at the same offset modulo the alignment in both kernel
-        # instantiations (the query launch's offsets must fit the other)
-        a(".p2align %d" % HANDLER_ALIGN)
     a("s_getpc_b64 %s" % sp(S_BASE))
     a.label(".Lbase_%=")
     a("s_bitcmp1_b32 %s, 1" % IN["mode"])
@@ -2020,8 +2019,6 @@ def generate() -> List[str]:
             dc_v, w32_v, ip_v = bool(var & V_DC), bool(var & V_W32), bool(var & V_IP)
             a.nw = bool(var & V_NW)
             for bank in (0, 1):
-                if HANDLER_ALIGN:
-                    a(".p2align %d" % HANDLER_ALIGN)
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
                 if name == "LEAFD":
                     h_leafd(a, bank, var)

@@ -42,7 +42,27 @@ struct mg_ctx {
     // grow-only device workspace for synchronous calls
     void* ws = nullptr;
     size_t ws_size = 0;
+    // device time of the last synchronous eval / search (HIP events around
+    // its launches on the context stream; mg_last_kernel_ms)
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    float last_ms = 0.f;
 };
+
+static void timing_begin(mg_ctx* ctx) {
+    ctx->last_ms = 0.f;
+    if (ctx->ev0) (void)hipEventRecord(ctx->ev0, ctx->stream);
+}
+
+static void timing_end(mg_ctx* ctx) {
+    if (ctx->ev1) (void)hipEventRecord(ctx->ev1, ctx->stream);
+}
+
+// after the stream was synchronised
+static void timing_read(mg_ctx* ctx) {
+    float ms = 0.f;
+    if (ctx->ev0 && ctx->ev1 && hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1) == hipSuccess)
+        ctx->last_ms = ms;
+}
 
 struct mg_prog {
     mg_ctx* ctx = nullptr;
@@ -175,6 +195,10 @@ int mg_init(int device, mg_ctx** out) {
         delete ctx;
         return MG_E_HIP;
     }
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+        mg_free(ctx);
+        return MG_E_HIP;
+    }
     if (const char* l = getenv("MYTHGPU_LDS_SLOTS")) {
         const long v = strtol(l, nullptr, 10);
         if (v >= 0 && v <= MG_MAX_LDS) ctx->lds_slots = (uint32_t)v;
@@ -202,11 +226,15 @@ void mg_free(mg_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_btab) (void)hipFree(ctx->d_btab);
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 
 const char* mg_last_error(const mg_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }
+
+float mg_last_kernel_ms(const mg_ctx* ctx) { return ctx ? ctx->last_ms : 0.f; }
 
 int mg_device_info(mg_ctx* ctx, char* name, size_t name_len, int* n_cus) {
     if (!ctx) return MG_E_ARG;
@@ -367,13 +395,16 @@ int mg_eval(mg_ctx* ctx, const mg_prog* prog, const uint32_t* leaves_soa, uint64
     run.words_per_prog = words;
     if (leaf_b)
         HIPCHECK(ctx, hipMemcpyAsync(base, leaves_soa, leaf_b, hipMemcpyHostToDevice, ctx->stream));
+    timing_begin(ctx);
     HIPCHECK(ctx, launch(ctx, 0, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
+    timing_end(ctx);
     HIPCHECK(ctx, hipMemcpyAsync(root_bits, run.root_bits, root_b, hipMemcpyDeviceToHost,
                                  ctx->stream));
     if (probes && probe_b)
         HIPCHECK(ctx, hipMemcpyAsync(probes, run.probes, probe_b, hipMemcpyDeviceToHost,
                                      ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    timing_read(ctx);
     return MG_OK;
 }
 
@@ -400,7 +431,9 @@ int mg_eval_gen(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_
     run.seed = gen->seed;
     run.first_index = gen->first_index;
     if (leaf_b) HIPCHECK(ctx, hipMemsetAsync(run.leaves_out, 0, leaf_b, ctx->stream));
+    timing_begin(ctx);
     HIPCHECK(ctx, launch(ctx, 1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
+    timing_end(ctx);
     HIPCHECK(ctx, hipMemcpyAsync(root_bits, run.root_bits, root_b, hipMemcpyDeviceToHost,
                                  ctx->stream));
     if (probe_b)
@@ -410,6 +443,7 @@ int mg_eval_gen(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_
         HIPCHECK(ctx, hipMemcpyAsync(leaves_out, run.leaves_out, leaf_b, hipMemcpyDeviceToHost,
                                      ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    timing_read(ctx);
     return MG_OK;
 }
 
@@ -431,6 +465,7 @@ int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_ca
     if (rc) return rc;
     unsigned long long* d_first = (unsigned long long*)ws;
     HIPCHECK(ctx, hipMemsetAsync(d_first, 0xFF, 8, ctx->stream));
+    timing_begin(ctx);
     for (uint64_t done = 0; done < n_cand; done += MG_SEARCH_LAUNCH) {
         mg_run run = empty_run();
         run.n_assign = n_cand - done < MG_SEARCH_LAUNCH ? n_cand - done : MG_SEARCH_LAUNCH;
@@ -441,9 +476,11 @@ int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_ca
         run.skip_solved = 1;
         HIPCHECK(ctx, launch(ctx, 1, prog->d_desc, 1, run, prog->n_lds, ctx->stream));
     }
+    timing_end(ctx);
     unsigned long long h = ~0ull;
     HIPCHECK(ctx, hipMemcpyAsync(&h, d_first, 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    timing_read(ctx);
     if (h != ~0ull) *first_sat = (int64_t)h;
     if (*first_sat >= 0 && witness_leaves && prog->n_leaves) {
         // regenerate the winning candidate (counter-based streams: no gather)
@@ -539,6 +576,7 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
     if (rc) return rc;
     unsigned long long* d_first = (unsigned long long*)ws;
     HIPCHECK(ctx, hipMemsetAsync(d_first, 0xFF, (size_t)b->n * 8, ctx->stream));
+    timing_begin(ctx);
     // every program's whole candidate range, queued with no host round trip;
     // waves of solved programs exit at once (skip_solved)
     for (uint64_t done = 0; done < n_cand; done += MG_SEARCH_LAUNCH) {
@@ -554,6 +592,7 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
             HIPCHECK(ctx, launch(ctx, 1, b->d_descs + p0, np, run, b->max_lds, ctx->stream));
         }
     }
+    timing_end(ctx);
     if (witness_leaves) {
         // one launch regenerates every program's winning candidate: lane 0
         // of program p evaluates candidate first_sat[p] (solved programs only)
@@ -577,6 +616,7 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
     HIPCHECK(ctx, hipMemcpyAsync(h.data(), d_first, (size_t)b->n * 8, hipMemcpyDeviceToHost,
                                  ctx->stream));
     HIPCHECK(ctx, hipStreamSynchronize(ctx->stream));
+    timing_read(ctx);
     for (uint32_t i = 0; i < b->n; ++i) first_sat[i] = h[i] == ~0ull ? -1 : (int64_t)h[i];
     return MG_OK;
 }

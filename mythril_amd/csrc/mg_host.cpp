@@ -13,6 +13,11 @@
 
 #include "mg_host.h"
 
+// LEAFD / RELOADD variants are the slot number, with MGA_V_WAITD as the wait
+// flag above the slot bits (wait_vm below adds it to the handler id): more
+// slots than that would alias slot d + 16 with slot d's WAITD handler
+static_assert(MG_NREG <= MGA_V_WAITD, "register slots overlap the WAITD variant bit");
+
 static int fail(std::string* err, int code, const char* fmt, ...) {
     char buf[512];
     va_list ap;

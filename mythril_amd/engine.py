@@ -22,7 +22,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
            "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_keccak256", "mg_version", "mg_config",
-           "mg_translate", "mg_asm_digest")
+           "mg_translate", "mg_asm_digest", "mg_last_kernel_ms")
 
 
 class EngineUnavailable(RuntimeError):
@@ -82,6 +82,8 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
         lib.mg_config.argtypes = [p, u32]
         lib.mg_asm_digest.restype = C.c_char_p
+        lib.mg_last_kernel_ms.argtypes = [p]
+        lib.mg_last_kernel_ms.restype = C.c_float
         pu32 = C.POINTER(u32)
         lib.mg_translate.argtypes = [p, u32, u32, u32, p, u32, p, u32, pu32, p, u32, pu32]
         for name in EXPORTS:
@@ -153,6 +155,10 @@ class Engine:
         if rc != 0:
             raise EngineError("%s failed (%d): %s" % (what, rc,
                               self.lib.mg_last_error(self._ctx).decode(errors="replace")))
+
+    def last_kernel_ms(self) -> float:
+        """Device time of the last synchronous eval / search call."""
+        return float(self.lib.mg_last_kernel_ms(self._ctx))
 
     def load(self, program: Program, leafgen: Optional[Sequence[LeafGen]] = None,
              prog_seed: int = 0) -> LoadedProgram:
@@ -267,6 +273,42 @@ class Engine:
         for k, (lp, f) in enumerate(zip(loaded, first.tolist())):
             out.append((-1, None) if f < 0 else (f, wit[k, :len(lp.program.leaves)].copy()))
         return out
+
+
+def record_handlers(program: Program, lds_slots: int = 6) -> List[int]:
+    """Host-only (no GPU): the assembly-interpreter handler id of every
+    record ``mg_load_program`` would upload for ``program`` (the translator
+    run with an identity offset table), in execution order.  ``lds_slots``
+    is the context's LDS spill tier (``MYTHGPU_LDS_SLOTS``, default 6)."""
+    from . import asmgen
+    lib = load_library()
+    code = np.ascontiguousarray(program.code, dtype=np.uint32)
+    n_ins = code.shape[0]
+    ident = np.arange(asmgen.NUM_HANDLERS, dtype=np.uint32)
+    max_rec = (2 * n_ins + 3) * 8
+    max_mask = (2 * n_ins + 4) * 16
+    rec = np.zeros(max_rec, dtype=np.uint32)
+    masks = np.zeros(max_mask, dtype=np.uint32)
+    nrw, nmw = C.c_uint32(), C.c_uint32()
+    rc = lib.mg_translate(_ptr(code), n_ins, program.consts.shape[0],
+                          min(program.n_lds, lds_slots), _ptr(ident), asmgen.NUM_HANDLERS,
+                          C.cast(rec.ctypes.data, C.POINTER(C.c_uint32)), max_rec, C.byref(nrw),
+                          _ptr(masks), max_mask, C.byref(nmw))
+    if rc != 0:
+        raise EngineError("mg_translate failed (%d)" % rc)
+    return [int(h) for h in rec[:nrw.value:8][:-1]]      # the last record is a zeroed pad
+
+
+def handler_variants(program: Program, lds_slots: int = 6):
+    """The set of (family, canonical variant) the program executes (every
+    record runs on every lane: programs are straight-line)."""
+    from . import asmgen
+    out = set()
+    for h in record_handlers(program, lds_slots):
+        c = asmgen.canonical(h)
+        aop, var = c // (2 * asmgen.NVAR), (c // 2) % asmgen.NVAR
+        out.add((asmgen.AOPS[aop], var))
+    return out
 
 
 def unpack_bits(bits: np.ndarray, n: int) -> np.ndarray:

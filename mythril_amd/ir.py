@@ -119,6 +119,9 @@ class Program:
     # search mode: fixed parts of every candidate model (abi.Plan: the ABI
     # offset words and calldatasize the query was compiled under)
     presets: object = None
+    # search mode: the independent group's constraint node ids (model.py's
+    # group-miss memo)
+    group_key: object = None
 
     @property
     def solved(self) -> bool:

@@ -102,7 +102,9 @@ class SolverStatistics:
         self.gpu_hits = 0
         self.gpu_candidates = 0
         self.gpu_time = 0.0
-        self.kernel_time = 0.0
+        self.kernel_time = 0.0          # device time of the search launches (HIP events)
+        self.memo_misses = 0            # queries answered "miss" by the group-miss memo
+        self.gated = 0                  # queries whose compile estimate exceeded the budget
         self.fallbacks = 0
         self.unsupported = 0
         self.errors = 0
@@ -111,11 +113,11 @@ class SolverStatistics:
 
     def gpu_report(self) -> str:
         return ("GPU pre-filter: queries: {} hits: {} fallbacks: {} unsupported: {} errors: {} "
-                "rejected by z3: {}\nGPU candidates: {} time: {:.3f}s (kernel {:.3f}s; "
-                "{})").format(
+                "rejected by z3: {} memo misses: {} compile-gated: {}\nGPU candidates: {} "
+                "time: {:.3f}s (kernel {:.3f}s; {})").format(
             self.gpu_queries, self.gpu_hits, self.fallbacks, self.unsupported, self.errors,
-            self.rejected, self.gpu_candidates, self.gpu_time, self.kernel_time,
-            ", ".join("%s %.3fs" % (k, self.phase[k]) for k in PHASES))
+            self.rejected, self.memo_misses, self.gated, self.gpu_candidates, self.gpu_time,
+            self.kernel_time, ", ".join("%s %.3fs" % (k, self.phase[k]) for k in PHASES))
 
     def __repr__(self):
         return "Query count: {} \nSolver time: {}\n{}".format(self.query_count, self.solver_time,
@@ -133,11 +135,16 @@ class _Phase:
         return self
 
     def __exit__(self, *exc):
-        dt = time.perf_counter() - self.t0
-        stats.phase[self.name] += dt
-        if self.name == "search":
-            stats.kernel_time += dt
+        stats.phase[self.name] += time.perf_counter() - self.t0
         return False
+
+
+def _count_kernel(eng) -> None:
+    """Device time of the engine's last search (HIP events around its
+    launches inside libmythgpu, ``mg_last_kernel_ms``)."""
+    ms = getattr(eng, "last_kernel_ms", None)
+    if ms is not None:
+        stats.kernel_time += ms() / 1000.0
 
 
 stats = SolverStatistics()
@@ -292,6 +299,7 @@ def _compile_search(nodes: Sequence[N.Node], probes: Sequence[N.Node] = ()) -> P
         _SEARCH_CACHE.move_to_end(key)
         return prog
     prog = _compile_search_uncached(nodes, probes)
+    prog.group_key = _group_key(nodes)
     _SEARCH_CACHE[key] = prog
     if len(_SEARCH_CACHE) > SEARCH_CACHE_SIZE:
         _SEARCH_CACHE.popitem(last=False)
@@ -406,40 +414,146 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
     (the corpus axis, mythril_amd/shard.py), each device searches its share
     in its own host thread (the C ABI releases the GIL; one context per
     device), and the results come back in program order as
-    (first index, witness Assignment) or (-1, None)."""
+    (first index, witness Assignment) or (-1, None).  A single program on
+    several devices is split on the assignment axis instead
+    (:func:`search_assignment_axis`)."""
     from .shard import lpt_assign
     devices = list(DEVICES) or [0]
+    if len(progs) == 1 and len(devices) > 1:
+        return [search_assignment_axis(progs[0], n_cand, devices)]
     if len(devices) == 1 or len(progs) < 2:
         eng = get_engine(devices[0])
         with _Phase("load"):
             loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
         with _Phase("search"):
             hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
+            _count_kernel(eng)
             return [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
                     for lp, h in zip(loaded, hits)]
     parts = lpt_assign([float(p.n_ins) for p in progs], len(devices))
     out: List = [None] * len(progs)
-    errors: List[BaseException] = []
 
     def run(dev, idx):
+        eng = get_engine(dev)
+        loaded = [eng.load(progs[i], search_leafgen(progs[i]), prog_seed=0) for i in idx]
+        hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
+        _count_kernel(eng)
+        for i, lp, h in zip(idx, loaded, hits):
+            out[i] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
+    with _Phase("search"):
+        _on_devices(run, [(d, idx) for d, idx in zip(devices, parts) if idx])
+    return out
+
+
+def _on_devices(fn, jobs) -> None:
+    """Run ``fn(*job)`` for every job, one host thread per job (one device
+    context each; the C ABI releases the GIL); the first error re-raises."""
+    import threading
+    errors: List[BaseException] = []
+
+    def body(*a):
         try:
-            eng = get_engine(dev)
-            loaded = [eng.load(progs[i], search_leafgen(progs[i]), prog_seed=0) for i in idx]
-            for i, lp, h in zip(idx, loaded, eng.batch_search(loaded, SEARCH_SEED, n_cand)):
-                out[i] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
+            fn(*a)
         except BaseException as e:  # noqa: BLE001 - re-raised in the caller
             errors.append(e)
-    import threading
-    with _Phase("search"):
-        threads = [threading.Thread(target=run, args=(d, idx)) for d, idx in zip(devices, parts)
-                   if idx]
-        for t in threads:
-            t.start()
-        for t in threads:
-            t.join()
+    threads = [threading.Thread(target=body, args=job) for job in jobs]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
     if errors:
         raise errors[0]
-    return out
+
+
+def search_assignment_axis(prog: Program, n_cand: int, devices: Sequence[int]):
+    """One program's candidate range split over devices (SURVEY §8e
+    assignment axis): device g searches candidate indices
+    [g*n/G, (g+1)*n/G) of the same counter-based stream, and the host
+    reduces MIN over the devices' first satisfying indices — the index a
+    single-device sweep of [0, n) returns (the ranges are ordered and
+    disjoint).  Only the seed and the range travel; the winning witness is
+    regenerated on the device that found it."""
+    G = len(devices)
+    bounds = [n_cand * g // G for g in range(G + 1)]
+    res: List = [None] * G
+
+    def run(g, dev):
+        eng = get_engine(dev)
+        lp = eng.load(prog, search_leafgen(prog), prog_seed=0)
+        n = bounds[g + 1] - bounds[g]
+        h = eng.search(lp, SEARCH_SEED, n, first_index=bounds[g]) if n else (-1, None)
+        _count_kernel(eng)
+        res[g] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
+    with _Phase("search"):
+        _on_devices(run, list(enumerate(devices)))
+    found = [r for r in res if r[0] >= 0]
+    return min(found, key=lambda r: r[0]) if found else (-1, None)
+
+
+# Group-miss memo.  A group's search program, leaf generator and candidate
+# streams are functions of its constraint nodes alone (hash-consed ids), so
+# a group that missed on candidates [0, N) misses again on any [0, n <= N):
+# such a query is answered "miss" without compiling or launching anything.
+# A group that EXTENDS a missed group (LASER appends one JUMPI condition at a
+# time, so successive is_possible groups grow) is not searched either: the
+# superset is satisfiable only where the subset is, and the subset's search
+# already failed — z3 decides it, as it decides every miss.  This never
+# changes an answer (UNSAT is only concluded by z3), only where the time goes.
+GROUP_MISS_SIZE = 1 << 14
+SUPERSET_SKIP = True
+_group_miss: "Dict[frozenset, int]" = {}
+_miss_index: "Dict[int, List[frozenset]]" = {}
+# compile-cost gate: estimated host compile time per source node of an
+# uncached group (Python compiler; measured ~0.035 ms/node on C3/C4 queries)
+COMPILE_MS_PER_NODE = 0.04
+
+
+def _group_key(nodes: Sequence[N.Node]) -> frozenset:
+    return frozenset(n.id for n in nodes)
+
+
+def _known_miss(key: frozenset, n_cand: int) -> bool:
+    if _group_miss.get(key, -1) >= n_cand:
+        return True
+    if not SUPERSET_SKIP:
+        return False
+    for c in key:
+        for m in _miss_index.get(c, ()):
+            if len(m) < len(key) and m <= key:        # a proper subset missed
+                return True
+    return False
+
+
+def _note_miss(key: frozenset, n_cand: int) -> None:
+    if key in _group_miss:
+        _group_miss[key] = max(_group_miss[key], n_cand)
+        return
+    if len(_group_miss) >= GROUP_MISS_SIZE:
+        old = next(iter(_group_miss))
+        del _group_miss[old]
+        lst = _miss_index.get(min(old), [])
+        if old in lst:
+            lst.remove(old)
+    _group_miss[key] = n_cand
+    if key:
+        _miss_index.setdefault(min(key), []).append(key)
+
+
+def clear_search_memos() -> None:
+    """Forget compiled groups and group misses (tools/search_bench.py's cold
+    runs)."""
+    global _SEARCH_CACHE
+    _SEARCH_CACHE = None
+    _group_miss.clear()
+    _miss_index.clear()
+
+
+def _compile_estimate_ms(buckets, keys) -> float:
+    cache = _SEARCH_CACHE or {}
+    todo = [b for b, k in zip(buckets, keys) if (tuple(n.id for n in b), ()) not in cache]
+    if not todo:
+        return 0.0
+    return COMPILE_MS_PER_NODE * len(N.topo_order([n for b in todo for n in b]))
 
 
 def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
@@ -448,21 +562,38 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     group in one batched launch sequence and join the group witnesses, so the
     hit probability is per group rather than their product.  The candidate
     count is sized to ``budget_ms``; the whole range runs on the device with
-    no host round trip (mg_search / mg_batch_search)."""
+    no host round trip (mg_search / mg_batch_search).  The group-miss memo
+    answers repeated (or extended) missed groups at once, and a query whose
+    estimated compile time exceeds the budget is not searched."""
     buckets = dependence_buckets(nodes)
+    keys = [_group_key(b) for b in buckets]
+    if any(_known_miss(k, SEARCH_CANDIDATES) for k in keys):
+        stats.memo_misses += 1
+        return None
+    if _compile_estimate_ms(buckets, keys) > budget_ms:
+        stats.gated += 1
+        return None
     with _Phase("compile"):
         progs = [_compile_search(b) for b in buckets]
     n_cand = _n_cand(progs, budget_ms)
-    if len(progs) > 1:
+    if any(_known_miss(k, n_cand) for k in keys):
+        stats.memo_misses += 1
+        return None
+    devices = list(DEVICES) or [0]
+    if len(progs) > 1 or len(devices) > 1:
         hits = batch_search_devices(progs, n_cand)
     else:
-        eng = get_engine()
+        eng = get_engine(devices[0])
         with _Phase("load"):
             lp = eng.load(progs[0], search_leafgen(progs[0]), prog_seed=0)
         with _Phase("search"):
             h = eng.search(lp, SEARCH_SEED, n_cand)
+            _count_kernel(eng)
             hits = [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)]
     stats.gpu_candidates += sum(n_cand if i < 0 else i + 1 for i, _ in hits)
+    for k, (i, _) in zip(keys, hits):
+        if i < 0:
+            _note_miss(k, n_cand)
     if any(i < 0 for i, _ in hits):
         return None
     return _merge([a for _, a in hits]), progs
@@ -527,26 +658,26 @@ def _wrap(z3_model, assignment, progs):
     return Model([z3_model], assignment, progs)
 
 
-def _accept(constraints, assignment, progs, deadline: float):
-    """get_model's rule for a GPU witness: re-verified by z3 (substitute +
-    simplify, then a genuine z3 model) when the constraints are z3 ASTs and
-    z3 is present; otherwise accepted as is — it was evaluated bit-exactly
-    on the device.  Returns the model, or None when z3 rejects it."""
+def _accept(constraints, assignment, progs, timeout_ms: int):
+    """get_model's rule for a GPU witness (north_star: every witness is
+    re-verified by z3 before a model is returned): whenever z3 is present —
+    z3 ASTs as given, mirror DAG nodes through ``z3bridge.to_z3`` —
+    substitute + simplify must give True and a genuine z3 model is returned.
+    Without z3 the witness is returned as is (it was evaluated bit-exactly on
+    the device).  None when z3 rejects it."""
     if z3bridge.available():
+        memo: Dict[int, object] = {}
         raws = [getattr(c, "raw", c) for c in constraints]
-        if raws and all(not isinstance(r, N.Node) for r in raws):
+        raws = [z3bridge.to_z3(r, memo) if isinstance(r, N.Node) else r for r in raws]
+        if raws:
             with _Phase("verify"):
-                m = z3bridge.verify(raws, assignment, _remaining_ms(deadline))
+                m = z3bridge.verify(raws, assignment, timeout_ms)
             if m is None:
                 stats.rejected += 1
                 log.warning("GPU witness rejected by z3; falling back")
                 return None
             return _wrap(m, assignment, progs)
     return Model(None, assignment, progs)
-
-
-def _remaining_ms(deadline: float) -> int:
-    return max(1, int((deadline - time.perf_counter()) * 1000.0))
 
 
 # Hand-over from batch_is_possible to get_model (bounded, oldest dropped):
@@ -578,7 +709,7 @@ def _take(d: dict, key):
 _engine_failed: Optional[str] = None
 
 
-def _prefilter(key, constraints, timeout: int, deadline: float):
+def _prefilter(key, constraints, timeout: int):
     """GPU path of get_model: a model, or None (miss / rejected witness)."""
     global _engine_failed
     hit = _take(_batch_witness, key)
@@ -598,7 +729,7 @@ def _prefilter(key, constraints, timeout: int, deadline: float):
             stats.gpu_time += time.perf_counter() - t0
         if hit is None:
             return None
-    m = _accept(constraints, hit[0], hit[1], deadline)
+    m = _accept(constraints, hit[0], hit[1], timeout)
     if m is not None:
         stats.gpu_hits += 1
     return m
@@ -616,13 +747,10 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         if type(constraint) == bool and not constraint:
             raise UnsatError
     constraints = [c for c in constraints if type(c) != bool]
-    # one deadline for the whole query: GPU search, witness verification and
-    # the z3 fallback together stay within the reference's timeout
-    deadline = time.perf_counter() + timeout / 1000.0
 
     if not minimize and not maximize:
         try:
-            m = _prefilter(key, constraints, timeout, deadline)
+            m = _prefilter(key, constraints, timeout)
             if m is not None:
                 return m
         except Unsupported as e:
@@ -632,7 +760,10 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
             stats.errors += 1
             log.debug("GPU pre-filter failed (%s: %s); falling back to z3", type(e).__name__, e)
         stats.fallbacks += 1
-    return _z3_check(constraints, minimize, maximize, _remaining_ms(deadline))
+    # the fallback gets the reference's own timeout (support/model.py:26-31),
+    # not what the pre-filter left of it: a GPU miss must not turn a query z3
+    # solves near its timeout into an ``unknown`` -> UnsatError prune
+    return _z3_check(constraints, minimize, maximize, timeout)
 
 
 def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool]:
@@ -684,8 +815,15 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
                 found = [next(hits) for _ in progs]
                 stats.gpu_queries += 1
                 stats.gpu_candidates += sum(n_cand if k < 0 else k + 1 for k, _ in found)
+                for p, (k, _) in zip(progs, found):
+                    if k < 0 and p.group_key is not None:
+                        _note_miss(p.group_key, n_cand)
                 if any(k < 0 for k, _ in found):
-                    _remember(_gpu_missed, cs, True)
+                    # the set goes straight to z3 only when the batch searched
+                    # it as far as get_model alone would have; otherwise
+                    # get_model runs its own (budgeted) search
+                    if n_cand >= _n_cand(progs, min(timeout, SEARCH_BUDGET_MS)):
+                        _remember(_gpu_missed, cs, True)
                 else:
                     a = _merge([w for _, w in found])
                     _remember(_batch_witness, cs, (a, progs))

@@ -33,7 +33,7 @@ Steps, over the lowered DAG (``ir._Lowerer``):
 
 Mythril's own solver never sees these programs; this is the GPU search's
 way of reaching the models z3 would construct for the same queries
-(``laser/ethereum/function_managers/keccak_function_manager.py``'s
+(``laser/ethereum/keccak_function_manager.py``'s
 ``inverse(f(x)) = x``, ``transaction/symbolic.py``'s actor ``Or``, the
 dispatcher's selector equalities)."""
 

@@ -449,8 +449,10 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
     uint64_t s = seed ^ (prog_seed * 0xD1B54A32D192ED03ull) ^
                  ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull) ^ idx;   /* v5 */
     uint64_t r0 = sm64(&s);
-    /* v2 range reduction: multiply-high (Lemire) instead of modulo */
-    uint32_t cls = mulhi32((uint32_t)(r0 >> 32), 100u), lo = (uint32_t)r0;
+    /* v2 range reduction: multiply-high (Lemire) instead of modulo; v7: the
+     * class from a remix of lo ^ hi, not from emitted value bits */
+    const uint32_t xr = (uint32_t)r0 ^ (uint32_t)(r0 >> 32);
+    uint32_t cls = mulhi32(xr * 0x2545F491u, 100u), lo = (uint32_t)r0;
     vzero(out);
     if (cls >= pct[0] && cls < pct[1]) {
         out->w[0] = r0;                       /* v3: the class word itself */

@@ -21,13 +21,25 @@ def _sm64(s):
     return s, z ^ (z >> 31)
 
 
+CLS_MUL = 0x2545F491
+
+
+def gen_class(r0: int) -> int:
+    """v7: the class comes from a multiplicative remix of x = lo ^ hi of r0,
+    not from bits that are emitted as value bits (v3-v6 used r0 >> 32, which
+    confined bits 32-63 of the uniform / small values to their class's
+    percentage band: bit 63 was never set by a random class)."""
+    x = (r0 ^ (r0 >> 32)) & 0xFFFFFFFF
+    return _mulhi((x * CLS_MUL) & 0xFFFFFFFF, 100)
+
+
 def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
              pct=(50, 70, 85)) -> int:
     s = (seed ^ ((prog_seed * 0xD1B54A32D192ED03) & M64) ^
          (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64) ^ idx) & M64    # v5: idx itself
     s, r0 = _sm64(s)
     # v2 range reduction: multiply-high (Lemire), no modulo
-    cls = _mulhi(r0 >> 32, 100)
+    cls = gen_class(r0)
     lo = r0 & 0xFFFFFFFF
     mask = (1 << width) - 1
     if pct[0] <= cls < pct[1]:

@@ -13,7 +13,7 @@ HDR = os.path.join(build.ROOT, "include", "mythgpu.h")
 
 def declared():
     text = open(HDR).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(mg_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|float|const char\*)\s+(mg_\w+)\s*\(", text, re.M)))
 
 
 def test_library_built_from_current_generator():

@@ -1,0 +1,120 @@
+"""Parity over the WHOLE bench configuration, not a sample.
+
+``bench.py`` times ``mg_batch_eval_gen`` over every DAG of a workload (C2:
+4096 corpus DAGs; C3 / C4: 256 distinct stand-in queries).  Here the same
+entry point runs over every one of them at a 2^12-lane slice from a nonzero
+first index, and every root bit and every per-DAG first satisfying index is
+compared with ``oracle/evalref.c`` (``run_gen``: the same generator, the same
+pools; pinned to ``oracle/smtlib_ref.py`` by tests/test_evalref.py).
+
+The interpreter selects among up to 64 handler variants per opcode from
+static properties, so the test also asserts that every
+(family, variant) the bench configurations execute — reported by the
+translator itself (``engine.handler_variants``) — belongs to a program this
+test checked lane by lane.
+"""
+
+import ctypes as C
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+
+import bench
+from mythril_amd import shard
+from mythril_amd.engine import default_leafgen, handler_variants, unpack_bits
+
+pytestmark = pytest.mark.gpu
+THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or 8
+N_LANES, FIRST = 1 << 12, (3 << 20) + 192
+SEED = bench.SEED
+FULL = {"c2": 4096, "c3": bench.STREAM_QUERIES, "c4": bench.STREAM_QUERIES}
+# (family, variant) handlers of the programs verified lane by lane below
+CHECKED = set()
+
+
+def _oracle_unit(item):
+    """Worker (spawned: no GPU state): compile one bench unit and evaluate it
+    with the C oracle on the test's lane slice."""
+    from oracle import evalref
+    workload, d = item
+    d, prog, _, _ = bench.compile_unit((workload, d))
+    roots = bench.workload_roots(workload, d)
+    want = evalref.run_gen(evalref.serialize(roots, prog), prog, SEED, d, FIRST, N_LANES, 1)
+    return d, prog, np.packbits(want, bitorder="little")
+
+
+@pytest.fixture(scope="module")
+def units():
+    """Every bench unit of C2, C3 and C4 with its oracle root bits (spawned
+    workers: this process may already hold the GPU)."""
+    out = {}
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(min(16, os.cpu_count() or 1)) as pool:
+        for w, n in FULL.items():
+            out[w] = sorted(pool.map(_oracle_unit, [(w, d) for d in range(n)], chunksize=8),
+                            key=lambda t: t[0])
+    return out
+
+
+def _run_batch(engine, progs):
+    hip = C.CDLL("libamdhip64.so.7")
+    loaded = [engine.load(p, default_leafgen(p), prog_seed=d) for d, p in progs]
+    batch = engine.batch_create(loaded)
+    bits = np.zeros((len(progs), N_LANES // 64), dtype=np.uint64)
+    firsts = np.full(len(progs), shard.NONE, dtype=np.int64)
+    d_bits, d_first = C.c_void_p(), C.c_void_p()
+    assert hip.hipMalloc(C.byref(d_bits), C.c_size_t(bits.nbytes)) == 0
+    assert hip.hipMalloc(C.byref(d_first), C.c_size_t(firsts.nbytes)) == 0
+    try:
+        assert hip.hipMemcpy(d_first, firsts.ctypes.data_as(C.c_void_p),
+                             C.c_size_t(firsts.nbytes), 1) == 0
+        engine.batch_eval_gen(batch, SEED, FIRST, N_LANES, d_bits.value, d_first.value)
+        assert hip.hipDeviceSynchronize() == 0
+        assert hip.hipMemcpy(bits.ctypes.data_as(C.c_void_p), d_bits,
+                             C.c_size_t(bits.nbytes), 2) == 0
+        assert hip.hipMemcpy(firsts.ctypes.data_as(C.c_void_p), d_first,
+                             C.c_size_t(firsts.nbytes), 2) == 0
+    finally:
+        engine.batch_free(batch)
+        hip.hipFree(d_bits)
+        hip.hipFree(d_first)
+    return bits, firsts.tolist()
+
+
+@pytest.mark.parametrize("workload", ["c2", "c3", "c4"])
+def test_every_bench_unit_every_lane(engine, units, workload):
+    us = units[workload]
+    assert len(us) == FULL[workload]
+    bits, firsts = _run_batch(engine, [(d, p) for d, p, _ in us])
+    n_sat = n_hit = 0
+    for k, (d, p, packed) in enumerate(us):
+        want = np.unpackbits(packed, bitorder="little")[:N_LANES].astype(bool)
+        got = unpack_bits(bits[k], N_LANES)
+        assert np.array_equal(got, want), (workload, d, int(np.argmax(got != want)))
+        hit = np.flatnonzero(want)
+        assert firsts[k] == (FIRST + int(hit[0]) if hit.size else shard.NONE), (workload, d)
+        n_sat += int(hit.size)
+        n_hit += bool(hit.size)
+    for d, p, _ in us:
+        CHECKED.update(handler_variants(p))
+    print("%s: %d units, %d with satisfying lanes, %d satisfying lanes"
+          % (workload, len(us), n_hit, n_sat))
+
+
+def test_bench_handler_variants_all_checked(units):
+    """Every (family, variant) executed by a bench configuration (what
+    bench.py compiles for C2, C3 and C4) belongs to a program the test above
+    verified lane by lane; the count is reported so a new variant shows up
+    in the log."""
+    assert CHECKED, "run with test_every_bench_unit_every_lane (same module)"
+    bench_set = set()
+    for w in FULL:                      # the programs bench.compile_unit builds
+        for d, p, _ in units[w]:
+            bench_set |= handler_variants(p)
+    missing = sorted(bench_set - CHECKED)
+    assert not missing, missing
+    fams = sorted({f for f, _ in bench_set})
+    print("bench configurations execute %d (family, variant) handlers in %d families"
+          % (len(bench_set), len(fams)))

@@ -266,7 +266,10 @@ def test_unexpected_prefilter_error_falls_back(monkeypatch, fresh, reset_engine_
     assert M.stats.errors == before + 1
 
 
-def test_one_deadline_bounds_search_and_fallback(monkeypatch, fresh, reset_engine_memo):
+def test_gpu_miss_does_not_shorten_the_z3_timeout(monkeypatch, fresh, reset_engine_memo):
+    """The fallback gets the reference's own timeout (support/model.py:26-31),
+    whatever the GPU search took: a query z3 solves close to
+    its timeout must not become unknown -> UnsatError because of a miss."""
     import time
     seen = {}
 
@@ -284,7 +287,7 @@ def test_one_deadline_bounds_search_and_fallback(monkeypatch, fresh, reset_engin
     with pytest.raises(M.UnsatError):
         M.get_model((c_sat(),))
     assert seen["budget"] <= 200
-    assert seen["z3_timeout"] <= 400 - 150 + 5
+    assert seen["z3_timeout"] == 400
 
 
 def test_batch_witness_is_handed_to_get_model(batch_env, monkeypatch, reset_engine_memo):
@@ -389,3 +392,146 @@ def test_batch_search_spreads_programs_over_devices(monkeypatch):
     assert sorted(len(e.seen) for e in engines.values()) != [0, 0, 7]
     for p, (idx, _) in zip(progs, hits):
         assert idx == owner[id(p)] * 1000 + p.n_ins       # each program answered by its device
+
+
+# ---- round 3: assignment axis, group-miss memo, verification with z3 -------
+
+class StreamEngine:
+    """A device whose candidate stream satisfies the program at fixed indices
+    (the same on every device: counter-based streams)."""
+
+    def __init__(self, dev, sat, log):
+        self.dev, self.sat, self.log = dev, sorted(sat), log
+
+    def load(self, prog, leafgen, prog_seed=0):
+        return prog
+
+    def search(self, lp, seed, n_cand, first_index=0):
+        import numpy as np
+        self.log.append((self.dev, first_index, n_cand))
+        for i in self.sat:
+            if first_index <= i < first_index + n_cand:
+                return i, np.zeros((len(lp.leaves), 8), np.uint32)
+        return -1, None
+
+    def witness(self, prog, seed, index):
+        import numpy as np
+        import ir_sim
+        _, probes = ir_sim.run(prog, [0] * len(prog.leaves))
+        pr = np.zeros((len(probes), 8), np.uint32)
+        for k, v in enumerate(probes):
+            pr[k] = [(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)]
+        return np.zeros((len(prog.leaves), 8), np.uint32), pr
+
+
+@pytest.mark.parametrize("sat", [[137], [70000, 5000, 9000], [1 << 21], [], [0], [(1 << 22) - 1]])
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_assignment_axis_equals_single_device_sweep(monkeypatch, sat, G):
+    """device g takes candidates [g*N/G, (g+1)*N/G); the host MIN
+    over devices is the first index one device sweeping [0, N) finds."""
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.smt import node as N
+    x = N.bv_var("x", 256)
+    prog = compile_constraints([N.bv_cmp("bvult", x, N.bv_num(9, 256))])
+    n = 1 << 22
+    log = []
+    one = StreamEngine(0, sat, log)
+    want = one.search(prog, 0, n)[0]
+    log.clear()
+    engines = {d: StreamEngine(d, sat, log) for d in range(G)}
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    idx, _ = M.search_assignment_axis(prog, n, list(range(G)))
+    assert idx == want
+    ranges = sorted((f, f + k) for _, f, k in log)
+    assert ranges[0][0] == 0 and ranges[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))       # a partition
+    assert sorted(d for d, _, _ in log) == list(range(G))
+
+
+def test_single_group_query_uses_every_device(monkeypatch, fresh, reset_engine_memo):
+    log = []
+    engines = {d: StreamEngine(d, [3 << 20], log) for d in range(4)}
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "DEVICES", [0, 1, 2, 3])
+    M.clear_search_memos()
+    x = symbol_factory.BitVecSym("ax", 256)
+    hit = REAL_GPU_SEARCH([ULT(x, symbol_factory.BitVecVal(7, 256)).raw], 200)
+    assert hit is not None
+    assert sorted(d for d, _, _ in log) == [0, 1, 2, 3]
+
+
+@pytest.fixture
+def miss_engine(monkeypatch):
+    log = []
+    eng = StreamEngine(0, [], log)                       # never satisfied
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: eng)
+    monkeypatch.setattr(M, "DEVICES", [0])
+    M.clear_search_memos()
+    yield log
+    M.clear_search_memos()
+
+
+def test_group_miss_memo_skips_repeated_and_extended_groups(miss_engine, fresh,
+                                                            reset_engine_memo):
+    log = miss_engine
+    x = symbol_factory.BitVecSym("mx", 256)
+    c1 = (x * x == symbol_factory.BitVecVal(3, 256)).raw
+    c2 = ULT(x, symbol_factory.BitVecVal(1000, 256)).raw
+    before = M.stats.memo_misses
+    assert REAL_GPU_SEARCH([c1], 200) is None
+    assert len(log) == 1                                 # searched once
+    assert REAL_GPU_SEARCH([c1], 200) is None            # same group: no search
+    assert REAL_GPU_SEARCH([c1, c2], 200) is None        # extends the missed group
+    assert len(log) == 1
+    assert M.stats.memo_misses == before + 2
+    y = symbol_factory.BitVecSym("my", 256)
+    REAL_GPU_SEARCH([ULT(y, symbol_factory.BitVecVal(5, 256)).raw], 200)
+    assert len(log) == 2                                 # an unrelated group is searched
+
+
+def test_group_miss_at_fewer_candidates_is_searched_again(miss_engine, fresh, reset_engine_memo):
+    log = miss_engine
+    x = symbol_factory.BitVecSym("fx", 256)
+    c1 = (x * x == symbol_factory.BitVecVal(3, 256)).raw
+    prog = M._compile_search([c1])
+    M._note_miss(prog.group_key, 1 << 16)                # e.g. a crowded batch
+    assert REAL_GPU_SEARCH([c1], 200) is None
+    assert len(log) == 1 and log[0][2] > (1 << 16)       # searched, with more candidates
+
+
+def test_compile_gate_skips_queries_over_budget(miss_engine, fresh, reset_engine_memo):
+    log = miss_engine
+    x = symbol_factory.BitVecSym("gx", 256)
+    c = (x * x == symbol_factory.BitVecVal(3, 256)).raw
+    before = M.stats.gated
+    assert REAL_GPU_SEARCH([c], 0.0001) is None
+    assert M.stats.gated == before + 1 and log == []
+
+
+def test_batch_miss_not_handed_over_when_under_searched(batch_env, monkeypatch,
+                                                        reset_engine_memo):
+    """a set the batch searched with fewer candidates than
+    get_model would use is not sent to z3 unsearched."""
+    eng, z3_calls = batch_env
+    unsat_like = (symbol_factory.Bool(False).__class__(symbol_factory.Bool(False).raw),)
+    monkeypatch.setattr(M, "_n_cand", lambda progs, budget: 1 << 16 if len(progs) > 1 else 1 << 20)
+    M.batch_is_possible([unsat_like, (c_sat(),)])
+    assert M._take(M._gpu_missed, unsat_like) is None
+
+
+def test_node_witness_verified_by_z3_when_present(monkeypatch, fresh):
+    """north_star: every GPU witness is re-verified by z3 before a model is
+    returned — mirror DAG nodes too (through z3bridge.to_z3)."""
+    seen = {}
+    monkeypatch.setattr(M.z3bridge, "available", lambda: True)
+    monkeypatch.setattr(M.z3bridge, "to_z3", lambda n, memo: ("z3", n.id))
+
+    def verify(raws, assignment, timeout_ms):
+        seen["raws"], seen["timeout"] = raws, timeout_ms
+        return None                                     # z3 rejects it
+    monkeypatch.setattr(M.z3bridge, "verify", verify)
+    c = c_sat()
+    before = M.stats.rejected
+    assert M._accept([c], Assignment(vars={"x": 1}), None, 1234) is None
+    assert seen["raws"] == [("z3", c.raw.id)] and seen["timeout"] == 1234
+    assert M.stats.rejected == before + 1

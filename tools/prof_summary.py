@@ -37,6 +37,18 @@ def pmc(pat, counter):
     return max(tot.values()) if tot else None
 
 
+def bench_line(log):
+    """The JSON line bench.py printed in a profiled run (its kernel_key says
+    which kernel the counters belong to)."""
+    try:
+        for line in open(os.path.join(SRC, log)):
+            if line.startswith("{"):
+                return json.loads(line)
+    except OSError:
+        pass
+    return None
+
+
 fetch_kb = pmc("fetch/**/*counter_collection.csv", "FETCH_SIZE")
 write_kb = pmc("write/**/*counter_collection.csv", "WRITE_SIZE")
 if fetch_kb is not None and write_kb is not None:
@@ -45,7 +57,10 @@ if fetch_kb is not None and write_kb is not None:
     # report both the raw sum and the read-doubled upper bound.
     raw = (fetch_kb + write_kb) * 1024
     doubled = (2 * fetch_kb + write_kb) * 1024
-    out = {"dags": 4096, "assign_log2": 20, "fetch_kib": fetch_kb, "write_kib": write_kb,
+    keys = [(bench_line(l) or {}).get("kernel_key") for l in ("fetch.log", "write.log")]
+    if keys[0] != keys[1] or keys[0] is None:
+        sys.exit("FETCH and WRITE passes ran different kernels: %s" % keys)
+    out = {"kernel_key": keys[0], "fetch_kib": fetch_kb, "write_kib": write_kb,
            "hbm_bytes_per_launch": doubled, "hbm_bytes_raw": raw,
            "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, per mg_interp "
                    "dispatch of the default bench config; read side doubled per the gfx950 "

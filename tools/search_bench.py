@@ -106,11 +106,11 @@ def shape_lines(eng, n_queries):
         def run(clear_each):
             lat, misses = [], 0
             M.stats.reset_gpu()
-            M._SEARCH_CACHE = None
+            M.clear_search_memos()
             for q in sample:
                 M.get_model.cache_clear()
                 if clear_each:
-                    M._SEARCH_CACHE = None
+                    M.clear_search_memos()      # compiled groups and group misses
                 t1 = time.perf_counter()
                 try:
                     M.get_model(tuple(q), enforce_execution_time=False)
@@ -119,6 +119,8 @@ def shape_lines(eng, n_queries):
                 lat.append((time.perf_counter() - t1) * 1000.0)
             return {"queries": len(sample), "median_ms": statistics.median(lat),
                     "max_ms": max(lat), "gpu_misses": misses,
+                    "memo_misses": M.stats.memo_misses, "kernel_ms_per_query":
+                        M.stats.kernel_time * 1000.0 / len(sample),
                     "phase_ms_per_query": {k: v * 1000.0 / len(sample)
                                            for k, v in M.stats.phase.items()}}
         cold = run(True)
