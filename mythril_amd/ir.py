@@ -362,7 +362,7 @@ class _Lowerer:
         if op == "ite":
             if n.is_array():
                 raise Unsupported("array-valued ite outside select")
-            return [self.mk(I.ITE, w, (A(0), A(1), A(2)))]
+            return [self.mk(I.ITE, w, (A(0), A(1), A(2)))]     # node width (>= both arms)
         if op == "concat":
             return self.assemble([(self.memo[a.id], a.width) for a in n.args])
         if op == "extract":
@@ -445,7 +445,7 @@ class _Lowerer:
         if op == "ite":
             c = self._narrow(n.args[0])
             a, b = self.memo[n.args[1].id], self.memo[n.args[2].id]
-            return [self.mk(I.ITE, x.width, (c, x, y)) for x, y in zip(a, b)]
+            return self._ite_chunks(c, a, b)
         if op == "select":
             return self._select(n.args[0], self.memo[n.args[1].id], n.args[1].width, w)
         if op == "apply":
@@ -459,7 +459,13 @@ class _Lowerer:
         return self._fold(I.AND, 1, parts)
 
     def _ite_chunks(self, c: LNode, a: List[LNode], b: List[LNode]) -> List[LNode]:
-        return [self.mk(I.ITE, x.width, (c, x, y)) for x, y in zip(a, b)]
+        """Chunk-wise ite.  A chunk's width is the WIDER of its two arms: a
+        lowered ``zero_extend`` is its narrow operand itself (values are
+        canonical), so one arm may be narrower than the other — taking the
+        first arm's width dropped the other arm's high bits (found by the
+        full bench-config parity test on C2 DAG 571: a store chain whose
+        stored value is a zero-extended 16-bit extract)."""
+        return [self.mk(I.ITE, max(x.width, y.width), (c, x, y)) for x, y in zip(a, b)]
 
     def _table(self, name: str, key: List[LNode], kw: int, vw: int, kind: str) -> List[LNode]:
         """Lookup of a free array / UF in the model's table: first match over

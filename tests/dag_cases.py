@@ -90,9 +90,14 @@ def array_case(entries=3):
     st = N.store(N.store(A, i, v), j, N.bv_op("bvadd", v, N.bv_num(1, 256)))
     kst = N.store(N.const_array(256, N.bv_num(0, 256)), i, v)
     c = N.bv_cmp("bvult", i, j)
+    # a zero-extended narrow value stored over a wide one: the lowered store
+    # link is an ite whose arms differ in width (C2 DAG 571, round 3)
+    nv = N.zero_extend(240, N.extract(79, 64, v))
+    st2 = N.store(N.store(A, i, v), j, nv)
     probes = [N.select(A, k), N.select(st, k), N.select(st, i), N.select(st, j),
               N.select(kst, k), N.select(kst, i), N.select(cd, k),
-              N.select(N.ite(c, st, kst), k)]
+              N.select(N.ite(c, st, kst), k), N.select(st2, i), N.select(st2, k),
+              N.ite(c, nv, v)]
     # calldata word as LASER builds it (calldata.py:219-232): concat of 4 bytes
     size = N.bv_var("cdsize", 256)
     parts = []

@@ -101,6 +101,10 @@ def run(program, leaf_vals):
             raise AssertionError("op %d" % op)
         if w0 & I.ROOT_FLAG:
             root &= r & 1
+        if op in (I.ITE, I.AND, I.OR, I.XOR, I.MOV, I.CONST):
+            # the IR contract: a value is canonical at its instruction's width
+            # (the kernel picks one-limb / masked handlers from it)
+            assert r >> w == 0, "op %d writes a %d-bit value at width %d" % (op, r.bit_length(), w)
         if op not in (I.SPILL, I.OUT, I.ROOT, I.NOP):   # these write no slot (mg_host.cpp)
             regs[d] = r
     return root, [probes.get(i, 0) for i in range(program.n_probes)]
