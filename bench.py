@@ -203,6 +203,8 @@ def main():
     ap.add_argument("--shard", choices=("assign", "corpus"), default="assign",
                     help="assignment axis (default, C2) or corpus axis (C5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--jit", action="store_true",
+                    help="compiled programs (mythril_amd/jit.py) instead of record dispatch")
     args = ap.parse_args()
     if args.dags is None:
         args.dags = 4096 if args.workload == "c2" else STREAM_QUERIES
@@ -218,6 +220,12 @@ def main():
     corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world, args.workload),
                           args.workload)
     t_compile = time.time() - t0
+    image, t_jit = None, 0.0
+    if args.jit:                      # code generation + assembly, still before the GPU
+        from mythril_amd import jit
+        t0 = time.time()
+        image = jit.compile_batch([(p, None, d) for d, p, _, _ in corpus], workers=workers)
+        t_jit = time.time() - t0
 
     import torch
     import torch.distributed as dist
@@ -230,6 +238,8 @@ def main():
     from mythril_amd.engine import Engine, default_leafgen
     eng = Engine(local)
     loaded = [eng.load(p, default_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
+    if image is not None:
+        jit_handle = eng.jit_attach(loaded, image)     # noqa: F841 (kept attached)
     batch = eng.batch_create(loaded)
     n_assign = 1 << args.assign_log2
     words = (n_assign + 63) // 64
@@ -274,7 +284,7 @@ def main():
         ops_launch = weight_per_lane * n_assign
         achieved = ops_launch / (kern_ms / 1000.0)
         key = kernel_key(eng.lib.mg_asm_digest().decode(), args.workload, args.dags,
-                         args.assign_log2, False)
+                         args.assign_log2, args.jit)
         traffic, traffic_note = None, "no profiles/traffic.json"
         if os.path.exists(args.traffic_json):
             try:
@@ -324,6 +334,7 @@ def main():
             "kernel_key": key,
             "sat_dags": sat_dags,
             "compile_s": round(t_compile, 2),
+            "jit_s": round(t_jit, 2) if args.jit else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(corpus, workload=args.workload)

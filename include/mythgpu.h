@@ -38,6 +38,7 @@ extern "C" {
 typedef struct mg_ctx mg_ctx;
 typedef struct mg_prog mg_prog;
 typedef struct mg_batch mg_batch;
+typedef struct mg_jit mg_jit;
 
 /* Device candidate generator for one leaf (free variable / table cell),
  * generator v7 (restated bit-exactly by oracle/gen_ref.py):
@@ -132,6 +133,20 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* batch, uint64_t seed, uint64_t firs
  * max_leaves must be >= the batch's largest leaf count. */
 int mg_batch_search(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_cand,
                     int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves);
+
+/* Compiled programs (batch path without interpretive dispatch; built on the
+ * host by mythril_amd/jit.py): ``image`` is a gfx950 code object holding the
+ * straight-line code of programs[0..n_progs) and their entry table
+ * ``mg_jit_table``.  Attaching points each program's descriptor at its
+ * code; evaluations of those programs — and batches created afterwards —
+ * then run the code instead of dispatching records (same results, same
+ * kernel).  Same role as mg_load_program for Optimize.add (solver.py:28-37),
+ * specialised for the batched evaluation (laser/smt/model.py:44-59). */
+int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const void* image,
+                  size_t image_size, mg_jit** out);
+/* Back to the interpreter for those programs; unloads the code object.
+ * Free batches created while attached first. */
+void mg_jit_detach(mg_jit* jit);
 
 /* Keccak-256 (0x01 padding) of n messages, one GPU lane per message.
  *   data/offsets/lens describe the messages in one host byte buffer;

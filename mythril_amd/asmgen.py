@@ -191,6 +191,23 @@ TMP = T[11]
 OP_ROOT, OP_IDX_LO, OP_IDX_HI, OP_LDS = "%[root]", "%[idx_lo]", "%[idx_hi]", "%[lds]"
 IN = {k: "%%[%s]" % k for k in ("desc", "seed", "first", "leaves", "stride", "lout", "probes",
                                 "mode", "scr", "active", "table")}
+# Every operand lives in a FIXED register (physical-register constraints in
+# mg_interp_asm.hip, generated from this table): compiled programs (jit.py),
+# assembled apart from the kernel, address them by these names too.
+PINNED = {"root": "v164", "idx_lo": "v165", "idx_hi": "v166", "lds": "v167",
+          "desc": "s[16:17]", "seed": "s[18:19]", "first": "s[20:21]", "leaves": "s[22:23]",
+          "stride": "s[24:25]", "lout": "s[26:27]", "probes": "s[28:29]", "mode": "s30",
+          "scr": "s31", "active": "s[32:33]", "table": "s[34:35]"}
+NVGPR_KERNEL = 168         # the kernel's VGPR budget (3 waves / SIMD)
+# mg_pdesc byte offsets the assembly reads (mg_device.h)
+PDESC_CONSTS, PDESC_XCODE, PDESC_BTAB, PDESC_JIT = 0x8, 0x30, 0x38, 0x40
+
+# Compiled-program (JIT) generation mode, set by mythril_amd/jit.py while it
+# renders handler templates: no record prefetch, no dispatch (a marker line
+# ends the handler's straight-line part), heavy stubs become call markers.
+JIT = False
+JIT_RET = 58               # s[58:59]: return address into the interpreter
+JIT_BODY_RET = 56          # s[56:57]: return address of a shared heavy body
 
 
 class Asm:
@@ -310,6 +327,8 @@ def cur(k: int) -> int:
 # ---------------------------------------------------------------------------
 
 def prologue(a: Asm, bank: int):
+    if JIT:
+        return
     ob = BANK[1 - bank]
     a("s_load_dwordx8 s[%d:%d], %s, %s" % (ob, ob + 7, sp(S_CODE), s(S_IP)))
     a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
@@ -319,6 +338,15 @@ _PROBE = os.environ.get("MYTHGPU_PROBE", "")     # sensitivity probes (A/B build
 
 
 def dispatch(a: Asm, next_bank: int):
+    if JIT:
+        # end of the handler's straight-line part: the dispatch's wait stays
+        # (handlers leave LDS reloads to it; jit.peephole drops the
+        # redundant ones) and the mode is left off
+        if not (a.lines and a.lines[-1].strip() == "s_set_gpr_idx_off"):
+            a("s_set_gpr_idx_off")
+        a("s_waitcnt lgkmcnt(0)")
+        a.lines.append("@@END")
+        return
     nb = BANK[next_bank]
     if a.lines and a.lines[-1].strip() == "s_set_gpr_idx_off":
         a.lines.pop()                  # the next handler turns it off if it must
@@ -432,6 +460,9 @@ def h_nop(a, bank, root, mask, dc=False, w32=False, ip=False):
 
 def h_halt(a, bank, root, mask, dc=False, w32=False, ip=False):
     a("s_waitcnt lgkmcnt(0)")
+    if JIT:
+        a.lines.append("@@HALT")
+        return
     far_jump(a, ".Lexit_%=")           # the handlers outgrow s_branch's range
 
 
@@ -1306,6 +1337,9 @@ def far_jump(a: Asm, label: str):
 
 
 def heavy_stub(a: Asm, bank: int, varbits: int, body: str):
+    if JIT:
+        a.lines.append("@@CALL %s %d" % (body, varbits))
+        return
     b = BANK[bank]
     for k in range(0, 8, 2):
         a("s_mov_b64 %s, %s" % (sp(S_CUR + k), sp(b + k)))
@@ -1314,8 +1348,9 @@ def heavy_stub(a: Asm, bank: int, varbits: int, body: str):
 
 
 def heavy_prologue(a: Asm):
-    a("s_load_dwordx8 s[%d:%d], %s, %s" % (BANK[0], BANK[0] + 7, sp(S_CODE), s(S_IP)))
-    a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
+    if not JIT:
+        a("s_load_dwordx8 s[%d:%d], %s, %s" % (BANK[0], BANK[0] + 7, sp(S_CODE), s(S_IP)))
+        a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
     load_masks(a, cur(F_MOFF))     # MOFF always names a valid 8-word entry
 
 
@@ -1982,13 +2017,40 @@ HEAVY = {"UMULNO": "UMULNO",
 HEAVY_AOPS = sorted(AOP[n] for n in HEAVY)
 
 
+def emit_handler(a: Asm, name: str, var: int, bank: int) -> None:
+    """The handler of family ``name``, variant ``var``, record bank ``bank``
+    (its body only; the caller places the label)."""
+    root_v, mask_v = bool(var & V_ROOT), bool(var & V_MASK)
+    dc_v, w32_v, ip_v = bool(var & V_DC), bool(var & V_W32), bool(var & V_IP)
+    a.nw = bool(var & V_NW)
+    if name == "LEAFD":
+        h_leafd(a, bank, var)
+    elif name == "RELOADD":
+        h_reloadd(a, bank, var)
+    elif name in SLOT_VARIANT:
+        SLOT_HANDLERS[name](a, bank, var)
+    elif name == "EQSEL":
+        h_eqsel(a, bank, var)
+    elif name == "EXTRACTN":
+        h_extractn(a, bank, var)
+    elif name == "CONCATQ":
+        h_concatq(a, bank, var)
+    elif name in CHEAP:
+        CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
+    else:
+        bits = var | (DIV_CODE.get(name, 0) << 4)
+        heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
+    a.nw = False
+
+
 def generate() -> List[str]:
     a = Asm()
     a("s_mov_b32 %s, m0" % s(S_M0))
     load_sm64_consts(a)
-    # mg_pdesc: code@0 consts@8 gen@16 ... xcode@48
-    a("s_load_dwordx2 %s, %s, 0x8" % (sp(S_CONST), IN["desc"]))
-    a("s_load_dwordx2 %s, %s, 0x30" % (sp(S_CODE), IN["desc"]))
+    # mg_pdesc: code@0 consts@8 gen@16 ... xcode@48 btab@56 jit@64
+    a("s_load_dwordx2 %s, %s, 0x%x" % (sp(S_CONST), IN["desc"], PDESC_CONSTS))
+    a("s_load_dwordx2 %s, %s, 0x%x" % (sp(S_CODE), IN["desc"], PDESC_XCODE))
+    a("s_load_dwordx2 %s, %s, 0x%x" % (sp(S_JMP), IN["desc"], PDESC_JIT))
     a("v_mov_b32 %s, 1" % OP_ROOT)
     a("s_getpc_b64 %s" % sp(S_BASE))
     a.label(".Lbase_%=")
@@ -1996,10 +2058,23 @@ def generate() -> List[str]:
     a("s_cbranch_scc1 .Lquery_%=")
     a("s_mov_b32 %s, 32" % s(S_IP))
     a("s_waitcnt lgkmcnt(0)")
+    # a compiled program (mythril_amd/jit.py) runs instead of the records
+    a("s_cmp_lg_u64 %s, 0" % sp(S_JMP))
+    a("s_cbranch_scc1 .Ljit_%=")
     a("s_load_dwordx8 s[%d:%d], %s, 0x0" % (BANK[0], BANK[0] + 7, sp(S_CODE)))
     dispatch(a, 0)
+    # compiled program: call it (it returns through s[JIT_RET]), then the
+    # dispatch base is re-established for the far jump to the exit
+    a.label(".Ljit_%=")
+    a("s_swappc_b64 %s, %s" % (sp(JIT_RET), sp(S_JMP)))
+    a("s_getpc_b64 %s" % sp(S_BASE))
+    a.label(".Ljret_%=")
+    a("s_sub_u32 %s, %s, (.Ljret_%%= - .Lbase_%%=)" % (s(S_BASE), s(S_BASE)))
+    a("s_subb_u32 %s, %s, 0" % (s(S_BASE + 1), s(S_BASE + 1)))
+    far_jump(a, ".Lexit_%=")
     # query mode: table[h] = offset of handler h from .Lbase
     a.label(".Lquery_%=")
+    a("s_waitcnt lgkmcnt(0)")              # the descriptor loads (S_JMP is reused)
     a("v_mov_b32 %s, 0" % v(T[0]))
     a("s_mov_b64 %s, %s" % (sp(S_T), IN["table"]))
     for h in range(NUM_HANDLERS):
@@ -2015,29 +2090,9 @@ def generate() -> List[str]:
         for var in range(NVAR):
             if canon_var(name, var) != var:
                 continue
-            root_v, mask_v = bool(var & V_ROOT), bool(var & V_MASK)
-            dc_v, w32_v, ip_v = bool(var & V_DC), bool(var & V_W32), bool(var & V_IP)
-            a.nw = bool(var & V_NW)
             for bank in (0, 1):
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
-                if name == "LEAFD":
-                    h_leafd(a, bank, var)
-                elif name == "RELOADD":
-                    h_reloadd(a, bank, var)
-                elif name in SLOT_VARIANT:
-                    SLOT_HANDLERS[name](a, bank, var)
-                elif name == "EQSEL":
-                    h_eqsel(a, bank, var)
-                elif name == "EXTRACTN":
-                    h_extractn(a, bank, var)
-                elif name == "CONCATQ":
-                    h_concatq(a, bank, var)
-                elif name in CHEAP:
-                    CHEAP[name](a, bank, root_v, mask_v, dc_v, w32_v, ip_v)
-                else:
-                    bits = var | (DIV_CODE.get(name, 0) << 4)
-                    heavy_stub(a, bank, bits, ".Lbody_%s_%%=" % HEAVY[name])
-    a.nw = False
+                emit_handler(a, name, var, bank)
     body_umulno(a)
     body_div(a)
     a.label(".Lexit_%=")
@@ -2095,6 +2150,14 @@ def drop_redundant_idx_off(lines: List[str]) -> List[str]:
     return [l for i, l in enumerate(lines) if i not in drop]
 
 
+def operand_constraints() -> Dict[str, str]:
+    """Inline-asm constraint of every operand: its pinned register."""
+    out = {}
+    for k, r in PINNED.items():
+        out[k] = ("={%s}" if k == "root" else "{%s}") % r
+    return out
+
+
 def clobbers() -> List[str]:
     vs = ['"v%d"' % i for i in range(NVGPR_FIXED)]
     ss = ['"s%d"' % i for i in range(BANK[0], S_LAST + 1)]
@@ -2103,20 +2166,26 @@ def clobbers() -> List[str]:
 
 
 def digest(lines: Optional[List[str]] = None) -> str:
-    """Short hash of the generated assembly (embedded in the library, so a
-    stale build is detected: engine.load_library, tests/test_abi.py)."""
+    """Short hash of the generated assembly and its operand registers
+    (embedded in the library, so a stale build is detected:
+    engine.load_library, tests/test_abi.py)."""
     import hashlib
-    return hashlib.sha256("\n".join(lines or generate()).encode()).hexdigest()[:16]
+    text = list(lines or generate()) + ["%s=%s" % kv for kv in sorted(PINNED.items())]
+    return hashlib.sha256("\n".join(text).encode()).hexdigest()[:16]
 
 
 def write_outputs(csrc: str) -> None:
     lines = generate()
     body = " \\\n".join('"%s\\n"' % l.replace('"', '\\"') for l in lines)
+    oc = operand_constraints()
+    cons = "".join('#define MG_ASM_C_%s "%s"\n' % (k.upper(), c) for k, c in oc.items())
     inc = ("// GENERATED by mythril_amd/asmgen.py -- do not edit.\n"
            "// Inline-asm body of mg_interp_asm (gfx950), %d lines.\n"
            "#define MG_ASM_BODY \\\n%s\n\n"
            "#define MG_ASM_CLOBBERS %s\n"
-           "#define MG_ASM_DIGEST \"%s\"\n") % (len(lines), body, ", ".join(clobbers()), digest(lines))
+           "// operand registers (asmgen.PINNED; compiled programs use them too)\n%s"
+           "#define MG_ASM_DIGEST \"%s\"\n") % (len(lines), body, ", ".join(clobbers()), cons,
+                                                 digest(lines))
     _write_if_changed(os.path.join(csrc, "mg_interp_gfx950.inc"), inc)
     hdr = ["// GENERATED by mythril_amd/asmgen.py -- do not edit.",
            "#ifndef MG_ASM_HANDLERS_H", "#define MG_ASM_HANDLERS_H",

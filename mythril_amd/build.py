@@ -9,6 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "mythril_amd", "csrc")
 LIBDIR = os.path.join(ROOT, "mythril_amd", "lib")
 LIB = os.path.join(LIBDIR, "libmythgpu.so")
+JIT_STUB = os.path.join(LIBDIR, "mg_jit_stub.s")
 SOURCES = ["mg_interp_asm.hip", "mg_keccak.hip", "mg_host.cpp", "mg_api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
@@ -17,6 +18,7 @@ ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
 def _deps():
     files = [os.path.join(CSRC, s) for s in SOURCES]
     files += [os.path.join(CSRC, "mg_device.h"), os.path.join(CSRC, "mg_host.h"),
+              os.path.join(CSRC, "mg_jit_stub.hip"),
               os.path.join(ROOT, "include", "mythgpu.h"),
               os.path.join(ROOT, "include", "mythgpu_ir.h"),
               os.path.join(ROOT, "mythril_amd", "asmgen.py")]
@@ -24,7 +26,7 @@ def _deps():
 
 
 def up_to_date() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(JIT_STUB):
         return False
     t = os.path.getmtime(LIB)
     return all(os.path.getmtime(f) <= t for f in _deps())
@@ -61,7 +63,20 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     os.replace(tmp, out)
     for o in objs:
         os.remove(o)
+    if out == LIB:
+        build_jit_stub()
     return out
+
+
+def build_jit_stub() -> str:
+    """Device assembly of the stub kernel every compiled-program code object
+    (mythril_amd/jit.py) is built around."""
+    tmp = JIT_STUB + ".tmp"
+    subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-O3", "--cuda-device-only", "-S",
+                    os.path.join(CSRC, "mg_jit_stub.hip"), "-o", tmp], check=True,
+                   stderr=subprocess.DEVNULL)
+    os.replace(tmp, JIT_STUB)
+    return JIT_STUB
 
 
 if __name__ == "__main__":

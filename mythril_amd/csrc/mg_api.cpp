@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <vector>
 
+#include <cstddef>
 #include <cstdlib>
 #include <map>
 
@@ -80,6 +81,14 @@ static hipError_t launch(const mg_ctx* ctx, int gen, const mg_pdesc* d_descs, ui
     return mg_launch_asm(d_descs, n_progs, run, gen ? 1u : 0u, kernel_lds_slots(ctx, n_lds),
                          nullptr, stream);
 }
+
+// A loaded compiled-program code object (mythril_amd/jit.py) and the
+// programs whose descriptors point into it.
+struct mg_jit {
+    mg_ctx* ctx = nullptr;
+    hipModule_t module = nullptr;
+    std::vector<mg_prog*> progs;
+};
 
 struct mg_batch {
     mg_ctx* ctx = nullptr;
@@ -619,6 +628,73 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
     timing_read(ctx);
     for (uint32_t i = 0; i < b->n; ++i) first_sat[i] = h[i] == ~0ull ? -1 : (int64_t)h[i];
     return MG_OK;
+}
+
+// Compiled programs: load the code object, read its entry table
+// (mg_jit_table: each program's entry relative to the table) and point the
+// programs' descriptors at their code.  Batches created afterwards copy the
+// entries; the interpreter kernel then calls the code instead of
+// dispatching records.  Every entry must lie inside the image's text, ahead
+// of the table (checked) so a malformed image cannot send the kernel to an
+// arbitrary address.
+int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const void* image,
+                  size_t image_size, mg_jit** out) {
+    if (!ctx || !out || !image || !image_size || (n_progs && !progs))
+        return fail(ctx, MG_E_ARG, "null argument");
+    *out = nullptr;
+    for (uint32_t i = 0; i < n_progs; ++i)
+        if (!progs[i] || progs[i]->ctx != ctx) return fail(ctx, MG_E_ARG, "program %u", i);
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
+    hipModule_t mod = nullptr;
+    HIPCHECK(ctx, hipModuleLoadData(&mod, image));
+    hipDeviceptr_t d_table = nullptr;
+    size_t table_b = 0;
+    hipError_t e = hipModuleGetGlobal(&d_table, &table_b, mod, "mg_jit_table");
+    std::vector<int64_t> rel(n_progs);
+    if (e == hipSuccess && table_b != (size_t)n_progs * 8) e = hipErrorInvalidValue;
+    if (e == hipSuccess && n_progs)
+        e = hipMemcpy(rel.data(), d_table, table_b, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+        (void)hipModuleUnload(mod);
+        return fail(ctx, MG_E_HIP, "JIT image: %s (table %zu bytes for %u programs)",
+                    hipGetErrorString(e), table_b, n_progs);
+    }
+    for (uint32_t i = 0; i < n_progs; ++i)
+        if (rel[i] >= 0 || -rel[i] > (int64_t)image_size || (rel[i] & 3)) {
+            (void)hipModuleUnload(mod);
+            return fail(ctx, MG_E_ARG, "JIT image: entry %u at %lld outside the code", i,
+                        (long long)rel[i]);
+        }
+    mg_jit* j = new mg_jit();
+    j->ctx = ctx;
+    j->module = mod;
+    for (uint32_t i = 0; i < n_progs; ++i) {
+        const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)rel[i];
+        e = hipMemcpy((uint8_t*)progs[i]->d_desc + offsetof(mg_pdesc, jit_entry), &entry,
+                      sizeof entry, hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            mg_jit_detach(j);
+            return fail(ctx, MG_E_HIP, "JIT attach: %s", hipGetErrorString(e));
+        }
+        j->progs.push_back(progs[i]);
+    }
+    *out = j;
+    return MG_OK;
+}
+
+// Back to the interpreter for every attached program (their descriptors'
+// entries cleared), then the code object is unloaded.  Batches created while
+// attached keep stale entries: free them first.
+void mg_jit_detach(mg_jit* j) {
+    if (!j) return;
+    (void)hipSetDevice(j->ctx->device);
+    const uint64_t zero = 0;
+    for (mg_prog* p : j->progs)
+        (void)hipMemcpy((uint8_t*)p->d_desc + offsetof(mg_pdesc, jit_entry), &zero, sizeof zero,
+                        hipMemcpyHostToDevice);
+    (void)hipDeviceSynchronize();
+    if (j->module) (void)hipModuleUnload(j->module);
+    delete j;
 }
 
 int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets, const uint32_t* lens,

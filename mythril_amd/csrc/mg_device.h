@@ -31,7 +31,16 @@ struct mg_pdesc {
     const uint32_t* btab;      /* generator boundary table (context-wide):
                                   [kind 0..5][p 0..255] x 8 words, see
                                   mg_boundary_table in mg_api.cpp         */
+    uint64_t jit_entry;        /* compiled program (mythril_amd/jit.py,
+                                  mg_jit_attach): code address the kernel
+                                  calls instead of interpreting the records;
+                                  0 = interpret                            */
 };
+static_assert(__builtin_offsetof(mg_pdesc, consts) == 0x8 &&
+              __builtin_offsetof(mg_pdesc, xcode) == 0x30 &&
+              __builtin_offsetof(mg_pdesc, btab) == 0x38 &&
+              __builtin_offsetof(mg_pdesc, jit_entry) == 0x40,
+              "mg_pdesc layout is read by the assembly (asmgen.PDESC_*)");
 
 /* Per-launch arguments (passed by value). */
 struct mg_run {

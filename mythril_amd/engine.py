@@ -22,7 +22,7 @@ _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "lib
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
            "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_keccak256", "mg_version", "mg_config",
-           "mg_translate", "mg_asm_digest", "mg_last_kernel_ms")
+           "mg_translate", "mg_asm_digest", "mg_last_kernel_ms", "mg_jit_attach", "mg_jit_detach")
 
 
 class EngineUnavailable(RuntimeError):
@@ -84,6 +84,9 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_asm_digest.restype = C.c_char_p
         lib.mg_last_kernel_ms.argtypes = [p]
         lib.mg_last_kernel_ms.restype = C.c_float
+        lib.mg_jit_attach.argtypes = [p, C.POINTER(p), u32, p, C.c_size_t, C.POINTER(p)]
+        lib.mg_jit_detach.argtypes = [p]
+        lib.mg_jit_detach.restype = None
         pu32 = C.POINTER(u32)
         lib.mg_translate.argtypes = [p, u32, u32, u32, p, u32, p, u32, pu32, p, u32, pu32]
         for name in EXPORTS:
@@ -243,6 +246,21 @@ class Engine:
     def batch_free(self, h):
         self.lib.mg_batch_free(h)
 
+    def jit_attach(self, loaded: Sequence[LoadedProgram], image: bytes):
+        """Point the programs at their compiled code (``jit.compile_batch``
+        of the same programs, leaf generators and seeds, in order); returns
+        the handle for :meth:`jit_detach`.  Attach before ``batch_create``."""
+        arr = (C.c_void_p * len(loaded))(*[lp.handle for lp in loaded])
+        buf = C.create_string_buffer(image, len(image))
+        h = C.c_void_p()
+        rc = self.lib.mg_jit_attach(self._ctx, arr, len(loaded), C.cast(buf, C.c_void_p),
+                                    len(image), C.byref(h))
+        self._check(rc, "mg_jit_attach")
+        return h
+
+    def jit_detach(self, h):
+        self.lib.mg_jit_detach(h)
+
     def batch_eval_gen(self, h, seed: int, first_index: int, n_assign: int,
                        d_root_bits: int = 0, d_first_sat: int = 0, stream: int = 0):
         rc = self.lib.mg_batch_eval_gen(self._ctx, h, seed & (2**64 - 1), first_index, n_assign,
@@ -275,11 +293,13 @@ class Engine:
         return out
 
 
-def record_handlers(program: Program, lds_slots: int = 6) -> List[int]:
-    """Host-only (no GPU): the assembly-interpreter handler id of every
-    record ``mg_load_program`` would upload for ``program`` (the translator
-    run with an identity offset table), in execution order.  ``lds_slots``
-    is the context's LDS spill tier (``MYTHGPU_LDS_SLOTS``, default 6)."""
+def translate_records(program: Program, lds_slots: int = 6):
+    """Host-only (no GPU): the records ``mg_load_program`` would upload for
+    ``program`` with handler IDS in word 0 (the translator run with an
+    identity offset table; the last record is the zeroed prefetch pad), and
+    the number of mask entries the translator appended to the constant
+    table.  ``lds_slots`` is the context's LDS spill tier
+    (``MYTHGPU_LDS_SLOTS``, default 6)."""
     from . import asmgen
     lib = load_library()
     code = np.ascontiguousarray(program.code, dtype=np.uint32)
@@ -296,7 +316,13 @@ def record_handlers(program: Program, lds_slots: int = 6) -> List[int]:
                           _ptr(masks), max_mask, C.byref(nmw))
     if rc != 0:
         raise EngineError("mg_translate failed (%d)" % rc)
-    return [int(h) for h in rec[:nrw.value:8][:-1]]      # the last record is a zeroed pad
+    return rec[:nrw.value], nmw.value // 8
+
+
+def record_handlers(program: Program, lds_slots: int = 6) -> List[int]:
+    """The assembly-interpreter handler id of every record, in order."""
+    rec, _ = translate_records(program, lds_slots)
+    return [int(h) for h in rec[::8][:-1]]       # the last record is a zeroed pad
 
 
 def handler_variants(program: Program, lds_slots: int = 6):

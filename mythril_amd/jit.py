@@ -1,0 +1,774 @@
+"""Compiled programs: the batch path without interpretive dispatch
+(DESIGN.md §3.5).
+
+The assembly interpreter (asmgen.py) spends, per IR record, a record
+prefetch, a computed jump (``s_setpc``: an instruction-fetch redirect) and
+GPR-index mode switches around every register-file access.  For a batch that
+evaluates each program under 2^20 candidates that cost is paid 2^20 / 64
+times per record, so the batch path compiles each program instead:
+
+* every record is rendered by the SAME handler generator the interpreter is
+  built from (``asmgen.emit_handler`` with ``asmgen.JIT`` set: no prefetch,
+  no dispatch), then **specialised** to the record: GPR-index mode is
+  resolved statically (each indexed VGPR operand becomes the register the
+  index selected), record fields become immediates or are folded through the
+  scalar arithmetic that consumes them, branches on them are decided, and the
+  mode switches disappear;
+* the records of a program are laid out as one straight line (out-of-line
+  blocks collected and placed every few records behind a jump), ending in a
+  return to the interpreter kernel, which calls the program's code through
+  the ``jit_entry`` of its descriptor (``mg_pdesc``, one ``s_swappc``);
+* division and ``bvumul_noovfl`` stay shared bodies (hundreds of VALU each):
+  the call sets the record fields they read and ``s_swappc``s to them.
+
+The interpreter stays the path for single ``get_model`` queries (a few ms of
+host compile here would cost more than the dispatch it saves).  Programs are
+assembled with the ROCm LLVM assembler and linked into a code object next to
+a tiny stub kernel (``lib/mg_jit_stub.s``, built from csrc/mg_jit_stub.hip);
+``mg_jit_attach`` loads it and points the descriptors at the code.
+Correctness is checked on the CPU by running the generated text through the
+instruction-level simulator (tests/asm_sim.py), and on the GPU by the same
+parity tests as the interpreter (tests/test_gpu_bench_parity.py).
+"""
+
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import tempfile
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import asmgen as G
+
+LLVM_BIN = os.environ.get("MYTHGPU_LLVM_BIN", "/opt/rocm/lib/llvm/bin")
+ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
+LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+STUB = os.path.join(LIBDIR, "mg_jit_stub.s")
+M32 = 0xFFFFFFFF
+BANK0 = G.BANK[0]
+COLD_FLUSH = 32            # out-of-line blocks are placed every this many records
+BODY_LABEL = {"DIV": ".Lbody_DIV_jb", "UMULNO": ".Lbody_UMULNO_jb"}
+
+
+class JitUnsupported(Exception):
+    """A record the specialiser cannot resolve statically (the program then
+    stays on the interpreter)."""
+
+
+# ---------------------------------------------------------------------------
+# templates: handler text rendered in JIT mode
+# ---------------------------------------------------------------------------
+
+_TEMPLATES: Dict[Tuple[str, int], List[str]] = {}
+
+
+def _render(fn) -> List[str]:
+    G.JIT = True
+    try:
+        a = G.Asm()
+        fn(a)
+        a.flush_cold()
+        return list(a.lines)
+    finally:
+        G.JIT = False
+
+
+def template(name: str, var: int) -> List[str]:
+    key = (name, var)
+    t = _TEMPLATES.get(key)
+    if t is None:
+        t = _render(lambda a: G.emit_handler(a, name, var, 0))
+        _TEMPLATES[key] = t
+    return t
+
+
+def bodies() -> List[str]:
+    """The shared heavy bodies in JIT form: no record prefetch, and the
+    dispatch replaced by a return through s[JIT_BODY_RET] (with GPR-index
+    mode off: the straight-line code after the call is not indexed)."""
+    out = []
+    # one Asm for both: its label counter keeps their labels distinct
+    for line in _render(lambda a: (G.body_umulno(a), G.body_div(a))):
+        if line == "@@END":
+            out.append("    s_setpc_b64 %s" % G.sp(G.JIT_BODY_RET))
+        else:
+            out.append(line)
+    labels = [l for l in out if l.endswith(":")]
+    assert len(labels) == len(set(labels)), "duplicate labels in the JIT bodies"
+    return [_subst(l, "jb") for l in out]
+
+
+def _subst(line: str, tag: str) -> str:
+    line = line.replace("%=", tag)
+    if "%[" in line:
+        for k, r in G.PINNED.items():
+            line = line.replace("%%[%s]" % k, r)
+    return line
+
+
+# ---------------------------------------------------------------------------
+# instruction text
+# ---------------------------------------------------------------------------
+
+def _tokens(rest: str) -> Tuple[List[str], List[str]]:
+    """Operands (split at depth-0 commas) and trailing modifiers
+    (``offset:16``, ``clamp``, ``op_sel:[1,0]``) of an instruction."""
+    ops, mods, cur, depth = [], [], "", 0
+    for ch in rest:
+        if ch in "([":
+            depth += 1
+        elif ch in ")]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            ops.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        ops.append(cur.strip())
+    if ops:
+        last = ops[-1]
+        # modifiers follow the last operand after whitespace (not inside ( ))
+        depth, cut = 0, None
+        for i, ch in enumerate(last):
+            if ch in "([":
+                depth += 1
+            elif ch in ")]":
+                depth -= 1
+            elif ch == " " and depth == 0:
+                cut = i
+                break
+        if cut is not None:
+            mods = last[cut:].split()
+            ops[-1] = last[:cut].strip()
+    return ops, mods
+
+
+def parse(line: str):
+    t = line.strip()
+    parts = t.split(None, 1)
+    ops, mods = _tokens(parts[1]) if len(parts) > 1 else ([], [])
+    return parts[0], ops, mods
+
+
+def render(m: str, ops: Sequence[str], mods: Sequence[str] = ()) -> str:
+    s = "    " + m
+    if ops:
+        s += " " + ", ".join(ops)
+    if mods:
+        s += " " + " ".join(mods)
+    return s
+
+
+_VREG = re.compile(r"(-?)v(\d+)$")
+_VPAIR = re.compile(r"(-?)v\[(\d+):(\d+)\]$")
+_SREG = re.compile(r"s(\d+)$")
+_SPAIR = re.compile(r"s\[(\d+):(\d+)\]$")
+
+
+def vreg(tok: str) -> Optional[Tuple[int, int]]:
+    m = _VREG.match(tok)
+    if m:
+        return int(m.group(2)), 1
+    m = _VPAIR.match(tok)
+    if m:
+        return int(m.group(2)), int(m.group(3)) - int(m.group(2)) + 1
+    return None
+
+
+def sreg(tok: str) -> Optional[Tuple[int, int]]:
+    m = _SREG.match(tok)
+    if m:
+        return int(m.group(1)), 1
+    m = _SPAIR.match(tok)
+    if m:
+        return int(m.group(1)), int(m.group(2)) - int(m.group(1)) + 1
+    return None
+
+
+def shift_vreg(tok: str, off: int) -> str:
+    m = _VREG.match(tok)
+    if m:
+        return "%sv%d" % (m.group(1), int(m.group(2)) + off)
+    m = _VPAIR.match(tok)
+    if m:
+        return "%sv[%d:%d]" % (m.group(1), int(m.group(2)) + off, int(m.group(3)) + off)
+    return tok
+
+
+def int_value(tok: str) -> Optional[int]:
+    try:
+        return int(tok, 0) & M32
+    except ValueError:
+        return None
+
+
+def n_dest(m: str) -> int:
+    if m.startswith("v_cmp"):
+        return 1
+    if re.match(r"v_(add|sub|subrev|addc|subb|subbrev)_co_u32", m) or \
+            m.startswith(("v_mad_u64_u32", "v_mad_i64_i32")):
+        return 2
+    if m.startswith("v_"):
+        return 1
+    if m.startswith(("global_store", "scratch_store", "ds_write", "buffer_store")):
+        return 0
+    if m.startswith(("global_load", "scratch_load", "ds_read", "buffer_load", "s_load")):
+        return 1
+    if m.startswith(("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_waitcnt", "s_nop",
+                     "s_setpc", "s_endpgm", "s_set_gpr_idx", "s_swappc")):
+        return 0
+    return 1
+
+
+def is_salu(m: str) -> bool:
+    return m.startswith("s_") and not m.startswith(("s_load", "s_waitcnt", "s_nop", "s_branch",
+                                                     "s_cbranch", "s_setpc", "s_swappc",
+                                                     "s_getpc", "s_endpgm", "s_set_gpr_idx"))
+
+
+def _inline(v: int) -> Optional[str]:
+    """The value as an inline constant, when it is one (-16..64)."""
+    x = v - (1 << 32) if v >> 31 else v
+    return str(x) if -16 <= x <= 64 else None
+
+
+# scalar ops folded when every input is known: value, scc
+def _fold(m: str, vals: List[int]) -> Optional[Tuple[int, Optional[int]]]:
+    a = vals[0] if vals else 0
+    b = vals[1] if len(vals) > 1 else 0
+    if m == "s_mov_b32":
+        return a, None
+    if m == "s_movk_i32":
+        x = a & 0xFFFF
+        return (x - 0x10000 if x & 0x8000 else x) & M32, None
+    if m == "s_add_u32":
+        r = a + b
+        return r & M32, int(r >> 32 != 0)
+    if m == "s_sub_u32":
+        return (a - b) & M32, int(b > a)
+    if m in ("s_and_b32", "s_or_b32", "s_xor_b32"):
+        r = {"s_and_b32": a & b, "s_or_b32": a | b, "s_xor_b32": a ^ b}[m]
+        return r, int(r != 0)
+    if m == "s_lshl_b32":
+        r = (a << (b & 31)) & M32
+        return r, int(r != 0)
+    if m == "s_lshr_b32":
+        r = a >> (b & 31)
+        return r, int(r != 0)
+    if m == "s_bfe_u32":
+        off, width = b & 31, (b >> 16) & 0x7F
+        r = (a >> off) & ((1 << width) - 1)
+        return r, int(r != 0)
+    if m == "s_mul_i32":
+        return (a * b) & M32, None
+    return None
+
+
+_CMP = {"s_cmp_eq_u32": lambda a, b: a == b, "s_cmp_lg_u32": lambda a, b: a != b,
+        "s_cmp_lt_u32": lambda a, b: a < b, "s_cmp_le_u32": lambda a, b: a <= b,
+        "s_cmp_gt_u32": lambda a, b: a > b, "s_cmp_ge_u32": lambda a, b: a >= b,
+        "s_bitcmp1_b32": lambda a, b: (a >> (b & 31)) & 1 == 1}
+
+
+# ---------------------------------------------------------------------------
+# the specialiser
+# ---------------------------------------------------------------------------
+
+RECORD_SGPRS = frozenset(range(BANK0, BANK0 + 8))
+_LIVE: Dict[int, List[frozenset]] = {}
+_TARGETS: Dict[int, frozenset] = {}
+
+
+def _branch_targets(lines: Sequence[str]) -> frozenset:
+    """Labels some branch of the template jumps to (the others are only
+    fall-through points: no join, no state reset)."""
+    key = id(lines)
+    hit = _TARGETS.get(key)
+    if hit is None:
+        out = set()
+        for l in lines:
+            t = l.strip()
+            if t.startswith(("s_branch", "s_cbranch")):
+                out.add(t.split()[1])
+        hit = _TARGETS[key] = frozenset(out)
+    return hit
+
+
+def _live_after(lines: Sequence[str]) -> List[frozenset]:
+    """For each template line, the SGPRs some LATER line reads (an
+    over-approximation of liveness: later writes are ignored)."""
+    key = id(lines)
+    hit = _LIVE.get(key)
+    if hit is not None and len(hit) == len(lines):
+        return hit
+    out: List[frozenset] = [frozenset()] * len(lines)
+    acc: set = set()
+    for i in range(len(lines) - 1, -1, -1):
+        out[i] = frozenset(acc)
+        t = lines[i].strip()
+        if not t or t.startswith("@@") or t.endswith(":"):
+            continue
+        m, ops, _ = parse(_subst(t, "x"))
+        for x in ops[n_dest(m):] if not m.startswith(("s_set_gpr_idx", "s_cmp", "s_bitcmp")) else ops:
+            r = sreg(x)
+            if r:
+                acc.update(range(r[0], r[0] + r[1]))
+    _LIVE[key] = out
+    return out
+
+
+class _State:
+    def __init__(self, rec: Sequence[int]):
+        self.rec = {BANK0 + k: int(rec[k]) & M32 for k in range(8)}
+        self.known: Dict[int, int] = dict(self.rec)
+        self.mat: set = set()           # known SGPRs whose register holds the value
+        self.idx: Optional[Tuple[int, frozenset]] = None
+        self.scc: Optional[int] = None
+
+
+def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
+    """(hot lines, cold lines, heavy body called or None) of one record:
+    ``lines`` is the handler's JIT template, ``rec`` its 8 record words.
+
+    Scalar state: the record fields (s40..s47, never written by a handler)
+    are known on every path.  Values derived from them by folded scalar
+    arithmetic are known along the straight path; before any branch or join
+    the live ones are materialized (``s_mov_b32``) so the register holds
+    them on every path, and after a label only the record fields are known.
+    GPR-index state must agree on every path into a label (checked)."""
+    st = _State(rec)
+    live = _live_after(lines)
+    targets = {l.replace("%=", tag) for l in _branch_targets(lines)}
+    hot: List[str] = []
+    cold: List[str] = []
+    out = hot
+    idx_in: Dict[str, object] = {}       # label -> index state on the branches into it
+    idx_at: Dict[str, object] = {}       # label -> index state where it was placed
+    call = None
+    fallthrough = True
+
+    def emit(text):
+        out.append(text)
+
+    def materialize(regs):
+        for r in regs:
+            if r in st.known and r not in st.mat:
+                emit("    s_mov_b32 s%d, 0x%x" % (r, st.known[r]))
+                st.mat.add(r)
+
+    def settle(i):
+        """Before a branch or a join: derived values a later line may read
+        go into their registers."""
+        materialize(sorted(r for r in st.known if r not in RECORD_SGPRS and r in live[i]))
+
+    def written(regs):
+        for r in regs:
+            st.known.pop(r, None)
+            st.mat.discard(r)
+
+    def sregs_of(tok):
+        r = sreg(tok)
+        return list(range(r[0], r[0] + r[1])) if r else []
+
+    def branch_to(label):
+        if label in idx_at:
+            if idx_at[label] != st.idx:
+                raise JitUnsupported("index state differs on a branch back to %s" % label)
+        elif label in idx_in:
+            if idx_in[label] != st.idx:
+                raise JitUnsupported("index state differs on the branches into %s" % label)
+        else:
+            idx_in[label] = st.idx
+
+    for i, raw in enumerate(lines):
+        line = _subst(raw, tag)
+        t = line.strip()
+        if not t:
+            continue
+        if t == "@@END":
+            out = cold
+            fallthrough = False
+            continue
+        if t == "@@HALT":
+            emit("    s_setpc_b64 %s" % G.sp(G.JIT_RET))
+            out = cold
+            fallthrough = False
+            continue
+        if t.startswith("@@CALL"):
+            _, body, bits = t.split()
+            kind = "DIV" if "DIV" in body else "UMULNO"
+            # the body reads its record from S_CUR and its variant from S_VAR
+            for k in (G.F_D, G.F_A, G.F_B, G.F_W, G.F_MOFF):
+                emit("    s_mov_b32 s%d, 0x%x" % (G.S_CUR + k, int(rec[k]) & M32))
+            emit("    s_mov_b32 s%d, 0x%x" % (G.S_VAR, int(bits)))
+            lab = ".Lcall_%s" % tag
+            emit("    s_getpc_b64 %s" % G.sp(G.S_JMP))
+            emit(lab + ":")
+            emit("    s_add_u32 s%d, s%d, (%s - %s)" % (G.S_JMP, G.S_JMP, BODY_LABEL[kind], lab))
+            emit("    s_addc_u32 s%d, s%d, 0" % (G.S_JMP + 1, G.S_JMP + 1))
+            emit("    s_swappc_b64 %s, %s" % (G.sp(G.JIT_BODY_RET), G.sp(G.S_JMP)))
+            call = kind
+            out = cold
+            fallthrough = False
+            continue
+        if t.endswith(":"):
+            lab = t[:-1]
+            if lab not in targets:
+                if not fallthrough:
+                    raise JitUnsupported("label %s is never reached" % lab)
+                continue                     # no branch comes here: not a join
+            incoming = idx_in.pop(lab, "none")
+            if fallthrough:
+                settle(i)
+                if incoming != "none" and incoming != st.idx:
+                    raise JitUnsupported("index state differs at label %s" % lab)
+            elif incoming != "none":
+                st.idx = incoming
+            else:
+                raise JitUnsupported("label %s reached only from later code" % lab)
+            idx_at[lab] = st.idx
+            st.known = dict(st.rec)
+            st.mat = set()
+            st.scc = None
+            fallthrough = True
+            emit(t)
+            continue
+        m, ops, mods = parse(t)
+        # ---- GPR-index mode: resolved statically ----------------------------
+        if m == "s_set_gpr_idx_on":
+            r = sreg(ops[0])
+            if r is None or r[0] not in st.known:
+                raise JitUnsupported("dynamic GPR index")
+            modes = frozenset(re.search(r"gpr_idx\(([^)]*)\)", ops[1]).group(1).split(","))
+            st.idx = (st.known[r[0]] & 0xFF, modes)
+            continue
+        if m == "s_set_gpr_idx_idx":
+            r = sreg(ops[0])
+            if r is None or r[0] not in st.known or st.idx is None:
+                raise JitUnsupported("dynamic GPR index")
+            st.idx = (st.known[r[0]] & 0xFF, st.idx[1])
+            continue
+        if m == "s_set_gpr_idx_mode":
+            if st.idx is None:
+                raise JitUnsupported("index mode change while off")
+            st.idx = (st.idx[0], frozenset(re.search(r"gpr_idx\(([^)]*)\)", ops[0]).group(1).split(",")))
+            continue
+        if m == "s_set_gpr_idx_off":
+            st.idx = None
+            continue
+        if not fallthrough:
+            raise JitUnsupported("unreachable code after a jump: %s" % t)
+        # ---- control flow ------------------------------------------------
+        if m in ("s_cbranch_scc0", "s_cbranch_scc1") and st.scc is not None:
+            if st.scc == (1 if m == "s_cbranch_scc1" else 0):
+                settle(i)
+                branch_to(ops[0])
+                emit(render("s_branch", ops))
+                fallthrough = False
+            continue
+        if m.startswith("s_cbranch") or m == "s_branch":
+            settle(i)
+            branch_to(ops[0])
+            emit(render(m, ops, mods))
+            if m == "s_branch":
+                fallthrough = False
+            continue
+        nd = n_dest(m)
+        # ---- scalar ALU: fold known inputs -------------------------------
+        if is_salu(m):
+            dst, srcs = ops[:nd], ops[nd:]
+            if m in _CMP:
+                vals = [st.known.get(sreg(x)[0]) if sreg(x) and sreg(x)[1] == 1 else
+                        (int_value(x) if not sreg(x) else None) for x in srcs]
+                if all(v is not None for v in vals):
+                    st.scc = int(_CMP[m](vals[0], vals[1]))
+                    continue
+            if m == "s_cselect_b64" and st.scc is not None:
+                m, srcs = "s_mov_b64", [srcs[0] if st.scc else srcs[1]]
+                if srcs[0] == dst[0]:
+                    continue                 # keeps its value
+            if m == "s_mov_b64":
+                rs, dr = sregs_of(srcs[0]), sregs_of(dst[0])
+                if dr and rs and all(r in st.known for r in rs):
+                    vals = [st.known[r] for r in rs]
+                    written(dr)
+                    for d_, v_ in zip(dr, vals):
+                        st.known[d_] = v_
+                    continue
+                if dr and not rs and int_value(srcs[0]) == 0:
+                    written(dr)
+                    for d_ in dr:
+                        st.known[d_] = 0
+                    continue
+            one_reg = all((sreg(x) is None or sreg(x)[1] == 1) for x in srcs)
+            vals = [st.known.get(sreg(x)[0]) if sreg(x) else int_value(x) for x in srcs]
+            if one_reg and dst and sreg(dst[0]) and sreg(dst[0])[1] == 1 and \
+                    all(v is not None for v in vals):
+                r = _fold(m, vals)
+                if r is not None:
+                    d_ = sreg(dst[0])[0]
+                    written([d_])
+                    st.known[d_] = r[0]
+                    if r[1] is not None:
+                        st.scc = r[1]
+                    continue
+            # runtime: a known register input becomes a literal (one per
+            # instruction), the others are materialized
+            lit = sum(1 for x in srcs if not sreg(x) and int_value(x) is not None and
+                      _inline(int_value(x)) is None and not x.startswith("("))
+            new_srcs = []
+            for x in srcs:
+                r = sreg(x)
+                if r and r[1] == 1 and r[0] in st.known and r[0] not in st.mat:
+                    v = st.known[r[0]]
+                    if _inline(v) is not None:
+                        new_srcs.append(_inline(v))
+                        continue
+                    if lit == 0:
+                        new_srcs.append("0x%x" % v)
+                        lit = 1
+                        continue
+                if r:
+                    materialize(range(r[0], r[0] + r[1]))
+                new_srcs.append(x)
+            emit(render(m, dst + new_srcs, mods))
+            for x in dst:
+                written(sregs_of(x))
+            st.scc = None
+            continue
+        # ---- scalar memory: a known offset becomes the immediate ----------
+        if m.startswith("s_load"):
+            r = sreg(ops[2]) if len(ops) > 2 else None
+            if r and r[1] == 1 and r[0] in st.known and st.known[r[0]] < (1 << 20):
+                ops = ops[:2] + ["0x%x" % st.known[r[0]]]
+            else:
+                for x in ops[1:]:
+                    materialize(sregs_of(x))
+            emit(render(m, ops, mods))
+            written(sregs_of(ops[0]))
+            continue
+        # ---- vector ALU: static GPR indexing, known scalar inputs ---------
+        if m.startswith("v_"):
+            new = []
+            for k, x in enumerate(ops):
+                pos = "DST" if k < nd else ("SRC%d" % (k - nd) if k - nd < 3 else None)
+                if st.idx is not None and pos in st.idx[1] and vreg(x):
+                    x = shift_vreg(x, st.idx[0])
+                if k >= nd:
+                    r = sreg(x)
+                    if r and any(q in st.known and q not in st.mat for q in range(r[0], r[0] + r[1])):
+                        if r[1] == 1 and _inline(st.known[r[0]]) is not None:
+                            x = _inline(st.known[r[0]])
+                        else:
+                            materialize(range(r[0], r[0] + r[1]))
+                new.append(x)
+            for x in new:
+                vr = vreg(x)
+                if vr and vr[0] + vr[1] > G.NVGPR_KERNEL:
+                    raise JitUnsupported("VGPR v%d outside the kernel's budget" % (vr[0] + vr[1] - 1))
+            emit(render(m, new, mods))
+            for x in new[:nd]:
+                written(sregs_of(x))
+            continue
+        # ---- everything else (vector memory, LDS, waits, getpc) -----------
+        for x in ops[nd:]:
+            materialize(sregs_of(x))
+        emit(render(m, ops, mods))
+        for x in ops[:nd]:
+            written(sregs_of(x))
+    if idx_in:
+        raise JitUnsupported("branches to labels outside the handler: %s" % sorted(idx_in))
+    return hot, cold, call
+
+
+_FIELDS: Dict[int, Tuple[int, ...]] = {}
+_SPEC: Dict[tuple, tuple] = {}
+_TAG = "@T@"
+
+
+def fields_read(lines: Sequence[str]) -> Tuple[int, ...]:
+    """Record words a template reads (its s40..s47 operands)."""
+    key = id(lines)
+    hit = _FIELDS.get(key)
+    if hit is None:
+        used = set()
+        for l in lines:
+            for m in re.finditer(r"s\[?(\d+)(?::(\d+)\])?", l):
+                lo = int(m.group(1))
+                hi = int(m.group(2)) if m.group(2) else lo
+                used.update(k - BANK0 for k in range(lo, hi + 1) if BANK0 <= k < BANK0 + 8)
+            if l.startswith("@@CALL"):
+                used.update((G.F_D, G.F_A, G.F_B, G.F_W, G.F_MOFF))
+        hit = _FIELDS[key] = tuple(sorted(used))
+    return hit
+
+
+def specialize_cached(name: str, var: int, rec: Sequence[int], tag: str):
+    """specialize() of a record, memoised on the record words its template
+    reads (records repeat across and within programs: same slots, same
+    widths)."""
+    lines = template(name, var)
+    key = (name, var) + tuple(int(rec[k]) for k in fields_read(lines))
+    hit = _SPEC.get(key)
+    if hit is None:
+        full = [0] * 8
+        for k in fields_read(lines):
+            full[k] = int(rec[k])
+        hit = specialize(lines, full, _TAG)
+        if len(_SPEC) > 200000:
+            _SPEC.clear()
+        _SPEC[key] = hit
+    hot, cold, call = hit
+    return ([l.replace(_TAG, tag) if _TAG in l else l for l in hot],
+            [l.replace(_TAG, tag) if _TAG in l else l for l in cold], call)
+
+
+# ---------------------------------------------------------------------------
+# programs
+# ---------------------------------------------------------------------------
+
+def decode(h: int) -> Tuple[str, int]:
+    c = G.canonical(int(h))
+    return G.AOPS[c // (2 * G.NVAR)], (c // 2) % G.NVAR
+
+
+def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6):
+    """The records ``mg_load_program`` uploads for ``prog`` (handler ids in
+    word 0; LEAFD records patched with their leaf's generator parameters
+    exactly as mg_load_program does), and the translator's mask count."""
+    from .engine import translate_records
+    rec, n_masks = translate_records(prog, lds_slots)
+    rec = rec.reshape(-1, 8).copy()
+    n_consts = prog.consts.shape[0]
+    n_leaves = len(prog.leaves)
+    for r in rec:
+        name, var = decode(r[0])
+        li = int(r[4])
+        if name == "LEAFD" and li < n_leaves:
+            g = leafgen[li]
+            salt = ((prog_seed * 0xD1B54A32D192ED03) ^ ((li + 1) * 0x8CB92BA72F3D8DD7)) & ((1 << 64) - 1)
+            r[1] = (n_consts + n_masks + 3 * g.pool_off) * 32
+            r[2], r[3] = salt & M32, salt >> 32
+            r[5] = g.pool_n
+            r[7] = g.pct_uniform | g.pct_small << 8 | g.pct_boundary << 16
+    return rec[:-1], n_masks                     # the last record is the zeroed pad
+
+
+def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
+                tag: Optional[str] = None) -> List[str]:
+    """Straight-line gfx950 code of one program, entered at label
+    ``entry`` (a local ``.L`` label, or a symbol the caller declares)."""
+    recs, _ = program_records(prog, leafgen, prog_seed, lds_slots)
+    tag = tag or entry.lstrip(".L")
+    out = [entry + ":"]
+    pending_cold: List[str] = []
+    flush_no = 0
+    for i, r in enumerate(recs):
+        name, var = decode(r[0])
+        hot, cold, _ = specialize_cached(name, var, r, "%s_%d" % (tag, i))
+        out.extend(hot)
+        pending_cold.extend(cold)
+        if name == "HALT" or (pending_cold and (i + 1) % COLD_FLUSH == 0):
+            if name != "HALT":
+                skip = ".L%s_k%d" % (tag, flush_no)
+                out.append("    s_branch %s" % skip)
+                out.extend(pending_cold)
+                out.append(skip + ":")
+            else:
+                out.extend(pending_cold)
+            pending_cold = []
+            flush_no += 1
+        if name == "HALT":
+            break
+    return peephole(out)
+
+
+def peephole(lines: List[str]) -> List[str]:
+    """Drop ``s_waitcnt lgkmcnt(0)`` where no LDS / scalar-memory operation
+    was issued since the last one on the straight path (a label or a call
+    counts as possibly pending)."""
+    out, pending = [], True
+    for l in lines:
+        t = l.strip()
+        if t.endswith(":") or t.startswith(("s_load", "ds_", "s_swappc")):
+            pending = True
+        elif t == "s_waitcnt lgkmcnt(0)":
+            if not pending:
+                continue
+            pending = False
+        out.append(l)
+    return out
+
+
+HEADER = '\t.amdgcn_target "amdgcn-amd-amdhsa--%s"\n' % ARCH
+
+
+def chunk_asm(items, first: int, lds_slots: int = 6) -> str:
+    """One object's worth of programs: program ``first + i`` is entered at
+    the (hidden) symbol ``mg_jp<first+i>``; the shared heavy bodies are
+    copied into every chunk (local labels, a few KiB)."""
+    parts = [HEADER, "\t.text\n\t.p2align 8\n"]
+    for i, (p, g, s) in enumerate(items):
+        sym = "mg_jp%d" % (first + i)
+        parts.append("\t.globl %s\n\t.hidden %s\n" % (sym, sym))
+        parts.append("\n".join(program_asm(p, g, s, sym, lds_slots, tag="p%d" % (first + i))))
+        parts.append("\n")
+    parts.append("\t.p2align 6\n" + "\n".join(bodies()) + "\n")
+    return "".join(parts)
+
+
+def table_asm(n: int) -> str:
+    """The stub kernel and ``mg_jit_table``: entry i = mg_jp<i> - table."""
+    stub = open(STUB).read()
+    cut = stub.index("\t.ident")
+    rows = "".join("\t.quad mg_jp%d - . + %d\n" % (i, 8 * i) for i in range(n))
+    return (stub[:cut] + "\t.data\n\t.globl mg_jit_table\n\t.protected mg_jit_table\n"
+            "\t.type mg_jit_table,@object\n\t.p2align 3\nmg_jit_table:\n" + rows +
+            "\t.size mg_jit_table, %d\n" % (8 * n) + stub[cut:])
+
+
+def _as(text: str, obj: str) -> None:
+    src = obj[:-2] + ".s"
+    with open(src, "w") as fh:
+        fh.write(text)
+    subprocess.run([os.path.join(LLVM_BIN, "clang"), "-cc1as", "-triple", "amdgcn-amd-amdhsa",
+                    "-target-cpu", ARCH, "-filetype", "obj", src, "-o", obj], check=True)
+
+
+def _chunk_job(args):
+    items, first, lds_slots, obj = args
+    if any(g is None for _, g, _ in items):
+        from .engine import default_leafgen
+        items = [(p, default_leafgen(p) if g is None else g, s) for p, g, s in items]
+    _as(chunk_asm(items, first, lds_slots), obj)
+    return obj
+
+
+def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
+                  start: str = "fork") -> bytes:
+    """gfx950 code object of [(program, leafgen or None (= the C2 default),
+    prog_seed)], entries in order (``Engine.jit_attach`` takes the same
+    programs in the same order).  Chunks of programs are rendered and
+    assembled on ``workers`` host processes (``start="fork"`` before the
+    process touches the GPU, ``"spawn"`` after), then linked with the table
+    into one shared object."""
+    with tempfile.TemporaryDirectory() as d:
+        jobs = [(list(items[i:i + chunk]), i, lds_slots, os.path.join(d, "c%d.o" % i))
+                for i in range(0, len(items), chunk)]
+        if workers > 1 and len(jobs) > 1:
+            import multiprocessing as mp
+            with mp.get_context(start).Pool(min(workers, len(jobs))) as pool:
+                objs = pool.map(_chunk_job, jobs, chunksize=1)
+        else:
+            objs = [_chunk_job(j) for j in jobs]
+        tab = os.path.join(d, "table.o")
+        _as(table_asm(len(items)), tab)
+        out = os.path.join(d, "jit.hsaco")
+        subprocess.run([os.path.join(LLVM_BIN, "ld.lld"), "-shared", tab] + objs + ["-o", out],
+                       check=True)
+        with open(out, "rb") as fh:
+            return fh.read()

@@ -309,6 +309,9 @@ class Wave:
     def i_s_nop(self, a, pc):
         return None
 
+    def i_s_endpgm(self, a, pc):
+        return len(self.instrs)          # the C++ shell's code after the asm
+
     def i_s_waitcnt(self, a, pc):
         t = " ".join(a)
         if "lgkmcnt(0)" in t:
@@ -347,6 +350,12 @@ class Wave:
         x, y = self.sread(a[1]), self.sread(a[2])
         self.swrite(a[0], (x - y) & M32)
         self.scc = int(x < y)
+
+    def i_s_subb_u32(self, a, pc):
+        x, y = self.sread(a[1]), self.sread(a[2])
+        r = x - y - self.scc
+        self.swrite(a[0], r & M32)
+        self.scc = int(r < 0)
 
     def i_s_and_b32(self, a, pc):
         self._sop2(a, lambda x, y: x & y)
@@ -441,6 +450,14 @@ class Wave:
         off = t - CODE_BASE
         if off < 0 or off % 8 or off // 8 >= len(self.instrs):
             raise SimError("s_setpc to a non-instruction address 0x%x" % t)
+        return off // 8
+
+    def i_s_swappc_b64(self, a, pc):
+        t = self.sread(a[1], 64)
+        self.swrite(a[0], CODE_BASE + 8 * (pc + 1))
+        off = t - CODE_BASE
+        if off < 0 or off % 8 or off // 8 >= len(self.instrs):
+            raise SimError("s_swappc to a non-instruction address 0x%x" % t)
         return off // 8
 
     def i_s_set_gpr_idx_on(self, a, pc):
@@ -810,23 +827,42 @@ class Wave:
 # driving the interpreter body like mg_interp_asm does
 # ---------------------------------------------------------------------------
 
-OPERANDS = {  # inline-asm operands -> registers the simulator uses
-    "%[root]": "v200", "%[idx_lo]": "v201", "%[idx_hi]": "v202", "%[lds]": "v203",
-    "%[desc]": "s[0:1]", "%[seed]": "s[2:3]", "%[first]": "s[4:5]", "%[leaves]": "s[6:7]",
-    "%[stride]": "s[8:9]", "%[lout]": "s[10:11]", "%[probes]": "s[12:13]", "%[mode]": "s14",
-    "%[scr]": "s15", "%[active]": "s[16:17]", "%[table]": "s[18:19]",
-}
+def _operands():
+    """inline-asm operands -> the registers the kernel pins them to
+    (asmgen.PINNED): the simulator runs the exact text, compiled programs
+    (mythril_amd/jit.py) included."""
+    from mythril_amd import asmgen
+    return {"%%[%s]" % k: r for k, r in asmgen.PINNED.items()}
+
+
+OPERANDS = _operands()
+
+
+def _set_input(w, name: str, val: int):
+    """Write a kernel input into its pinned register(s)."""
+    from mythril_amd import asmgen
+    reg = asmgen.PINNED[name]
+    m = re.fullmatch(r"s\[(\d+):(\d+)\]", reg) or re.fullmatch(r"s(\d+)", reg)
+    base = int(m.group(1))
+    w.s[base] = val & M32
+    if "[" in reg:
+        w.s[base + 1] = (val >> 32) & M32
+
+
+def _vreg_of(name: str) -> int:
+    from mythril_amd import asmgen
+    return int(asmgen.PINNED[name][1:])
 
 
 def handler_table(lines: List[str], n_handlers: int) -> List[int]:
     """Run the body in query mode (as mg_init does) and return the table."""
     mem = Memory()
-    desc = mem.alloc(bytes(64), "desc")
+    desc = mem.alloc(bytes(80), "desc")
     table = mem.alloc(bytes(4 * n_handlers), "table")
     w = Wave(lines, OPERANDS, mem)
-    w.s[0], w.s[1] = desc & M32, desc >> 32
-    w.s[14] = 2
-    w.s[18], w.s[19] = table & M32, table >> 32
+    _set_input(w, "desc", desc)
+    _set_input(w, "mode", 2)
+    _set_input(w, "table", table)
     w.run()
     buf = mem.region(table)
     return list(struct.unpack_from("<%dI" % n_handlers, buf, 0))
@@ -894,13 +930,23 @@ def expanded_pool(consts: np.ndarray) -> np.ndarray:
 
 
 def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
-             active: int = (1 << NL) - 1, rcp_noise: float = 0.0, want_leaves: bool = False):
+             active: int = (1 << NL) - 1, rcp_noise: float = 0.0, want_leaves: bool = False,
+             jit: bool = False):
     """Run one 64-lane wave of the assembly interpreter on a compiled
     Program.  Eval mode: soa [n_leaves][8][64] u32.  Generator mode: gen =
     (seed, prog_seed, first_index, leafgens) with leafgens the engine's
-    LeafGen list.  Returns (root bits [64] bool, probes [n_probes][8][64],
+    LeafGen list.  ``jit``: the program's compiled code (mythril_amd/jit.py)
+    is appended and entered through the descriptor's jit_entry, as on the
+    GPU.  Returns (root bits [64] bool, probes [n_probes][8][64],
     leaves_out [n_leaves][8][64] or None, wave)."""
     lines, _ = body_and_table()
+    if jit:
+        from mythril_amd import jit as J
+        from mythril_amd.engine import default_leafgen
+        lg = gen[3] if gen is not None else default_leafgen(prog)
+        ps = gen[1] if gen is not None else 0
+        lines = list(lines) + ["    s_endpgm"] + J.program_asm(prog, lg, ps, ".Ljp0", n_lds) + \
+            J.bodies()
     rec, masks = translate(prog, n_lds)
     mem = Memory()
     pc = np.ascontiguousarray(prog.consts, dtype=np.uint32).reshape(-1, 8)
@@ -932,28 +978,29 @@ def simulate(prog, soa: Optional[np.ndarray] = None, gen=None, n_lds: int = 6,
         x_base = mem.alloc(rec.astype(np.uint32).tobytes(), "records")
     g_base = mem.alloc(gdev.tobytes(), "gen")
     b_base = mem.alloc(boundary_table().tobytes(), "btab")
-    desc = struct.pack("<QQQIIIIQQQ", 0, c_base, g_base, prog.n_ins, n_leaves, 0, 0,
-                       prog_seed & M64, x_base, b_base)
+    w = Wave(lines, OPERANDS, mem, rcp_noise=rcp_noise)
+    jit_entry = w.addr_of(".Ljp0") if jit else 0
+    desc = struct.pack("<QQQIIIIQQQQ", 0, c_base, g_base, prog.n_ins, n_leaves, 0, 0,
+                       prog_seed & M64, x_base, b_base, jit_entry)
     d_base = mem.alloc(desc, "desc")
     lv = soa if soa is not None else np.zeros((max(1, n_leaves), 8, NL), dtype=np.uint32)
     l_base = mem.alloc(np.ascontiguousarray(lv, dtype=np.uint32).tobytes(), "leaves")
     n_pr = max(1, prog.n_probes)
     p_base = mem.alloc(bytes(n_pr * 8 * NL * 4), "probes")
     o_base = mem.alloc(bytes(max(1, n_leaves) * 8 * NL * 4), "leaves_out") if want_leaves else 0
-    w = Wave(lines, OPERANDS, mem, rcp_noise=rcp_noise)
-    for reg, val in ((0, d_base), (2, seed & M64), (4, first & M64), (6, l_base), (8, NL),
-                     (10, o_base), (12, p_base if prog.n_probes else 0), (16, active)):
-        w.s[reg], w.s[reg + 1] = val & M32, (val >> 32) & M32
-    w.s[14] = 1 if gen is not None else 0
-    w.s[15] = 0
+    for name, val in (("desc", d_base), ("seed", seed & M64), ("first", first & M64),
+                      ("leaves", l_base), ("stride", NL), ("lout", o_base),
+                      ("probes", p_base if prog.n_probes else 0), ("active", active),
+                      ("mode", 1 if gen is not None else 0), ("scr", 0)):
+        _set_input(w, name, val)
     idx = [(first + lane) & M64 for lane in range(NL)]      # the shell's first + lane
-    w.v[201] = np.array([i & M32 for i in idx], dtype=np.uint64)
-    w.v[202] = np.array([i >> 32 for i in idx], dtype=np.uint64)
-    w.v[203] = np.arange(NL, dtype=np.uint64) * 16
-    w.run()
+    w.v[_vreg_of("idx_lo")] = np.array([i & M32 for i in idx], dtype=np.uint64)
+    w.v[_vreg_of("idx_hi")] = np.array([i >> 32 for i in idx], dtype=np.uint64)
+    w.v[_vreg_of("lds")] = np.arange(NL, dtype=np.uint64) * 16
+    w.run(max_steps=20_000_000)
     if w.pending:
         raise SimError("loads still pending at exit: %s" % sorted(w.pending))
-    root = (w.v[200] & 1).astype(bool)
+    root = (w.v[_vreg_of("root")] & 1).astype(bool)
     probes = np.frombuffer(bytes(mem.region(p_base)), dtype=np.uint32).reshape(n_pr, 8, NL)
     lout = None
     if want_leaves:

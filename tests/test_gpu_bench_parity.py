@@ -58,9 +58,10 @@ def units():
     return out
 
 
-def _run_batch(engine, progs):
+def _run_batch(engine, progs, image=None):
     hip = C.CDLL("libamdhip64.so.7")
     loaded = [engine.load(p, default_leafgen(p), prog_seed=d) for d, p in progs]
+    jit_h = engine.jit_attach(loaded, image) if image is not None else None
     batch = engine.batch_create(loaded)
     bits = np.zeros((len(progs), N_LANES // 64), dtype=np.uint64)
     firsts = np.full(len(progs), shard.NONE, dtype=np.int64)
@@ -78,29 +79,43 @@ def _run_batch(engine, progs):
                              C.c_size_t(firsts.nbytes), 2) == 0
     finally:
         engine.batch_free(batch)
+        if jit_h is not None:
+            engine.jit_detach(jit_h)
         hip.hipFree(d_bits)
         hip.hipFree(d_first)
     return bits, firsts.tolist()
 
 
+@pytest.fixture(scope="module")
+def images(units):
+    """Compiled-program code objects of every bench unit (bench.py --jit),
+    built on spawned workers."""
+    from mythril_amd import jit
+    return {w: jit.compile_batch([(p, None, d) for d, p, _ in units[w]], workers=16,
+                                 start="spawn") for w in FULL}
+
+
+@pytest.mark.parametrize("path", ["interp", "jit"])
 @pytest.mark.parametrize("workload", ["c2", "c3", "c4"])
-def test_every_bench_unit_every_lane(engine, units, workload):
+def test_every_bench_unit_every_lane(engine, units, images, workload, path):
     us = units[workload]
     assert len(us) == FULL[workload]
-    bits, firsts = _run_batch(engine, [(d, p) for d, p, _ in us])
+    bits, firsts = _run_batch(engine, [(d, p) for d, p, _ in us],
+                              images[workload] if path == "jit" else None)
     n_sat = n_hit = 0
     for k, (d, p, packed) in enumerate(us):
         want = np.unpackbits(packed, bitorder="little")[:N_LANES].astype(bool)
         got = unpack_bits(bits[k], N_LANES)
-        assert np.array_equal(got, want), (workload, d, int(np.argmax(got != want)))
+        assert np.array_equal(got, want), (workload, path, d, int(np.argmax(got != want)))
         hit = np.flatnonzero(want)
         assert firsts[k] == (FIRST + int(hit[0]) if hit.size else shard.NONE), (workload, d)
         n_sat += int(hit.size)
         n_hit += bool(hit.size)
-    for d, p, _ in us:
-        CHECKED.update(handler_variants(p))
-    print("%s: %d units, %d with satisfying lanes, %d satisfying lanes"
-          % (workload, len(us), n_hit, n_sat))
+    if path == "interp":
+        for d, p, _ in us:
+            CHECKED.update(handler_variants(p))
+    print("%s %s: %d units, %d with satisfying lanes, %d satisfying lanes"
+          % (workload, path, len(us), n_hit, n_sat))
 
 
 def test_bench_handler_variants_all_checked(units):

@@ -1,0 +1,116 @@
+"""Compiled programs (mythril_amd/jit.py) on the CPU: the straight-line code
+generated for a program, run through the instruction-level simulator
+(tests/asm_sim.py) exactly as the GPU enters it (the interpreter kernel's
+body, the descriptor's jit_entry, s_swappc, shared division bodies), gives
+the interpreter's results bit for bit and the oracle's values on every lane;
+the code object assembles and its entry table points at each program."""
+
+import random
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import asm_sim
+import dag_cases
+from mythril_amd import jit
+from mythril_amd.assign import Assignment as PA, pack, unpack
+from mythril_amd.corpus import make_dag
+from mythril_amd.engine import default_leafgen, limbs_to_int
+from mythril_amd.ir import compile_constraints
+from oracle import smtlib_ref as R
+from test_gpu_parity import flat_expected
+
+CASES = dag_cases.named_cases()
+SEED = 0x6D797468
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_jit_case_equals_interpreter_and_oracle(name):
+    constraints, probes, gen, tables = CASES[name]
+    prog = compile_constraints(constraints, probes, table_sizes=tables)
+    rng = random.Random(3000 + len(name))
+    asgs = [gen(rng) for _ in range(64)]
+    soa = pack(prog, [PA(a.vars, a.arrays, a.funcs) for a in asgs])
+    r_i, pr_i, _, _ = asm_sim.simulate(prog, soa)
+    r_j, pr_j, _, _ = asm_sim.simulate(prog, soa, jit=True)
+    assert np.array_equal(pr_i, pr_j) and np.array_equal(r_i, r_j)
+    for a, asg in enumerate(asgs):
+        want = flat_expected(probes, R.evaluate(list(probes), asg))
+        got = [limbs_to_int(pr_j[k, :, a]) for k in range(prog.n_probes)]
+        assert got == want, a
+        assert bool(r_j[a]) == bool(R.eval_constraints(constraints, asg)), a
+
+
+@pytest.mark.parametrize("dag_id,n_lds", [(0, 6), (5, 6), (571, 6), (7, 2), (33, 0)])
+def test_jit_corpus_dag_generator_mode(dag_id, n_lds):
+    """Corpus DAGs with every constraint probed, device-generated leaves,
+    spills split between LDS and scratch: interpreter == compiled, and the
+    oracle agrees on every lane."""
+    roots, _ = make_dag(dag_id, SEED)
+    prog = compile_constraints([], roots)
+    lg = default_leafgen(prog)
+    first = 4096 + 77 * dag_id
+    r_i, pr_i, lo_i, _ = asm_sim.simulate(prog, gen=(SEED, dag_id, first, lg), n_lds=n_lds,
+                                          want_leaves=True)
+    r_j, pr_j, lo_j, _ = asm_sim.simulate(prog, gen=(SEED, dag_id, first, lg), n_lds=n_lds,
+                                          want_leaves=True, jit=True)
+    assert np.array_equal(lo_i, lo_j) and np.array_equal(pr_i, pr_j) and np.array_equal(r_i, r_j)
+    for lane in range(0, 64, 7):
+        asg = unpack(prog, lo_j[:, :, lane])
+        want = R.evaluate(list(roots), R.Assignment(asg.vars, asg.arrays, asg.funcs))
+        assert [int(pr_j[k, 0, lane]) for k in range(len(roots))] == [int(w) for w in want]
+
+
+def test_jit_text_has_no_scalar_stores_and_fits_the_register_budget():
+    roots, _ = make_dag(9, SEED)
+    prog = compile_constraints(roots)
+    text = jit.program_asm(prog, default_leafgen(prog), 9, ".Ljp0") + jit.bodies()
+    for bad in ("s_store", "s_buffer_store", "s_scratch_store", "s_dcache", "s_atomic"):
+        assert not any(bad in l for l in text)
+    for l in text:
+        for m in re.finditer(r"v\[?(\d+)", l):
+            assert int(m.group(1)) < 168, l
+    assert not any("s_set_gpr_idx" in l for l in jit.program_asm(prog, default_leafgen(prog), 9,
+                                                                  ".Ljp1"))
+
+
+def test_jit_image_entries_point_at_each_program():
+    """compile_batch links chunk objects and the table: entry i (relative
+    to mg_jit_table) is the first instruction of program i."""
+    items = []
+    for d in (1, 2, 3, 4, 5):
+        roots, _ = make_dag(d, SEED)
+        p = compile_constraints(roots)
+        items.append((p, default_leafgen(p), d))
+    image = jit.compile_batch(items, chunk=2)
+    with open("/tmp/_mg_jit_test.hsaco", "wb") as fh:
+        fh.write(image)
+    syms = subprocess.run([jit.LLVM_BIN + "/llvm-readelf", "-s", "/tmp/_mg_jit_test.hsaco"],
+                          capture_output=True, text=True, check=True).stdout
+    tab = int(re.search(r"([0-9a-f]+)\s+40 OBJECT\s+GLOBAL\s+\w+\s+\d+ mg_jit_table", syms).group(1), 16)
+    data = subprocess.run([jit.LLVM_BIN + "/llvm-objdump", "-s", "-j", ".data",
+                           "/tmp/_mg_jit_test.hsaco"], capture_output=True, text=True,
+                          check=True).stdout
+    words = {}
+    for line in data.splitlines():
+        m = re.match(r"\s*([0-9a-f]+)\s+((?:[0-9a-f]{8}\s?){1,4})", line)
+        if m:
+            base = int(m.group(1), 16)
+            for k, wd in enumerate(m.group(2).split()):
+                words[base + 4 * k] = int.from_bytes(bytes.fromhex(wd), "little")
+    dis = subprocess.run([jit.LLVM_BIN + "/llvm-objdump", "-d", "/tmp/_mg_jit_test.hsaco"],
+                         capture_output=True, text=True, check=True).stdout
+    at = {}
+    for line in dis.splitlines():
+        m = re.search(r"^\s+(\S+).*//\s*([0-9A-F]+):", line)
+        if m:
+            at[int(m.group(2), 16)] = m.group(1)
+    for i, (p, g, s) in enumerate(items):
+        rel = words[tab + 8 * i] | words[tab + 8 * i + 4] << 32
+        rel -= 1 << 64 if rel >> 63 else 0
+        assert rel < 0
+        text = jit.program_asm(p, g, s, "x", tag="p%d" % i)
+        first = next(l.split()[0] for l in text[1:] if l.strip() and not l.strip().endswith(":"))
+        assert at[tab + rel].startswith(first), (i, at[tab + rel], first)
