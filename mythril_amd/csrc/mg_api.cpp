@@ -659,8 +659,10 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
         return fail(ctx, MG_E_HIP, "JIT image: %s (table %zu bytes for %u programs)",
                     hipGetErrorString(e), table_b, n_progs);
     }
+    // (segment alignment can place the table past the file size; the bound
+    // only guards against garbage)
     for (uint32_t i = 0; i < n_progs; ++i)
-        if (rel[i] >= 0 || -rel[i] > (int64_t)image_size || (rel[i] & 3)) {
+        if (rel[i] >= 0 || -rel[i] > 2 * (int64_t)image_size + (1 << 20) || (rel[i] & 3)) {
             (void)hipModuleUnload(mod);
             return fail(ctx, MG_E_ARG, "JIT image: entry %u at %lld outside the code", i,
                         (long long)rel[i]);
