@@ -927,6 +927,10 @@ def h_spill_lds(a: Asm, bank: int, slot: int):
     """LDS spill straight from slot ``slot`` (the variant)."""
     fa = FB + 8 * slot
     prologue(a, bank)
+    if JIT:       # the slot's byte offset is the record's: an instruction offset
+        a("ds_write_b128 %s, v[%d:%d] offset:@F%d@" % (OP_LDS, fa, fa + 3, F_IMM))
+        a("ds_write_b128 %s, v[%d:%d] offset:@F%d+4096@" % (OP_LDS, fa + 4, fa + 7, F_IMM))
+        return dispatch(a, 1 - bank)
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
     a("ds_write_b128 %s, v[%d:%d]" % (v(T[0]), fa, fa + 3))
     a("ds_write_b128 %s, v[%d:%d] offset:4096" % (v(T[0]), fa + 4, fa + 7))
@@ -938,6 +942,10 @@ def h_reload_lds(a: Asm, bank: int, slot: int):
     lgkmcnt wait covers the reads."""
     fd = FB + 8 * slot
     prologue(a, bank)
+    if JIT:
+        a("ds_read_b128 v[%d:%d], %s offset:@F%d@" % (fd, fd + 3, OP_LDS, F_IMM))
+        a("ds_read_b128 v[%d:%d], %s offset:@F%d+4096@" % (fd + 4, fd + 7, OP_LDS, F_IMM))
+        return dispatch(a, 1 - bank)
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
     a("ds_read_b128 v[%d:%d], %s" % (fd, fd + 3, v(T[0])))
     a("ds_read_b128 v[%d:%d], %s offset:4096" % (fd + 4, fd + 7, v(T[0])))

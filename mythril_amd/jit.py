@@ -386,6 +386,10 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
 
     for i, raw in enumerate(lines):
         line = _subst(raw, tag)
+        if "@F" in line:            # a record field as an instruction immediate
+            line = re.sub(r"@F(\d)(?:\+(\d+))?@",
+                          lambda mm: str((int(rec[int(mm.group(1))]) + int(mm.group(2) or 0))
+                                         & M32), line)
         t = line.strip()
         if not t:
             continue
@@ -585,6 +589,227 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
     return hot, cold, call
 
 
+# ---------------------------------------------------------------------------
+# copy coalescing: the interpreter stages operands in temporaries (Y <- slot,
+# R = op(...), slot <- R) because its register file is indexed; with fixed
+# registers the staging copies can go
+# ---------------------------------------------------------------------------
+
+SLOTS = range(G.FB, G.FB + 8 * G.NREG)                 # v8..v135
+TEMPS = frozenset(list(range(G.XB, G.XB + 8)) + list(range(G.YB, G.TB + G.NT)))
+COALESCE = os.environ.get("MYTHGPU_JIT_COALESCE", "1") != "0"
+
+
+def _vregs(tok: str) -> List[int]:
+    r = vreg(tok)
+    return list(range(r[0], r[0] + r[1])) if r else []
+
+
+class _Ins:
+    """One instruction of a straight segment: VGPR defs / uses per operand."""
+    __slots__ = ("m", "ops", "mods", "nd", "masked", "load", "valu")
+
+    def __init__(self, m, ops, mods, masked):
+        self.m, self.ops, self.mods, self.masked = m, ops, mods, masked
+        self.nd = n_dest(m)
+        self.load = m.startswith(("global_load", "scratch_load", "ds_read", "buffer_load"))
+        self.valu = m.startswith("v_")
+
+    def def_ops(self):
+        return [i for i in range(self.nd) if vreg(self.ops[i])]
+
+    def use_ops(self):
+        return [i for i in range(self.nd, len(self.ops)) if vreg(self.ops[i])]
+
+    def defs(self):
+        return {r for i in self.def_ops() for r in _vregs(self.ops[i])}
+
+    def uses(self):
+        u = {r for i in self.use_ops() for r in _vregs(self.ops[i])}
+        if self.masked:                 # inactive lanes keep the old value
+            u |= self.defs()
+        return u
+
+    def text(self):
+        return render(self.m, self.ops, self.mods)
+
+
+def _rename(tok: str, mp: Dict[int, int]) -> Optional[str]:
+    """tok with its registers mapped (all or none, contiguously), or None."""
+    regs = _vregs(tok)
+    if not regs or not any(r in mp for r in regs):
+        return tok
+    if not all(r in mp for r in regs):
+        return None
+    new = [mp[r] for r in regs]
+    if new != list(range(new[0], new[0] + len(new))) or (len(new) > 1 and new[0] % 2):
+        return None
+    return shift_vreg(tok, new[0] - regs[0])
+
+
+def _copy(ins: _Ins) -> Optional[Tuple[List[int], List[int]]]:
+    if ins.m not in ("v_mov_b32", "v_mov_b64") or ins.mods or len(ins.ops) != 2:
+        return None
+    d, s_ = _vregs(ins.ops[0]), _vregs(ins.ops[1])
+    if not d or not s_ or len(d) != len(s_) or ins.ops[1].startswith("-"):
+        return None
+    return d, s_
+
+
+def _forward(seg: List[Optional[_Ins]], final: bool) -> None:
+    """temp <- slot copies: later reads of the temp read the slot instead;
+    the copy goes when no read of the temp needs it any more."""
+    for k, ins in enumerate(seg):
+        c = _copy(ins) if ins is not None else None
+        if c is None or ins.masked:
+            continue                        # a masked copy merges: the temp != the slot
+        d, s_ = c
+        if not all(r in TEMPS for r in d) or not all(r in SLOTS for r in s_):
+            continue
+        mp = dict(zip(d, s_))
+        state = {t: "active" for t in d}    # active: substitutable; stale: slot changed
+        keep = False
+        for j in range(k + 1, len(seg)):
+            x = seg[j]
+            if x is None:
+                continue
+            for i in x.use_ops():
+                regs = [r for r in _vregs(x.ops[i]) if state.get(r) in ("active", "stale")]
+                if not regs:
+                    continue
+                live = {t: mp[t] for t in d if state[t] == "active"}
+                t = _rename(x.ops[i], live)
+                if t is None:
+                    keep = True
+                else:
+                    x.ops[i] = t
+            dd = x.defs()
+            if x.masked and any(state.get(r) in ("active", "stale") for r in dd):
+                keep = True                 # inactive lanes keep the temp's value
+            for r in dd:
+                if state.get(r) in ("active", "stale"):
+                    state[r] = "dead"       # rewritten: later reads are not ours
+            for t in d:
+                if state[t] == "active" and mp[t] in dd:
+                    state[t] = "stale"      # the slot changed under the temp
+        if not final and any(v != "dead" for v in state.values()):
+            keep = True                     # may be read after the segment
+        if not keep:
+            seg[k] = None
+
+
+def _read_later(seg, start, reg) -> bool:
+    for x in seg[start:]:
+        if x is None:
+            continue
+        if reg in x.uses():
+            return True
+        if reg in x.defs():
+            return False
+    return False
+
+
+def _backward(seg: List[Optional[_Ins]], final: bool) -> None:
+    """slot <- temp copies: the instructions that build the temp write the
+    slot directly; the copy goes."""
+    for k in range(len(seg) - 1, -1, -1):
+        ins = seg[k]
+        c = _copy(ins) if ins is not None else None
+        if c is None or ins.masked:
+            continue
+        d, s_ = c
+        if not all(r in SLOTS for r in d) or not all(r in TEMPS for r in s_):
+            continue
+        mp = dict(zip(s_, d))               # temp -> slot
+        # the temp must be dead after the copy
+        dead = True
+        for r in s_:
+            if _read_later(seg, k + 1, r):
+                dead = False
+            elif not final and not any(r in x.defs() for x in seg[k + 1:] if x is not None):
+                dead = False
+        if not dead:
+            continue
+        need = set(s_)                      # temps whose full definition is still ahead (backward)
+        web = []
+        ok = False
+        for j in range(k - 1, -1, -1):
+            x = seg[j]
+            if x is None:
+                continue
+            touched = (x.defs() | x.uses()) & set(d)
+            if touched:
+                break                        # the slot is read / written inside the web
+            dd = x.defs() & set(mp)
+            uu = x.uses() & set(mp)
+            if not dd and not uu:
+                continue
+            if dd and (x.load or not x.valu):
+                break
+            web.append(j)
+            for r in dd & need:
+                if not x.masked and r not in x.uses():
+                    need.discard(r)         # a full definition: the web starts here
+            if not need:
+                ok = True
+                break
+        if not ok:
+            continue
+        # rename every operand of the web (all-or-nothing per operand)
+        new_ops = {}
+        for j in web:
+            x = seg[j]
+            ops = list(x.ops)
+            for i in range(len(ops)):
+                t = _rename(ops[i], mp)
+                if t is None:
+                    break
+                ops[i] = t
+            else:
+                new_ops[j] = ops
+                continue
+            break
+        else:
+            for j, ops in new_ops.items():
+                seg[j].ops = ops
+            seg[k] = None
+
+
+def coalesce(lines: List[str], final: bool = True) -> List[str]:
+    """Drop the staging copies of one record's straight-line code.  Segments
+    end at labels and branches (the analysis never crosses them);
+    ``final``: the record's temporaries are dead at its end (true for every
+    record: handlers never pass values in temporaries)."""
+    if not COALESCE:
+        return lines
+    out: List[str] = []
+    seg: List[Optional[_Ins]] = []
+    masked = False
+
+    def flush(last: bool):
+        _forward(seg, last)
+        _backward(seg, last)
+        out.extend(x.text() for x in seg if x is not None)
+        seg.clear()
+
+    for l in lines:
+        t = l.strip()
+        if t.endswith(":") or t.startswith(("s_branch", "s_cbranch", "s_setpc", "s_swappc",
+                                            "s_getpc")):
+            flush(False)
+            out.append(l)
+            continue
+        m, ops, mods = parse(t)
+        if m in ("s_and_saveexec_b64", "s_andn1_saveexec_b64") or \
+                (m.startswith("s_") and ops[:1] == ["exec"] and m != "s_mov_b64"):
+            masked = True
+        elif m == "s_mov_b64" and ops[:1] == ["exec"]:
+            masked = ops[1] == G.PINNED["active"]     # a restore, or the active lanes
+        seg.append(_Ins(m, ops, mods, masked))
+    flush(True)
+    return out
+
+
 _FIELDS: Dict[int, Tuple[int, ...]] = {}
 _SPEC: Dict[tuple, tuple] = {}
 _TAG = "@T@"
@@ -597,6 +822,7 @@ def fields_read(lines: Sequence[str]) -> Tuple[int, ...]:
     if hit is None:
         used = set()
         for l in lines:
+            used.update(int(x) for x in re.findall(r"@F(\d)", l))
             for m in re.finditer(r"s\[?(\d+)(?::(\d+)\])?", l):
                 lo = int(m.group(1))
                 hi = int(m.group(2)) if m.group(2) else lo
@@ -618,7 +844,8 @@ def specialize_cached(name: str, var: int, rec: Sequence[int], tag: str):
         full = [0] * 8
         for k in fields_read(lines):
             full[k] = int(rec[k])
-        hit = specialize(lines, full, _TAG)
+        hot, cold, call = specialize(lines, full, _TAG)
+        hit = (coalesce(hot), cold, call)
         if len(_SPEC) > 200000:
             _SPEC.clear()
         _SPEC[key] = hit
@@ -658,6 +885,34 @@ def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6):
     return rec[:-1], n_masks                     # the last record is the zeroed pad
 
 
+def const_code(var: int, rec, prog) -> List[str]:
+    """CONST with the value known: immediate moves instead of a scalar load
+    of the constant table and its wait."""
+    off = int(rec[G.F_IMM]) // 32
+    limbs = [int(x) for x in prog.consts[off]] if off < prog.consts.shape[0] else None
+    if limbs is None:
+        raise JitUnsupported("CONST outside the program's constants")
+    d = G.FB + int(rec[G.F_D])
+    n = 1 if var & G.V_W32 else 8
+    if var & G.V_W32 and var & G.V_DC:
+        idx = [0]                               # upper limbs already zero
+    else:
+        idx = list(range(8))
+    out = []
+    vals = [limbs[j] if j < n else 0 for j in range(8)]
+    for j in range(0, 8, 2):                    # pairs stay 64-bit aligned
+        if j in idx and j + 1 in idx and vals[j] == 0 and vals[j + 1] == 0:
+            out.append("    v_mov_b64 v[%d:%d], 0" % (d + j, d + j + 1))
+            continue
+        for q in (j, j + 1):
+            if q in idx:
+                out.append("    v_mov_b32 v%d, %s" % (d + q, _inline(vals[q]) or "0x%x" % vals[q]))
+    if var & G.V_ROOT:
+        out.append("    v_and_b32 %s, %s, %s" % (G.PINNED["root"], _inline(limbs[0]) or
+                                                   "0x%x" % limbs[0], G.PINNED["root"]))
+    return out
+
+
 def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
                 tag: Optional[str] = None) -> List[str]:
     """Straight-line gfx950 code of one program, entered at label
@@ -669,7 +924,10 @@ def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
     flush_no = 0
     for i, r in enumerate(recs):
         name, var = decode(r[0])
-        hot, cold, _ = specialize_cached(name, var, r, "%s_%d" % (tag, i))
+        if name == "CONST":
+            hot, cold = const_code(var, r, prog), []
+        else:
+            hot, cold, _ = specialize_cached(name, var, r, "%s_%d" % (tag, i))
         out.extend(hot)
         pending_cold.extend(cold)
         if name == "HALT" or (pending_cold and (i + 1) % COLD_FLUSH == 0):
