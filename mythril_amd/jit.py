@@ -945,13 +945,22 @@ def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
     return peephole(out)
 
 
+_WIDE_STORE = re.compile(r"(scratch|global|flat|buffer)_store_dwordx[34]\b")
+
+
 def peephole(lines: List[str]) -> List[str]:
     """Drop ``s_waitcnt lgkmcnt(0)`` where no LDS / scalar-memory operation
     was issued since the last one on the straight path (a label or a call
-    counts as possibly pending)."""
+    counts as possibly pending), and keep one wait state between a vector-
+    memory store of more than 64 bits and a following VALU instruction (the
+    store reads its data VGPRs after issue: a VALU write to them in the next
+    cycle would corrupt the stored data — the interpreter's dispatch gave
+    that slack for free; straight-line code must ask for it)."""
     out, pending = [], True
-    for l in lines:
+    for n, l in enumerate(lines):
         t = l.strip()
+        if out and _WIDE_STORE.match(out[-1].strip()) and t.startswith("v_"):
+            out.append("    s_nop 0")
         if t.endswith(":") or t.startswith(("s_load", "ds_", "s_swappc")):
             pending = True
         elif t == "s_waitcnt lgkmcnt(0)":
