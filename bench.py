@@ -203,9 +203,15 @@ def main():
     ap.add_argument("--shard", choices=("assign", "corpus"), default="assign",
                     help="assignment axis (default, C2) or corpus axis (C5)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    ap.add_argument("--jit", action="store_true",
-                    help="compiled programs (mythril_amd/jit.py) instead of record dispatch")
+    ap.add_argument("--interp", action="store_true",
+                    help="record dispatch through the assembly interpreter instead of the "
+                         "compiled programs (mythril_amd/jit.py, the default)")
+    ap.add_argument("--jit", action="store_true", help=argparse.SUPPRESS)  # the default
+    ap.add_argument("--jit-build-only", action="store_true",
+                    help="compile the corpus and its code object into $MYTHGPU_JIT_CACHE and "
+                         "exit (no GPU): profiling runs then load it")
     args = ap.parse_args()
+    args.jit = not args.interp
     if args.dags is None:
         args.dags = 4096 if args.workload == "c2" else STREAM_QUERIES
 
@@ -220,12 +226,19 @@ def main():
     corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world, args.workload),
                           args.workload)
     t_compile = time.time() - t0
-    image, t_jit = None, 0.0
+    image, t_jit, jit_cached = None, 0.0, False
     if args.jit:                      # code generation + assembly, still before the GPU
         from mythril_amd import jit
         t0 = time.time()
-        image = jit.compile_batch([(p, None, d) for d, p, _, _ in corpus], workers=workers)
+        ids = [d for d, _, _, _ in corpus]
+        image, jit_cached = jit.cached_image(
+            "%s_%d_%d_%d_%d" % (args.workload, len(ids), ids[0], ids[-1], sum(ids)),
+            lambda: jit.compile_batch([(p, None, d) for d, p, _, _ in corpus], workers=workers))
         t_jit = time.time() - t0
+    if args.jit_build_only:
+        print("jit image %.1f MB in %.1f s (cached: %s)" % (len(image or b"") / 1e6, t_jit,
+                                                          jit_cached), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -334,7 +347,9 @@ def main():
             "kernel_key": key,
             "sat_dags": sat_dags,
             "compile_s": round(t_compile, 2),
+            "path": "compiled programs (mythril_amd/jit.py)" if args.jit else "interpreter",
             "jit_s": round(t_jit, 2) if args.jit else None,
+            "jit_cached": jit_cached if args.jit else None,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(corpus, workload=args.workload)

@@ -1015,6 +1015,45 @@ def _chunk_job(args):
     return obj
 
 
+def source_digest() -> str:
+    """Digest of everything a compiled image depends on: the Python compiler
+    and generator sources and the C++ translator (the records)."""
+    import hashlib
+    h = hashlib.sha1(ARCH.encode())
+    pkg = os.path.dirname(os.path.abspath(__file__))
+    for sub in ("", "smt", "csrc"):
+        d = os.path.join(pkg, sub)
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".py", ".cpp", ".h")):
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(f.encode() + fh.read())
+    h.update(("coalesce=%d flush=%d" % (COALESCE, COLD_FLUSH)).encode())
+    return h.hexdigest()[:16]
+
+
+def cached_image(key: str, build) -> Tuple[bytes, bool]:
+    """(image, was_cached): ``build()``'s code object, memoised in
+    ``$MYTHGPU_JIT_CACHE/<key>.hsaco`` when that variable names a directory
+    (profiling runs: the image is assembled in a separate step, so a process
+    the profiler has already attached to the GPU never starts the assembler).
+    ``key`` must identify the programs (workload, ids); the source digest is
+    added here."""
+    d = os.environ.get("MYTHGPU_JIT_CACHE")
+    if not d:
+        return build(), False
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, "%s_%s.hsaco" % (re.sub(r"[^\w.-]", "_", key), source_digest()))
+    if os.path.exists(path):
+        with open(path, "rb") as fh:
+            return fh.read(), True
+    image = build()
+    tmp = path + ".tmp%d" % os.getpid()
+    with open(tmp, "wb") as fh:
+        fh.write(image)
+    os.replace(tmp, path)
+    return image, False
+
+
 def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
                   start: str = "fork") -> bytes:
     """gfx950 code object of [(program, leafgen or None (= the C2 default),
@@ -1023,6 +1062,8 @@ def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
     assembled on ``workers`` host processes (``start="fork"`` before the
     process touches the GPU, ``"spawn"`` after), then linked with the table
     into one shared object."""
+    if workers > 1:                   # enough chunks to keep every worker busy
+        chunk = max(1, min(chunk, -(-len(items) // (4 * workers))))
     with tempfile.TemporaryDirectory() as d:
         jobs = [(list(items[i:i + chunk]), i, lds_slots, os.path.join(d, "c%d.o" % i))
                 for i in range(0, len(items), chunk)]
