@@ -914,9 +914,11 @@ def const_code(var: int, rec, prog) -> List[str]:
 
 
 def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
-                tag: Optional[str] = None) -> List[str]:
+                tag: Optional[str] = None, marks: bool = False) -> List[str]:
     """Straight-line gfx950 code of one program, entered at label
-    ``entry`` (a local ``.L`` label, or a symbol the caller declares)."""
+    ``entry`` (a local ``.L`` label, or a symbol the caller declares).
+    ``marks``: a label ``.Lmark_<record>_<family>_<variant>`` ahead of each
+    record's code (profiling in the simulator, tools/jit_profile.py)."""
     recs, _ = program_records(prog, leafgen, prog_seed, lds_slots)
     tag = tag or entry.lstrip(".L")
     out = [entry + ":"]
@@ -924,6 +926,8 @@ def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
     flush_no = 0
     for i, r in enumerate(recs):
         name, var = decode(r[0])
+        if marks:
+            out.append(".Lmark_%d_%s_%d:" % (i, name, var))
         if name == "CONST":
             hot, cold = const_code(var, r, prog), []
         else:

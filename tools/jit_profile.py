@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Dynamic instruction counts of compiled programs per IR family, from the
+instruction-level simulator (tests/asm_sim.py) running corpus DAGs in
+generator mode: VALU / SALU / other per record of each family, so the JIT's
+remaining overhead can be located without a GPU.
+usage: tools/jit_profile.py [dag ids...]"""
+import bisect
+import collections
+import functools
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+import asm_sim  # noqa: E402
+from mythril_amd import jit  # noqa: E402
+from mythril_amd.corpus import make_dag  # noqa: E402
+from mythril_amd.engine import default_leafgen  # noqa: E402
+from mythril_amd.ir import compile_constraints  # noqa: E402
+
+SEED = 0x6D797468
+jit.program_asm = functools.partial(jit.program_asm, marks=True)
+CNT = collections.defaultdict(collections.Counter)
+OPS = collections.defaultdict(collections.Counter)
+NREC = collections.Counter()
+_step = asm_sim.Wave.step
+
+
+def kind(op):
+    if op.startswith("v_"):
+        return "valu"
+    if op.startswith(("s_waitcnt", "s_nop")):
+        return "wait"
+    if op.startswith(("s_branch", "s_cbranch", "s_setpc", "s_swappc", "s_getpc")):
+        return "branch"
+    if op.startswith("s_load"):
+        return "smem"
+    if op.startswith("s_"):
+        return "salu"
+    return "vmem/lds"
+
+
+def step(self, op, a, pc):
+    if not hasattr(self, "_marks"):
+        ms = sorted((i, l) for l, i in self.labels.items() if l.startswith((".Lmark_", ".Lbody_", ".Ljp0")))
+        self._marks = ([i for i, _ in ms], [l for _, l in ms])
+    idx, labs = self._marks
+    k = bisect.bisect_right(idx, pc) - 1
+    lab = labs[k] if k >= 0 else "interp"
+    if lab.startswith(".Lmark_"):
+        fam = lab.split("_")[2]
+    elif lab.startswith(".Lbody_"):
+        fam = "body_" + lab.split("_")[1]
+    else:
+        fam = "entry"
+    if pc < idx[0] if idx else True:
+        fam = "interp"
+    CNT[fam][kind(op)] += 1
+    OPS[fam][op] += 1
+    return _step(self, op, a, pc)
+
+
+asm_sim.Wave.step = step
+dags = [int(x) for x in sys.argv[1:]] or [0, 1, 2, 3, 5, 8]
+for d in dags:
+    roots, _ = make_dag(d, SEED)
+    prog = compile_constraints(roots)
+    for name, n in prog.stats["hist"].items():
+        NREC[name] += n
+    asm_sim.simulate(prog, gen=(SEED, d, 4096, default_leafgen(prog)), jit=True)
+tot = collections.Counter()
+for c in CNT.values():
+    tot.update(c)
+T = sum(NREC.values())
+print("IR records %d; per record: %s" % (T, {k: round(v / T, 2) for k, v in tot.most_common()}))
+for fam in sorted(CNT, key=lambda f: -sum(CNT[f].values())):
+    c = CNT[fam]
+    print("%-12s n %5d  all/IR %5.2f  %s" % (fam, NREC.get(fam, 0), sum(c.values()) / T,
+                                            {k: round(v / T, 2) for k, v in c.most_common()}))
+    top = [(o, round(v / T, 2)) for o, v in OPS[fam].most_common(8) if not o.startswith("v_")]
+    print("             scalar/other top: %s" % top)
