@@ -83,11 +83,16 @@ def build_corpus(n_dags, workers, dag_ids=None, workload="c2", start="fork"):
 
 def kernel_key(lib_digest, workload, dags, assign_log2, jit):
     """What a traffic measurement (profiles/traffic.json) is valid for: the
-    generated assembly, the allocator's leaf policy, the code path and the
+    generated assembly, the allocator's leaf policy, the code path (and for
+    compiled programs the digest of the sources that generate them) and the
     workload.  bench.py reports ``traffic`` only when every field matches."""
     from mythril_amd import ir
-    return {"asm_digest": lib_digest, "leaf_remat": ir.LEAF_REMAT, "jit": bool(jit),
-            "workload": workload, "dags": dags, "assign_log2": assign_log2}
+    key = {"asm_digest": lib_digest, "leaf_remat": ir.LEAF_REMAT, "jit": bool(jit),
+           "workload": workload, "dags": dags, "assign_log2": assign_log2}
+    if jit:                           # the compiled programs' own code
+        from mythril_amd import jit as J
+        key["jit_code"] = J.code_digest()
+    return key
 
 
 def my_dags(mode, n_dags, rank, world, workload="c2"):

@@ -137,10 +137,13 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_
 /* Compiled programs (batch path without interpretive dispatch; built on the
  * host by mythril_amd/jit.py): ``image`` is a gfx950 code object holding the
  * straight-line code of programs[0..n_progs) and their entry table
- * ``mg_jit_table``.  Attaching points each program's descriptor at its
- * code; evaluations of those programs — and batches created afterwards —
- * then run the code instead of dispatching records (same results, same
- * kernel).  Same role as mg_load_program for Optimize.add (solver.py:28-37),
+ * ``mg_jit_table`` (row i: entry offset from the table, fingerprint of the
+ * records program i was compiled from).  Attaching points each program's
+ * descriptor at its code; evaluations of those programs — and batches
+ * created afterwards — then run the code instead of dispatching records
+ * (same results, same kernel).  MG_E_ARG when a row's fingerprint is not the
+ * loaded program's (code compiled for other records is never entered).
+ * Same role as mg_load_program for Optimize.add (solver.py:28-37),
  * specialised for the batched evaluation (laser/smt/model.py:44-59). */
 int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const void* image,
                   size_t image_size, mg_jit** out);

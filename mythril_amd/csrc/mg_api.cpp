@@ -70,7 +70,23 @@ struct mg_prog {
     void* d_blob = nullptr;         // code | consts | gen | desc | xcode
     mg_pdesc* d_desc = nullptr;
     uint32_t n_ins = 0, n_consts = 0, n_leaves = 0, n_lds = 0, n_probes = 0;
+    uint64_t rec_fp = 0;            // records' fingerprint (rec_fingerprint)
 };
+
+// Fingerprint of a program's uploaded records: sum of the operand words
+// (words 1..7 of each record; word 0 is this library's handler offset) times
+// successive powers of 0x100000001B3 mod 2^64, plus the record count
+// (mythril_amd/jit.py records_fingerprint).  A compiled-program image carries
+// it per entry, so mg_jit_attach refuses code built for other records.
+static uint64_t rec_fingerprint(const std::vector<uint32_t>& rec) {
+    uint64_t h = 0, p = 1;
+    for (size_t r = 0; r + 8 <= rec.size(); r += 8)
+        for (int k = 1; k < 8; ++k) {
+            p *= 0x100000001B3ull;
+            h += (uint64_t)rec[r + k] * p;
+        }
+    return h + rec.size() / 8;
+}
 
 static uint32_t kernel_lds_slots(const mg_ctx* ctx, uint32_t n_lds) {
     return n_lds < ctx->lds_slots ? n_lds : ctx->lds_slots;
@@ -316,6 +332,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
             rec[r + 7] = g.pct_uniform | g.pct_small << 8 | g.pct_boundary << 16;
         }
     }
+    const uint64_t rec_fp = rec_fingerprint(rec);
     // 8 zeroed NOPs after the IR code: the C++ interpreter prefetches ahead
     const size_t code_b = (size_t)(n_ins + 8) * 16, const_b = (size_t)n_const_all * 32,
                  gen_b = gdev.size() * sizeof(mg_leafgen_dev), rec_b = rec.size() * 4;
@@ -357,6 +374,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     }
     mg_prog* p = new mg_prog();
     p->ctx = ctx;
+    p->rec_fp = rec_fp;
     p->d_blob = d;
     p->d_desc = (mg_pdesc*)(db + off_desc);
     p->n_ins = n_ins;
@@ -650,10 +668,11 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
     hipDeviceptr_t d_table = nullptr;
     size_t table_b = 0;
     hipError_t e = hipModuleGetGlobal(&d_table, &table_b, mod, "mg_jit_table");
-    std::vector<int64_t> rel(n_progs);
-    if (e == hipSuccess && table_b != (size_t)n_progs * 8) e = hipErrorInvalidValue;
+    // rows: (entry - table, records' fingerprint)
+    std::vector<int64_t> row(2 * (size_t)n_progs);
+    if (e == hipSuccess && table_b != (size_t)n_progs * 16) e = hipErrorInvalidValue;
     if (e == hipSuccess && n_progs)
-        e = hipMemcpy(rel.data(), d_table, table_b, hipMemcpyDeviceToHost);
+        e = hipMemcpy(row.data(), d_table, table_b, hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
         (void)hipModuleUnload(mod);
         return fail(ctx, MG_E_HIP, "JIT image: %s (table %zu bytes for %u programs)",
@@ -661,17 +680,25 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
     }
     // (segment alignment can place the table past the file size; the bound
     // only guards against garbage)
-    for (uint32_t i = 0; i < n_progs; ++i)
-        if (rel[i] >= 0 || -rel[i] > 2 * (int64_t)image_size + (1 << 20) || (rel[i] & 3)) {
+    for (uint32_t i = 0; i < n_progs; ++i) {
+        const int64_t rel = row[2 * i];
+        if (rel >= 0 || -rel > 2 * (int64_t)image_size + (1 << 20) || (rel & 3)) {
             (void)hipModuleUnload(mod);
             return fail(ctx, MG_E_ARG, "JIT image: entry %u at %lld outside the code", i,
-                        (long long)rel[i]);
+                        (long long)rel);
         }
+        if ((uint64_t)row[2 * i + 1] != progs[i]->rec_fp) {
+            (void)hipModuleUnload(mod);
+            return fail(ctx, MG_E_ARG, "JIT image: entry %u was compiled for other records "
+                        "(fingerprint %016llx, loaded program %016llx)", i,
+                        (unsigned long long)row[2 * i + 1], (unsigned long long)progs[i]->rec_fp);
+        }
+    }
     mg_jit* j = new mg_jit();
     j->ctx = ctx;
     j->module = mod;
     for (uint32_t i = 0; i < n_progs; ++i) {
-        const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)rel[i];
+        const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)row[2 * i];
         e = hipMemcpy((uint8_t*)progs[i]->d_desc + offsetof(mg_pdesc, jit_entry), &entry,
                       sizeof entry, hipMemcpyHostToDevice);
         if (e != hipSuccess) {

@@ -863,7 +863,24 @@ def decode(h: int) -> Tuple[str, int]:
     return G.AOPS[c // (2 * G.NVAR)], (c // 2) % G.NVAR
 
 
-def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6):
+FP_MUL = 0x100000001B3
+
+
+def records_fingerprint(rec) -> int:
+    """Fingerprint of a program's records as mg_load_program uploads them
+    (zeroed pad record included): sum of the operand words (words 1..7 of
+    every record; word 0 is the library's handler offset) times successive
+    powers of FP_MUL, mod 2^64, plus the record count.  mg_jit_attach refuses
+    an image entry whose fingerprint is not the loaded program's
+    (mg_api.cpp rec_fingerprint)."""
+    w = np.ascontiguousarray(np.asarray(rec, dtype=np.uint64).reshape(-1, 8)[:, 1:]).reshape(-1)
+    with np.errstate(over="ignore"):
+        pw = np.cumprod(np.full(w.size, FP_MUL, dtype=np.uint64), dtype=np.uint64)
+        h = int(np.sum(w * pw, dtype=np.uint64))
+    return (h + len(w) // 7) & ((1 << 64) - 1)
+
+
+def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6, full: bool = False):
     """The records ``mg_load_program`` uploads for ``prog`` (handler ids in
     word 0; LEAFD records patched with their leaf's generator parameters
     exactly as mg_load_program does), and the translator's mask count."""
@@ -882,6 +899,8 @@ def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6):
             r[2], r[3] = salt & M32, salt >> 32
             r[5] = g.pool_n
             r[7] = g.pct_uniform | g.pct_small << 8 | g.pct_boundary << 16
+    if full:
+        return rec, n_masks
     return rec[:-1], n_masks                     # the last record is the zeroed pad
 
 
@@ -914,12 +933,17 @@ def const_code(var: int, rec, prog) -> List[str]:
 
 
 def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
-                tag: Optional[str] = None, marks: bool = False) -> List[str]:
+                tag: Optional[str] = None, marks: bool = False,
+                fps: Optional[List[int]] = None) -> List[str]:
     """Straight-line gfx950 code of one program, entered at label
     ``entry`` (a local ``.L`` label, or a symbol the caller declares).
     ``marks``: a label ``.Lmark_<record>_<family>_<variant>`` ahead of each
-    record's code (profiling in the simulator, tools/jit_profile.py)."""
-    recs, _ = program_records(prog, leafgen, prog_seed, lds_slots)
+    record's code (profiling in the simulator, tools/jit_profile.py).
+    ``fps``: the records' fingerprint is appended to it."""
+    full, _ = program_records(prog, leafgen, prog_seed, lds_slots, full=True)
+    recs = full[:-1]                             # the last record is the zeroed pad
+    if fps is not None:
+        fps.append(records_fingerprint(full))
     tag = tag or entry.lstrip(".L")
     out = [entry + ":"]
     pending_cold: List[str] = []
@@ -978,28 +1002,32 @@ def peephole(lines: List[str]) -> List[str]:
 HEADER = '\t.amdgcn_target "amdgcn-amd-amdhsa--%s"\n' % ARCH
 
 
-def chunk_asm(items, first: int, lds_slots: int = 6) -> str:
+def chunk_asm(items, first: int, lds_slots: int = 6, fps: Optional[List[int]] = None) -> str:
     """One object's worth of programs: program ``first + i`` is entered at
     the (hidden) symbol ``mg_jp<first+i>``; the shared heavy bodies are
-    copied into every chunk (local labels, a few KiB)."""
+    copied into every chunk (local labels, a few KiB).  The programs' record
+    fingerprints are appended to ``fps``."""
     parts = [HEADER, "\t.text\n\t.p2align 8\n"]
     for i, (p, g, s) in enumerate(items):
         sym = "mg_jp%d" % (first + i)
         parts.append("\t.globl %s\n\t.hidden %s\n" % (sym, sym))
-        parts.append("\n".join(program_asm(p, g, s, sym, lds_slots, tag="p%d" % (first + i))))
+        parts.append("\n".join(program_asm(p, g, s, sym, lds_slots, tag="p%d" % (first + i),
+                                            fps=fps)))
         parts.append("\n")
     parts.append("\t.p2align 6\n" + "\n".join(bodies()) + "\n")
     return "".join(parts)
 
 
-def table_asm(n: int) -> str:
-    """The stub kernel and ``mg_jit_table``: entry i = mg_jp<i> - table."""
+def table_asm(fps: Sequence[int]) -> str:
+    """The stub kernel and ``mg_jit_table``: row i = (mg_jp<i> - table,
+    fingerprint of program i's records)."""
     stub = open(STUB).read()
     cut = stub.index("\t.ident")
-    rows = "".join("\t.quad mg_jp%d - . + %d\n" % (i, 8 * i) for i in range(n))
+    rows = "".join("\t.quad mg_jp%d - . + %d\n\t.quad 0x%x\n" % (i, 16 * i, fp)
+                   for i, fp in enumerate(fps))
     return (stub[:cut] + "\t.data\n\t.globl mg_jit_table\n\t.protected mg_jit_table\n"
             "\t.type mg_jit_table,@object\n\t.p2align 3\nmg_jit_table:\n" + rows +
-            "\t.size mg_jit_table, %d\n" % (8 * n) + stub[cut:])
+            "\t.size mg_jit_table, %d\n" % (16 * len(fps)) + stub[cut:])
 
 
 def _as(text: str, obj: str) -> None:
@@ -1015,8 +1043,9 @@ def _chunk_job(args):
     if any(g is None for _, g, _ in items):
         from .engine import default_leafgen
         items = [(p, default_leafgen(p) if g is None else g, s) for p, g, s in items]
-    _as(chunk_asm(items, first, lds_slots), obj)
-    return obj
+    fps: List[int] = []
+    _as(chunk_asm(items, first, lds_slots, fps), obj)
+    return obj, fps
 
 
 def source_digest() -> str:
@@ -1032,6 +1061,23 @@ def source_digest() -> str:
                 with open(os.path.join(d, f), "rb") as fh:
                     h.update(f.encode() + fh.read())
     h.update(("coalesce=%d flush=%d" % (COALESCE, COLD_FLUSH)).encode())
+    return h.hexdigest()[:16]
+
+
+CODE_FILES = ("jit.py", "asmgen.py", "ir.py", "irdefs.py", "corpus.py", "engine.py",
+              "csrc/mg_host.cpp", "csrc/mg_api.cpp")
+
+
+def code_digest() -> str:
+    """Digest of the sources that decide a bench program's compiled code
+    (generator, specialiser, compiler, corpus, translator): bench.py keys
+    traffic measurements on it (profiles/traffic.json)."""
+    import hashlib
+    h = hashlib.sha1(ARCH.encode())
+    pkg = os.path.dirname(os.path.abspath(__file__))
+    for f in CODE_FILES:
+        with open(os.path.join(pkg, f), "rb") as fh:
+            h.update(f.encode() + fh.read())
     return h.hexdigest()[:16]
 
 
@@ -1077,8 +1123,10 @@ def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
                 objs = pool.map(_chunk_job, jobs, chunksize=1)
         else:
             objs = [_chunk_job(j) for j in jobs]
+        fps = [fp for _, f in objs for fp in f]
+        objs = [o for o, _ in objs]
         tab = os.path.join(d, "table.o")
-        _as(table_asm(len(items)), tab)
+        _as(table_asm(fps), tab)
         out = os.path.join(d, "jit.hsaco")
         subprocess.run([os.path.join(LLVM_BIN, "ld.lld"), "-shared", tab] + objs + ["-o", out],
                        check=True)

@@ -356,6 +356,24 @@ def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
     return sorted(out)
 
 
+_SYMS: "Dict[int, frozenset]" = {}
+_SYMS_SIZE = 1 << 16
+
+
+def _symbols(c: N.Node) -> frozenset:
+    """Free symbols under one constraint, memoised by node id (nodes are
+    immutable and ids never reused: LASER re-asks the same path constraints
+    on every JUMPI, so a stream walks each constraint once)."""
+    hit = _SYMS.get(c.id)
+    if hit is None:
+        hit = frozenset((n.op == "var", n.params[0]) for n in N.topo_order([c])
+                        if n.op in ("var", "array", "apply"))
+        if len(_SYMS) >= _SYMS_SIZE:
+            _SYMS.clear()
+        _SYMS[c.id] = hit
+    return hit
+
+
 def dependence_buckets(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
     """Split constraints into groups that share no free symbol — the
     ``DependenceMap`` of ``IndependenceSolver``
@@ -372,13 +390,8 @@ def dependence_buckets(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
             k = parent[k]
         return k
 
-    syms_of = []
     for i, c in enumerate(nodes):
-        syms = set()
-        for n in N.topo_order([c]):
-            if n.op in ("var", "array", "apply"):
-                syms.add((n.op == "var", n.params[0]))
-        syms_of.append(syms)
+        syms = _symbols(c)
         parent.setdefault(("c", i), ("c", i))
         for sym in syms:
             parent.setdefault(sym, sym)

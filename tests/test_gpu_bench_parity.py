@@ -133,3 +133,22 @@ def test_bench_handler_variants_all_checked(units):
     fams = sorted({f for f, _ in bench_set})
     print("bench configurations execute %d (family, variant) handlers in %d families"
           % (len(bench_set), len(fams)))
+
+
+def test_jit_attach_refuses_code_compiled_for_other_records(engine):
+    """mg_jit_attach compares each table row's record fingerprint with the
+    loaded program's: an image compiled for another program (or another
+    allocation of the same DAG) is refused, never entered."""
+    from mythril_amd import jit
+    from mythril_amd.engine import EngineError
+    d1, p1, _, _ = bench.compile_unit(("c2", 1))
+    d2, p2, _, _ = bench.compile_unit(("c2", 2))
+    image = jit.compile_batch([(p1, None, d1)])
+    lp2 = engine.load(p2, default_leafgen(p2), prog_seed=d2)
+    with pytest.raises(EngineError, match="other records"):
+        engine.jit_attach([lp2], image)
+    lp1 = engine.load(p1, default_leafgen(p1), prog_seed=d1 + 1)     # another salt
+    with pytest.raises(EngineError, match="other records"):
+        engine.jit_attach([lp1], image)
+    lp1 = engine.load(p1, default_leafgen(p1), prog_seed=d1)
+    engine.jit_detach(engine.jit_attach([lp1], image))

@@ -76,9 +76,29 @@ def test_jit_text_has_no_scalar_stores_and_fits_the_register_budget():
                                                                   ".Ljp1"))
 
 
+def test_records_fingerprint_matches_the_c_definition():
+    """records_fingerprint (numpy, wrapping uint64) against a plain restatement
+    of mg_api.cpp's rec_fingerprint loop."""
+    rng = np.random.default_rng(5)
+    rec = rng.integers(0, 1 << 32, size=8 * 37, dtype=np.uint64)
+    h, p = 0, 1
+    for r in range(0, len(rec), 8):
+        for k in range(1, 8):
+            p = p * 0x100000001B3 % (1 << 64)
+            h = (h + int(rec[r + k]) * p) % (1 << 64)
+    assert jit.records_fingerprint(rec) == (h + 37) % (1 << 64)
+    rec2 = rec.copy()
+    rec2[8 * 5 + 3] ^= 1
+    assert jit.records_fingerprint(rec2) != jit.records_fingerprint(rec)
+    rec2 = rec.copy()
+    rec2[8 * 5] ^= 1                          # word 0 (handler offset) is not hashed
+    assert jit.records_fingerprint(rec2) == jit.records_fingerprint(rec)
+
+
 def test_jit_image_entries_point_at_each_program():
     """compile_batch links chunk objects and the table: entry i (relative
-    to mg_jit_table) is the first instruction of program i."""
+    to mg_jit_table) is the first instruction of program i, and its
+    fingerprint is that of program i's records."""
     items = []
     for d in (1, 2, 3, 4, 5):
         roots, _ = make_dag(d, SEED)
@@ -89,7 +109,7 @@ def test_jit_image_entries_point_at_each_program():
         fh.write(image)
     syms = subprocess.run([jit.LLVM_BIN + "/llvm-readelf", "-s", "/tmp/_mg_jit_test.hsaco"],
                           capture_output=True, text=True, check=True).stdout
-    tab = int(re.search(r"([0-9a-f]+)\s+40 OBJECT\s+GLOBAL\s+\w+\s+\d+ mg_jit_table", syms).group(1), 16)
+    tab = int(re.search(r"([0-9a-f]+)\s+80 OBJECT\s+GLOBAL\s+\w+\s+\d+ mg_jit_table", syms).group(1), 16)
     data = subprocess.run([jit.LLVM_BIN + "/llvm-objdump", "-s", "-j", ".data",
                            "/tmp/_mg_jit_test.hsaco"], capture_output=True, text=True,
                           check=True).stdout
@@ -108,9 +128,12 @@ def test_jit_image_entries_point_at_each_program():
         if m:
             at[int(m.group(2), 16)] = m.group(1)
     for i, (p, g, s) in enumerate(items):
-        rel = words[tab + 8 * i] | words[tab + 8 * i + 4] << 32
+        rel = words[tab + 16 * i] | words[tab + 16 * i + 4] << 32
         rel -= 1 << 64 if rel >> 63 else 0
         assert rel < 0
+        fp = words[tab + 16 * i + 8] | words[tab + 16 * i + 12] << 32
+        full, _ = jit.program_records(p, g, s, full=True)
+        assert fp == jit.records_fingerprint(full)
         text = jit.program_asm(p, g, s, "x", tag="p%d" % i)
         first = next(l.split()[0] for l in text[1:] if l.strip() and not l.strip().endswith(":"))
         assert at[tab + rel].startswith(first), (i, at[tab + rel], first)
