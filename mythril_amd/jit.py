@@ -33,6 +33,7 @@ parity tests as the interpreter (tests/test_gpu_bench_parity.py).
 
 from __future__ import annotations
 
+import functools
 import os
 import re
 import subprocess
@@ -147,11 +148,16 @@ def _tokens(rest: str) -> Tuple[List[str], List[str]]:
     return ops, mods
 
 
-def parse(line: str):
-    t = line.strip()
+@functools.lru_cache(maxsize=1 << 18)
+def _parse_cached(t: str):
     parts = t.split(None, 1)
     ops, mods = _tokens(parts[1]) if len(parts) > 1 else ([], [])
-    return parts[0], ops, mods
+    return parts[0], tuple(ops), tuple(mods)
+
+
+def parse(line: str):
+    m, ops, mods = _parse_cached(line.strip())
+    return m, list(ops), list(mods)
 
 
 def render(m: str, ops: Sequence[str], mods: Sequence[str] = ()) -> str:
@@ -169,6 +175,7 @@ _SREG = re.compile(r"s(\d+)$")
 _SPAIR = re.compile(r"s\[(\d+):(\d+)\]$")
 
 
+@functools.lru_cache(maxsize=1 << 16)
 def vreg(tok: str) -> Optional[Tuple[int, int]]:
     m = _VREG.match(tok)
     if m:
@@ -179,6 +186,7 @@ def vreg(tok: str) -> Optional[Tuple[int, int]]:
     return None
 
 
+@functools.lru_cache(maxsize=1 << 16)
 def sreg(tok: str) -> Optional[Tuple[int, int]]:
     m = _SREG.match(tok)
     if m:
@@ -206,6 +214,7 @@ def int_value(tok: str) -> Optional[int]:
         return None
 
 
+@functools.lru_cache(maxsize=4096)
 def n_dest(m: str) -> int:
     if m.startswith("v_cmp"):
         return 1
@@ -600,9 +609,14 @@ TEMPS = frozenset(list(range(G.XB, G.XB + 8)) + list(range(G.YB, G.TB + G.NT)))
 COALESCE = os.environ.get("MYTHGPU_JIT_COALESCE", "1") != "0"
 
 
-def _vregs(tok: str) -> List[int]:
+@functools.lru_cache(maxsize=1 << 16)
+def _vregs_t(tok: str) -> Tuple[int, ...]:
     r = vreg(tok)
-    return list(range(r[0], r[0] + r[1])) if r else []
+    return tuple(range(r[0], r[0] + r[1])) if r else ()
+
+
+def _vregs(tok: str) -> List[int]:
+    return list(_vregs_t(tok))
 
 
 class _Ins:
@@ -616,19 +630,25 @@ class _Ins:
         self.valu = m.startswith("v_")
 
     def def_ops(self):
-        return [i for i in range(self.nd) if vreg(self.ops[i])]
+        return [i for i in range(self.nd) if _vregs_t(self.ops[i])]
 
     def use_ops(self):
-        return [i for i in range(self.nd, len(self.ops)) if vreg(self.ops[i])]
+        return [i for i in range(self.nd, len(self.ops)) if _vregs_t(self.ops[i])]
 
     def defs(self):
-        return {r for i in self.def_ops() for r in _vregs(self.ops[i])}
+        out = set()
+        for i in range(self.nd):
+            out.update(_vregs_t(self.ops[i]))
+        return out
 
     def uses(self):
-        u = {r for i in self.use_ops() for r in _vregs(self.ops[i])}
+        out = set()
+        for i in range(self.nd, len(self.ops)):
+            out.update(_vregs_t(self.ops[i]))
         if self.masked:                 # inactive lanes keep the old value
-            u |= self.defs()
-        return u
+            for i in range(self.nd):
+                out.update(_vregs_t(self.ops[i]))
+        return out
 
     def text(self):
         return render(self.m, self.ops, self.mods)
@@ -810,6 +830,76 @@ def coalesce(lines: List[str], final: bool = True) -> List[str]:
     return out
 
 
+# coalescing is memoised up to a relabelling of register-file slots: records
+# that differ only in their slots (most cache misses above) give the same
+# text once every 8-register file block is renamed in order of first use,
+# and coalesce() commutes with such a renaming (aliasing, the SLOTS / TEMPS
+# sets and 64-bit pair alignment are all preserved)
+_COAL: Dict[str, Tuple[str, ...]] = {}
+_VTOK = re.compile(r"(?<![\w.])v(?:(\d+)|\[(\d+):(\d+)\])(?![\w])")
+FILE_LO, FILE_HI = G.FB, G.FB + 8 * G.NREG
+
+
+def _relabel(lines: Sequence[str], blocks: Optional[Dict[int, int]] = None):
+    """(lines with file blocks renamed, mapping used) — blocks: actual ->
+    canonical; built in order of first appearance when None.  None when a
+    register range straddles two blocks (no relabelling then)."""
+    build = blocks is None
+    mp: Dict[int, int] = {} if build else blocks
+    bad = []
+
+    def blk(r):
+        return (r - FILE_LO) >> 3
+
+    def sub(m):
+        if m.group(1) is not None:
+            r = int(m.group(1))
+            if not FILE_LO <= r < FILE_HI:
+                return m.group(0)
+            b = blk(r)
+            if b not in mp:
+                if not build:
+                    bad.append(r)
+                    return m.group(0)
+                mp[b] = len(mp)
+            return "v%d" % (r + 8 * (mp[b] - b))
+        lo, hi = int(m.group(2)), int(m.group(3))
+        if not (FILE_LO <= lo < FILE_HI or FILE_LO <= hi < FILE_HI):
+            return m.group(0)
+        if not (FILE_LO <= lo and hi < FILE_HI) or blk(lo) != blk(hi):
+            bad.append(lo)
+            return m.group(0)
+        b = blk(lo)
+        if b not in mp:
+            if not build:
+                bad.append(lo)
+                return m.group(0)
+            mp[b] = len(mp)
+        d = 8 * (mp[b] - b)
+        return "v[%d:%d]" % (lo + d, hi + d)
+
+    out = [_VTOK.sub(sub, l) if "v" in l else l for l in lines]
+    return (None, None) if bad else (out, mp)
+
+
+def coalesce_cached(hot: List[str]) -> List[str]:
+    """coalesce(hot), memoised on the slot-relabelled text."""
+    canon, mp = _relabel(hot)
+    if canon is None:
+        return coalesce(hot)
+    key = "\n".join(canon)
+    res = _COAL.get(key)
+    if res is None:
+        res = tuple(coalesce(list(canon)))
+        if len(_COAL) > 100000:
+            _COAL.clear()
+        _COAL[key] = res
+    back, _ = _relabel(res, {c: a for a, c in mp.items()})
+    if back is None:                   # (cannot happen: coalesce renames within blocks)
+        return coalesce(hot)
+    return back
+
+
 _FIELDS: Dict[int, Tuple[int, ...]] = {}
 _SPEC: Dict[tuple, tuple] = {}
 _TAG = "@T@"
@@ -845,7 +935,7 @@ def specialize_cached(name: str, var: int, rec: Sequence[int], tag: str):
         for k in fields_read(lines):
             full[k] = int(rec[k])
         hot, cold, call = specialize(lines, full, _TAG)
-        hit = (coalesce(hot), cold, call)
+        hit = (coalesce_cached(hot), cold, call)
         if len(_SPEC) > 200000:
             _SPEC.clear()
         _SPEC[key] = hit

@@ -79,3 +79,33 @@ for fam in sorted(CNT, key=lambda f: -sum(CNT[f].values())):
                                             {k: round(v / T, 2) for k, v in c.most_common()}))
     top = [(o, round(v / T, 2)) for o, v in OPS[fam].most_common(8) if not o.startswith("v_")]
     print("             scalar/other top: %s" % top)
+if os.environ.get("JIT_PROFILE_OP"):
+    op = os.environ["JIT_PROFILE_OP"]
+    print("\n%s per family (per IR record of the sample):" % op)
+    for fam in sorted(OPS, key=lambda f: -OPS[f][op]):
+        if OPS[fam][op]:
+            print("  %-12s %6.2f" % (fam, OPS[fam][op] / T))
+# measured SIMD cycles per wave64 instruction at 3 waves / SIMD
+# (tools/valu_rate.hip, profiles/r03/valu_rate_r3*.log): plain VOP2 add/sub/
+# logic/mov pair waves (2.67), everything else the kernel uses costs ~4
+FAST = ("v_add_u32", "v_sub_u32", "v_subrev_u32", "v_and_b32", "v_or_b32", "v_xor_b32",
+        "v_mov_b32", "v_not_b32")
+
+
+def cycles(op):
+    base = op.replace("_e32", "").replace("_e64", "")
+    if base in FAST:
+        return 2.67
+    return 4.1
+
+
+if os.environ.get("JIT_PROFILE_CYCLES"):
+    cyc = {f: sum(cycles(o) * n for o, n in OPS[f].items() if o.startswith("v_")) for f in OPS}
+    tot_c = sum(v for f, v in cyc.items() if f != "interp")
+    print("\nVALU cycles per IR record by family (3 waves/SIMD rates), total %.1f:" % (tot_c / T))
+    for f in sorted(cyc, key=lambda f: -cyc[f]):
+        if f != "interp" and cyc[f]:
+            top = sorted(((cycles(o) * n, o) for o, n in OPS[f].items() if o.startswith("v_")),
+                         reverse=True)[:5]
+            print("  %-12s %6.2f  %4.1f%%  %s" % (f, cyc[f] / T, 100 * cyc[f] / tot_c,
+                                                 ", ".join("%s %.2f" % (o, c / T) for c, o in top)))
