@@ -1165,12 +1165,18 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     for k in range(3):
         a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(tt[0]), s(S_PAIR + k),
                                                  vp(z[0])))
-    _class_mask(a, S_T + 2, f["pu"], f["ps"], cls)                   # small
+    # class masks from three compares (cls >= each threshold), ranges by
+    # SALU: small = ge_u & ~ge_s, boundary = ge_s & ~ge_b, pool = ge_b
+    ge_s, ge_b = S_X, S_X + 2                   # (division's lane masks: free here)
+    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T + 2), s(f["pu"]), v(cls)))
+    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(ge_s), s(f["ps"]), v(cls)))
+    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(ge_b), s(f["pb"]), v(cls)))
+    a("s_andn2_b64 %s, %s, %s" % (sp(S_T + 2), sp(S_T + 2), sp(ge_s)))   # small
     lab = exec_begin(a, S_T + 2, S_T + 4)
     moves(a, dst[2:], [None] * 6)
     exec_end(a, lab, S_T + 4)
     # ---- boundary: pct_small <= cls < pct_boundary -------------------------
-    _class_mask(a, S_T + 2, f["ps"], f["pb"], cls)
+    a("s_andn2_b64 %s, %s, %s" % (sp(S_T + 2), sp(ge_s), sp(ge_b)))     # boundary
     # (no skip branch: with 64 lanes some lane nearly always is in the class;
     # with exec = 0 the loads access nothing)
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
@@ -1195,9 +1201,8 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
     # the pool is stored as (v-1, v, v+1) triples: entry e * 3 + delta
     a("s_mov_b64 exec, %s" % sp(S_T + 4))
-    _class_mask(a, S_T + 2, f["pb"], None, cls)
     a("s_cmp_lg_u32 %s, 0" % s(f["pn"]))
-    a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(S_T + 2)))
+    a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(ge_b)))             # pool
     a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
     e, delta = tt[0], tt[1]
     a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(f["pn"])))
