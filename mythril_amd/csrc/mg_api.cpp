@@ -682,6 +682,7 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
     // only guards against garbage)
     for (uint32_t i = 0; i < n_progs; ++i) {
         const int64_t rel = row[2 * i];
+        if (rel == 0 && row[2 * i + 1] == 0) continue;     // not compiled: interpreter
         if (rel >= 0 || -rel > 2 * (int64_t)image_size + (1 << 20) || (rel & 3)) {
             (void)hipModuleUnload(mod);
             return fail(ctx, MG_E_ARG, "JIT image: entry %u at %lld outside the code", i,
@@ -698,6 +699,7 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
     j->ctx = ctx;
     j->module = mod;
     for (uint32_t i = 0; i < n_progs; ++i) {
+        if (row[2 * i] == 0) continue;                      // stays on the interpreter
         const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)row[2 * i];
         e = hipMemcpy((uint8_t*)progs[i]->d_desc + offsetof(mg_pdesc, jit_entry), &entry,
                       sizeof entry, hipMemcpyHostToDevice);

@@ -1100,21 +1100,32 @@ def chunk_asm(items, first: int, lds_slots: int = 6, fps: Optional[List[int]] = 
     parts = [HEADER, "\t.text\n\t.p2align 8\n"]
     for i, (p, g, s) in enumerate(items):
         sym = "mg_jp%d" % (first + i)
+        fp: List[int] = []
+        try:
+            text = program_asm(p, g, s, sym, lds_slots, tag="p%d" % (first + i), fps=fp)
+        except JitUnsupported:
+            fp = [None]               # stays on the interpreter: a zero table row
+            text = None
+        if fps is not None:
+            fps.append(fp[0])
+        if text is None:
+            continue
         parts.append("\t.globl %s\n\t.hidden %s\n" % (sym, sym))
-        parts.append("\n".join(program_asm(p, g, s, sym, lds_slots, tag="p%d" % (first + i),
-                                            fps=fps)))
+        parts.append("\n".join(text))
         parts.append("\n")
     parts.append("\t.p2align 6\n" + "\n".join(bodies()) + "\n")
     return "".join(parts)
 
 
-def table_asm(fps: Sequence[int]) -> str:
+def table_asm(fps: Sequence[Optional[int]]) -> str:
     """The stub kernel and ``mg_jit_table``: row i = (mg_jp<i> - table,
-    fingerprint of program i's records)."""
+    fingerprint of program i's records), or (0, 0) for a program that was
+    not compiled (JitUnsupported: mg_jit_attach leaves it on the
+    interpreter)."""
     stub = open(STUB).read()
     cut = stub.index("\t.ident")
-    rows = "".join("\t.quad mg_jp%d - . + %d\n\t.quad 0x%x\n" % (i, 16 * i, fp)
-                   for i, fp in enumerate(fps))
+    rows = "".join(("\t.quad mg_jp%d - . + %d\n\t.quad 0x%x\n" % (i, 16 * i, fp)) if fp is not None
+                   else "\t.quad 0\n\t.quad 0\n" for i, fp in enumerate(fps))
     return (stub[:cut] + "\t.data\n\t.globl mg_jit_table\n\t.protected mg_jit_table\n"
             "\t.type mg_jit_table,@object\n\t.p2align 3\nmg_jit_table:\n" + rows +
             "\t.size mg_jit_table, %d\n" % (16 * len(fps)) + stub[cut:])

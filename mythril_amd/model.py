@@ -105,6 +105,7 @@ class SolverStatistics:
         self.kernel_time = 0.0          # device time of the search launches (HIP events)
         self.memo_misses = 0            # queries answered "miss" by the group-miss memo
         self.gated = 0                  # queries whose compile estimate exceeded the budget
+        self.shape_skipped = 0          # queries of a shape the search keeps missing
         self.fallbacks = 0
         self.unsupported = 0
         self.errors = 0
@@ -113,10 +114,11 @@ class SolverStatistics:
 
     def gpu_report(self) -> str:
         return ("GPU pre-filter: queries: {} hits: {} fallbacks: {} unsupported: {} errors: {} "
-                "rejected by z3: {} memo misses: {} compile-gated: {}\nGPU candidates: {} "
-                "time: {:.3f}s (kernel {:.3f}s; {})").format(
+                "rejected by z3: {} memo misses: {} compile-gated: {} shape-skipped: {}\n"
+                "GPU candidates: {} time: {:.3f}s (kernel {:.3f}s; {})").format(
             self.gpu_queries, self.gpu_hits, self.fallbacks, self.unsupported, self.errors,
-            self.rejected, self.memo_misses, self.gated, self.gpu_candidates, self.gpu_time,
+            self.rejected, self.memo_misses, self.gated, self.shape_skipped, self.gpu_candidates,
+            self.gpu_time,
             self.kernel_time, ", ".join("%s %.3fs" % (k, self.phase[k]) for k in PHASES))
 
     def __repr__(self):
@@ -161,6 +163,11 @@ INS_CAND_PER_S = 3.0e11
 # devices the batched search spreads programs over (corpus axis)
 DEVICES = [0]
 GPU_ENABLED = True
+# adaptive gate (see _shape_gate): after SHAPE_MIN searches of one query
+# shape with a hit rate below SHAPE_FLOOR, only every SHAPE_PROBE-th query of
+# that shape is searched
+SHAPE_GATE = True
+SHAPE_MIN, SHAPE_FLOOR, SHAPE_PROBE = 4, 1.0 / 16, 8
 
 
 def configure_from_env(env=None) -> None:
@@ -169,8 +176,8 @@ def configure_from_env(env=None) -> None:
     ``MYTHRIL_GPU_DEVICES=0,1,...`` the devices batched searches use,
     ``MYTHRIL_GPU_CANDIDATES`` the candidates per query (a power of two),
     ``MYTHRIL_GPU_BUDGET_MS`` the share of a query's timeout the search may
-    take."""
-    global GPU_ENABLED, DEVICES, SEARCH_CANDIDATES, SEARCH_BUDGET_MS
+    take, ``MYTHRIL_GPU_ADAPTIVE=0`` turns the per-shape gate off."""
+    global GPU_ENABLED, DEVICES, SEARCH_CANDIDATES, SEARCH_BUDGET_MS, SHAPE_GATE
     import os
     env = os.environ if env is None else env
     GPU_ENABLED = env.get("MYTHRIL_GPU", "1").strip().lower() not in ("0", "off", "false", "no")
@@ -182,6 +189,8 @@ def configure_from_env(env=None) -> None:
         SEARCH_CANDIDATES = 1 << (n.bit_length() - 1)
     if env.get("MYTHRIL_GPU_BUDGET_MS"):
         SEARCH_BUDGET_MS = max(0.0, float(env["MYTHRIL_GPU_BUDGET_MS"]))
+    SHAPE_GATE = env.get("MYTHRIL_GPU_ADAPTIVE", "1").strip().lower() not in ("0", "off", "false",
+                                                                             "no")
 
 
 configure_from_env()
@@ -552,13 +561,63 @@ def _note_miss(key: frozenset, n_cand: int) -> None:
         _miss_index.setdefault(min(key), []).append(key)
 
 
+# Adaptive gate.  LASER asks the same KIND of question again and again: a
+# module's check at one instruction (an overflow test, an ``ISZERO`` of a
+# selector comparison) is the newest constraint of every query it makes, on
+# every path that reaches the instruction.  Behind SafeMath such checks are
+# unsatisfiable on every path, so searching them only adds compile time to a
+# z3 call that has to happen anyway.  The gate keeps hit / miss counts per
+# shape of the newest constraint (its operator tree to depth 3, leaves by
+# kind); once a shape has been searched SHAPE_MIN times with a hit rate below
+# SHAPE_FLOOR, only every SHAPE_PROBE-th query of it is searched (so a shape
+# that starts to hit is noticed again).  Like the memo it never changes an
+# answer — a skipped query goes to z3, as stock Mythril's does — only where
+# the time goes.
+_shape_stats: "Dict[str, List[int]]" = {}     # shape -> [searches, hits, skipped since probe]
+_SHAPE_DEPTH = 3
+
+
+def query_shape(c: N.Node, depth: int = _SHAPE_DEPTH) -> str:
+    """Operator tree of ``c`` to ``depth`` (numerals as ``k``, other leaves
+    by kind and width): constraints a module builds at one instruction on
+    different paths share it."""
+    if depth == 0 or not c.args:
+        if c.op == "bvnum":
+            return "k%d" % c.width
+        return "%s%d" % (c.op, c.width or 0)
+    return "%s(%s)" % (c.op, ",".join(query_shape(a, depth - 1) for a in c.args))
+
+
+def _shape_gate(shape: str) -> bool:
+    """True when the query should be searched."""
+    if not SHAPE_GATE:
+        return True
+    st = _shape_stats.get(shape)
+    if st is None or st[0] < SHAPE_MIN or st[1] >= SHAPE_FLOOR * st[0]:
+        return True
+    st[2] += 1
+    if st[2] >= SHAPE_PROBE:
+        st[2] = 0
+        return True
+    return False
+
+
+def _shape_note(shape: str, hit: bool) -> None:
+    st = _shape_stats.setdefault(shape, [0, 0, 0])
+    st[0] += 1
+    st[1] += int(hit)
+    if len(_shape_stats) > GROUP_MISS_SIZE:
+        _shape_stats.pop(next(iter(_shape_stats)))
+
+
 def clear_search_memos() -> None:
-    """Forget compiled groups and group misses (tools/search_bench.py's cold
-    runs)."""
+    """Forget compiled groups, group misses and shape statistics
+    (tools/search_bench.py's cold runs)."""
     global _SEARCH_CACHE
     _SEARCH_CACHE = None
     _group_miss.clear()
     _miss_index.clear()
+    _shape_stats.clear()
 
 
 def _compile_estimate_ms(buckets, keys) -> float:
@@ -582,6 +641,10 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     keys = [_group_key(b) for b in buckets]
     if any(_known_miss(k, SEARCH_CANDIDATES) for k in keys):
         stats.memo_misses += 1
+        return None
+    shape = query_shape(nodes[-1]) if nodes else ""
+    if not _shape_gate(shape):
+        stats.shape_skipped += 1
         return None
     if _compile_estimate_ms(buckets, keys) > budget_ms:
         stats.gated += 1
@@ -607,6 +670,7 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     for k, (i, _) in zip(keys, hits):
         if i < 0:
             _note_miss(k, n_cand)
+    _shape_note(shape, all(i >= 0 for i, _ in hits))
     if any(i < 0 for i, _ in hits):
         return None
     return _merge([a for _, a in hits]), progs

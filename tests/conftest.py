@@ -19,3 +19,13 @@ def engine():
     unavailable: a silent fallback would hide a broken native path."""
     from mythril_amd.engine import get_engine
     return get_engine(0)
+
+
+@pytest.fixture(autouse=True)
+def _fresh_shape_statistics():
+    """Each test starts with no per-shape hit statistics (model._shape_gate):
+    a test's expectations must not depend on which queries earlier tests of
+    the session happened to miss."""
+    import mythril_amd.model as M
+    M._shape_stats.clear()
+    yield

@@ -137,3 +137,26 @@ def test_jit_image_entries_point_at_each_program():
         text = jit.program_asm(p, g, s, "x", tag="p%d" % i)
         first = next(l.split()[0] for l in text[1:] if l.strip() and not l.strip().endswith(":"))
         assert at[tab + rel].startswith(first), (i, at[tab + rel], first)
+
+
+def test_unsupported_program_stays_on_the_interpreter(monkeypatch):
+    """A program the specialiser rejects gets a zero table row (mg_jit_attach
+    leaves its descriptor on the interpreter); the others are compiled."""
+    items = []
+    for d in (1, 2, 3):
+        roots, _ = make_dag(d, SEED)
+        p = compile_constraints(roots)
+        items.append((p, default_leafgen(p), d))
+    real = jit.program_asm
+
+    def flaky(p, *a, **k):
+        if p is items[1][0]:
+            raise jit.JitUnsupported("test")
+        return real(p, *a, **k)
+    monkeypatch.setattr(jit, "program_asm", flaky)
+    fps = []
+    text = jit.chunk_asm(items, 0, fps=fps)
+    assert fps[1] is None and fps[0] is not None and fps[2] is not None
+    assert "mg_jp1:" not in text and "mg_jp0:" in text and "mg_jp2:" in text
+    table = jit.table_asm(fps)
+    assert "\t.quad 0\n\t.quad 0\n" in table and "mg_jp1" not in table

@@ -535,3 +535,72 @@ def test_node_witness_verified_by_z3_when_present(monkeypatch, fresh):
     assert M._accept([c], Assignment(vars={"x": 1}), None, 1234) is None
     assert seen["raws"] == [("z3", c.raw.id)] and seen["timeout"] == 1234
     assert M.stats.rejected == before + 1
+
+
+# ---- round 3: adaptive per-shape gate ----------------------------------------
+
+def _miss_query(k):
+    """A fresh group (new symbol) of one fixed shape that the stub never
+    satisfies: x_k * x_k == 3."""
+    x = symbol_factory.BitVecSym("sg%d" % k, 256)
+    return [(x * x == symbol_factory.BitVecVal(3, 256)).raw]
+
+
+def test_shape_gate_skips_a_shape_that_keeps_missing(miss_engine, fresh, reset_engine_memo):
+    log = miss_engine
+    before = M.stats.shape_skipped
+    for k in range(M.SHAPE_MIN):                       # learning: every query searched
+        assert REAL_GPU_SEARCH(_miss_query(k), 200) is None
+    assert len(log) == M.SHAPE_MIN
+    searched = []
+    for k in range(M.SHAPE_MIN, M.SHAPE_MIN + 2 * M.SHAPE_PROBE):
+        n = len(log)
+        assert REAL_GPU_SEARCH(_miss_query(k), 200) is None
+        searched.append(len(log) > n)
+    assert sum(searched) == 2                          # one probe per SHAPE_PROBE queries
+    assert M.stats.shape_skipped == before + 2 * M.SHAPE_PROBE - 2
+    # another shape is unaffected
+    y = symbol_factory.BitVecSym("sgy", 256)
+    n = len(log)
+    REAL_GPU_SEARCH([ULT(y, symbol_factory.BitVecVal(5, 256)).raw], 200)
+    assert len(log) == n + 1
+    # cold runs forget the statistics; the switch turns the gate off
+    M.clear_search_memos()
+    n = len(log)
+    REAL_GPU_SEARCH(_miss_query(999), 200)
+    assert len(log) == n + 1
+
+
+def test_shape_gate_keeps_searching_a_shape_that_hits(monkeypatch, fresh, reset_engine_memo):
+    log = []
+    engines = {0: StreamEngine(0, [5], log)}          # every program satisfied at index 5
+    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "DEVICES", [0])
+    M.clear_search_memos()
+    for k in range(3 * M.SHAPE_MIN):
+        x = symbol_factory.BitVecSym("sh%d" % k, 256)
+        assert REAL_GPU_SEARCH([ULT(x, symbol_factory.BitVecVal(9, 256)).raw], 200) is not None
+    assert len(log) == 3 * M.SHAPE_MIN
+    M.clear_search_memos()
+
+
+def test_shape_gate_switch(miss_engine, fresh, reset_engine_memo, monkeypatch):
+    log = miss_engine
+    M.configure_from_env({"MYTHRIL_GPU_ADAPTIVE": "0"})
+    try:
+        for k in range(M.SHAPE_MIN + M.SHAPE_PROBE):
+            REAL_GPU_SEARCH(_miss_query(500 + k), 200)
+        assert len(log) == M.SHAPE_MIN + M.SHAPE_PROBE
+    finally:
+        M.configure_from_env({})
+
+
+def test_query_shape_abstracts_leaves_not_structure():
+    a, b = symbol_factory.BitVecSym("qa", 256), symbol_factory.BitVecSym("qb", 256)
+    c = symbol_factory.BitVecSym("qc", 8)
+    s1 = M.query_shape(ULT(a + b, a).raw)
+    s2 = M.query_shape(ULT(b + a, b).raw)
+    assert s1 == s2
+    assert M.query_shape(ULT(a * b, a).raw) != s1
+    assert M.query_shape((c == symbol_factory.BitVecVal(1, 8)).raw) != \
+        M.query_shape((a == symbol_factory.BitVecVal(1, 256)).raw)
