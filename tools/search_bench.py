@@ -63,7 +63,7 @@ def reference_sat_queries(engine):
     }
 
 
-def shape_lines(eng, n_queries):
+def shape_lines(eng, n_queries, n_sample=48):
     import mythril_amd.model as M
     from mythril_amd import workloads as W
     from mythril_amd.smt.node import topo_order
@@ -91,23 +91,25 @@ def shape_lines(eng, n_queries):
         needed = sum(n_cand if i < 0 else i + 1 for i, _ in hits)
         ins_cand = sum((n_cand if i < 0 else i + 1) * p.n_ins for (i, _), p in zip(hits, progs))
         # the drop-in get_model, one query at a time (no z3 here: a miss
-        # raises SolverUnavailable after the GPU search), over 16 distinct
-        # queries: "cold" compiles every group afresh, "stream" keeps the
-        # group cache across the 16 (what successive is_possible calls see)
+        # raises SolverUnavailable after the GPU search): "cold" compiles
+        # every group afresh (16 distinct queries, every memo cleared before
+        # each), "stream" keeps the group cache, the group-miss memo and the
+        # per-shape statistics across n_sample distinct queries (what
+        # successive is_possible calls of one analysis see)
         sample, seen = [], set()
         for q in qs:
             key = tuple(c.id for c in q)
             if key not in seen:
                 seen.add(key)
                 sample.append(q)
-            if len(sample) == 16:
+            if len(sample) == n_sample:
                 break
 
         def run(clear_each):
             lat, misses = [], 0
             M.stats.reset_gpu()
             M.clear_search_memos()
-            for q in sample:
+            for q in (sample[:16] if clear_each else sample):
                 M.get_model.cache_clear()
                 if clear_each:
                     M.clear_search_memos()      # compiled groups and group misses
@@ -117,11 +119,13 @@ def shape_lines(eng, n_queries):
                 except M.SolverUnavailable:
                     misses += 1
                 lat.append((time.perf_counter() - t1) * 1000.0)
-            return {"queries": len(sample), "median_ms": statistics.median(lat),
+            return {"queries": len(lat), "median_ms": statistics.median(lat),
+                    "mean_ms": statistics.mean(lat),
                     "max_ms": max(lat), "gpu_misses": misses,
-                    "memo_misses": M.stats.memo_misses, "kernel_ms_per_query":
-                        M.stats.kernel_time * 1000.0 / len(sample),
-                    "phase_ms_per_query": {k: v * 1000.0 / len(sample)
+                    "memo_misses": M.stats.memo_misses, "shape_skipped": M.stats.shape_skipped,
+                    "gated": M.stats.gated, "kernel_ms_per_query":
+                        M.stats.kernel_time * 1000.0 / len(lat),
+                    "phase_ms_per_query": {k: v * 1000.0 / len(lat)
                                            for k, v in M.stats.phase.items()}}
         cold = run(True)
         stream = run(False)
