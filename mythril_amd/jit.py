@@ -994,6 +994,9 @@ def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6, full: boo
     return rec[:-1], n_masks                     # the last record is the zeroed pad
 
 
+CONST_SPAIR = G.BANK[1] + 4
+
+
 def const_code(var: int, rec, prog) -> List[str]:
     """CONST with the value known: immediate moves instead of a scalar load
     of the constant table and its wait."""
@@ -1010,8 +1013,21 @@ def const_code(var: int, rec, prog) -> List[str]:
     out = []
     vals = [limbs[j] if j < n else 0 for j in range(8)]
     for j in range(0, 8, 2):                    # pairs stay 64-bit aligned
-        if j in idx and j + 1 in idx and vals[j] == 0 and vals[j + 1] == 0:
-            out.append("    v_mov_b64 v[%d:%d], 0" % (d + j, d + j + 1))
+        if j in idx and j + 1 in idx:
+            # one v_mov_b64 per limb pair (4 cycles) instead of two v_mov_b32
+            # (2.67 each): an inline constant when the pair is one, else the
+            # pair staged in s[52:53] (record bank B: unused by compiled code
+            # outside the division body, which sets it itself)
+            lo, hi = vals[j], vals[j + 1]
+            pair = "v[%d:%d]" % (d + j, d + j + 1)
+            if hi == 0 and lo <= 64:
+                out.append("    v_mov_b64 %s, %d" % (pair, lo))
+            elif lo == hi == M32:
+                out.append("    v_mov_b64 %s, -1" % pair)
+            else:
+                out.append("    s_mov_b32 s%d, 0x%x" % (CONST_SPAIR, lo))
+                out.append("    s_mov_b32 s%d, 0x%x" % (CONST_SPAIR + 1, hi))
+                out.append("    v_mov_b64 %s, s[%d:%d]" % (pair, CONST_SPAIR, CONST_SPAIR + 1))
             continue
         for q in (j, j + 1):
             if q in idx:
