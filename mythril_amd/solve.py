@@ -61,6 +61,27 @@ def _bit_indices(x: int):
         x ^= low
 
 
+class _Overlay(dict):
+    """A rewrite memo layered over another: reads fall through to the
+    parent, writes stay local.  ``_branches`` tries each disjunct's
+    definitions on top of the run's memo (valid for the definitions in force
+    before the disjunct: rewrite re-folds the entries a new definition
+    reaches) and drops the layer when the definitions are rolled back."""
+    __slots__ = ("parent",)
+
+    def __init__(self, parent):
+        super().__init__()
+        self.parent = parent
+
+    def get(self, k, d=None):
+        v = dict.get(self, k)
+        return self.parent.get(k, d) if v is None else v
+
+    def __getitem__(self, k):
+        v = dict.get(self, k)
+        return self.parent[k] if v is None else v
+
+
 def _mask(w: int) -> int:
     return (1 << w) - 1
 
@@ -82,6 +103,7 @@ class Solver:
         self.leaf_imm: Dict[int, int] = {}       # defined LEAF id -> leaf index
         self.leaf_node: Dict[int, object] = {}   # defined LEAF id -> the LEAF node
         self._dm = None                          # bit set of the defined leaves
+        self._memo: Dict[int, object] = {}       # the run's rewrite memo (run)
         # LEAF id -> generation of a branch's stand-in for an undefined value
         # (a stand-in may be split again by a later ``or``, to BRANCH_DEPTH)
         self.depth: Dict[int, int] = {}
@@ -849,7 +871,7 @@ class Solver:
         per: List[Dict[int, object]] = []
         for d in disj:
             self.unsat = False
-            atoms = self._atoms(d, {})
+            atoms = self._atoms(d, _Overlay(self._memo))
             if self.unsat:
                 per.append({})
                 continue
@@ -981,6 +1003,7 @@ class Solver:
         # one memo for the whole run: rewrite drops the entries a new
         # definition reaches (later roots see the new definitions folded)
         memo: Dict[int, object] = {}
+        self._memo = memo
         for _ in range(PASSES):
             found = 0
             every = []
