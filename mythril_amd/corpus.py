@@ -59,7 +59,15 @@ def dag_target_nodes(dag_id: int, seed: int = SEED) -> int:
 
 
 def make_dag(dag_id: int, seed: int = SEED, n_nodes: int = 0) -> Tuple[List[N.Node], int]:
-    """Return (constraints, source node count) for DAG ``dag_id``."""
+    """Return (constraints, source node count) for DAG ``dag_id``, built in
+    a fresh hash-consing scope: its compiled program is then the same in
+    every process (constants shared with DAGs built earlier would otherwise
+    carry older ids and move in the schedule)."""
+    with N.fresh_scope():
+        return _make_dag(dag_id, seed, n_nodes)
+
+
+def _make_dag(dag_id: int, seed: int, n_nodes: int) -> Tuple[List[N.Node], int]:
     rng = SplitMix64(dag_seed(seed, dag_id))
     target = n_nodes or 64 + rng.below(449)
     n_vars = 4 + rng.below(13)

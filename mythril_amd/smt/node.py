@@ -15,6 +15,7 @@ function name and signature (reference ``mythril/laser/smt/function.py:7-25``).
 
 from __future__ import annotations
 
+import contextlib
 import itertools
 import threading
 from typing import Dict, Tuple
@@ -80,6 +81,24 @@ def mk(op: str, sort: str, width: int, args: Tuple[Node, ...] = (), params: tupl
             n = Node(op, sort, width, dom, tuple(args), params)
             _table[key] = n
     return n
+
+
+@contextlib.contextmanager
+def fresh_scope():
+    """Build inside an empty hash-consing table (the previous one is restored
+    afterwards).  Node ids then follow the construction order of what is
+    built inside alone — not which equal nodes this process happened to
+    build before — so a compiled program's schedule (ordered by source ids,
+    ir._schedule) is the same in every process.  Nodes built inside are not
+    shared with equal nodes outside."""
+    global _table
+    with _lock:
+        saved, _table = _table, {}
+    try:
+        yield
+    finally:
+        with _lock:
+            _table = saved
 
 
 # ----------------------------------------------------------------------------

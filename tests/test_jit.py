@@ -160,3 +160,33 @@ def test_unsupported_program_stays_on_the_interpreter(monkeypatch):
     assert "mg_jp1:" not in text and "mg_jp0:" in text and "mg_jp2:" in text
     table = jit.table_asm(fps)
     assert "\t.quad 0\n\t.quad 0\n" in table and "mg_jp1" not in table
+
+
+def _program_digests(order):
+    """(worker, spawned fresh) compile the corpus DAGs in ``order``; digest
+    of each program's code, constants and record fingerprint."""
+    import hashlib
+    import bench
+    out = {}
+    for d in order:
+        p = bench.compile_unit(("c2", d))[1]
+        full, _ = jit.program_records(p, default_leafgen(p), d, full=True)
+        out[d] = (hashlib.sha1(p.code.tobytes() + p.consts.tobytes()).hexdigest(),
+                  jit.records_fingerprint(full))
+    return out
+
+
+def test_corpus_programs_do_not_depend_on_build_history():
+    """A corpus DAG compiles to the same program whatever its process built
+    before (corpus.make_dag builds in a fresh hash-consing scope): the
+    compiled-program image one process builds (bench.py --jit-build-only,
+    chunk workers) must fit the programs another process loads —
+    mg_jit_attach compares their record fingerprints, and refused a cached
+    image before this held (constants shared with DAGs built earlier carried
+    older ids and moved in the schedule)."""
+    import multiprocessing as mp
+    ids = list(range(40))
+    orders = [ids, ids[::-1]]
+    with mp.get_context("spawn").Pool(2) as pool:
+        a, b = pool.map(_program_digests, orders)
+    assert a == b
