@@ -27,7 +27,10 @@ def test_dump_parse_round_trip_corpus():
         text = smtlib.dump_query(roots)
         assert "define-fun" in text                 # shared sub-terms named once
         back = smtlib.parse_query(text)
-        assert len(back) == len(roots) and all(a is b for a, b in zip(roots, back))
+        # corpus DAGs live in their own hash-consing scope (corpus.make_dag),
+        # so the parsed nodes are equal in structure, not the same objects
+        assert len(back) == len(roots)
+        assert smtlib.dump_query(back) == text
 
 
 def test_parse_z3_style_text():
