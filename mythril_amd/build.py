@@ -79,5 +79,24 @@ def build_jit_stub() -> str:
     return JIT_STUB
 
 
+CC_LIB = os.path.join(LIBDIR, "libmythcc.so")
+CC_SOURCES = [os.path.join(CSRC, "mg_compile.cpp"), os.path.join(ROOT, "include", "mythcc.h"),
+              os.path.join(ROOT, "include", "mythgpu_ir.h")]
+
+
+def build_compiler(force: bool = False) -> str:
+    """The native host compiler (include/mythcc.h): plain host C++, g++."""
+    if not force and os.path.exists(CC_LIB) and \
+            all(os.path.getmtime(f) <= os.path.getmtime(CC_LIB) for f in CC_SOURCES):
+        return CC_LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    tmp = "%s.%d.tmp" % (CC_LIB, os.getpid())
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
+                    "-I" + os.path.join(ROOT, "include"), CC_SOURCES[0], "-o", tmp], check=True)
+    os.replace(tmp, CC_LIB)
+    return CC_LIB
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_compiler(force="--force" in sys.argv))

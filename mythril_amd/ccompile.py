@@ -1,0 +1,201 @@
+"""Python side of the native host compiler (``include/mythcc.h``,
+``mythril_amd/csrc/mg_compile.cpp``).
+
+:func:`compile_native` takes the same arguments as
+``ir.compile_constraints`` and returns the same :class:`ir.Program`: the
+source DAG (hash-consed ``smt.node`` terms) is flattened into arrays in one
+topological walk, the C++ compiler runs lowering, model construction
+(search mode), scheduling, register allocation and the leaf pools, and the
+result comes back as the instruction words, the constant table and a JSON
+record of the rest.  ``tests/test_native_compiler.py`` checks that both
+compilers emit identical programs.
+
+The library is host code (g++, no GPU); it is built in-tree next to
+``libmythgpu.so`` by ``mythril_amd/build.py`` and rebuilt on import when its
+sources are newer."""
+
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import threading
+from array import array
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import irdefs as I
+from .smt.node import ARRAY, BOOL, topo_order
+
+_lib = None
+_lock = threading.Lock()
+_OPS: Dict[str, int] = {}
+_OTHER = 0
+
+MGC_OK, MGC_UNSUPPORTED = 0, 1
+_SORT = {"bv": 0, BOOL: 1, ARRAY: 2}
+_REMAT = {"spill": 0, "always": 2}
+
+
+class _Input(ctypes.Structure):
+    _fields_ = [("n_nodes", ctypes.c_int32)] + \
+        [(n, ctypes.c_void_p) for n in ("op", "sort", "width", "dom", "id", "arg_off", "args", "p0",
+                                         "p1", "str", "cval_off", "cval")] + \
+        [("strings", ctypes.c_char_p), ("n_strings", ctypes.c_int32),
+         ("n_cons", ctypes.c_int32), ("cons", ctypes.c_void_p),
+         ("n_probes", ctypes.c_int32), ("probes", ctypes.c_void_p),
+         ("n_tables", ctypes.c_int32), ("table_name", ctypes.c_void_p),
+         ("table_size", ctypes.c_void_p),
+         ("default_entries", ctypes.c_int32), ("nreg", ctypes.c_int32),
+         ("n_extra", ctypes.c_int32), ("extra", ctypes.c_void_p),
+         ("leaf_pools", ctypes.c_int32), ("const_keys", ctypes.c_int32), ("solve", ctypes.c_int32),
+         ("remat_mode", ctypes.c_int32), ("remat_k", ctypes.c_int32),
+         ("keep_clean", ctypes.c_int32)]
+
+
+def load():
+    """The compiler library (built in-tree on first use)."""
+    global _lib, _OTHER
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        from .build import build_compiler
+        path = build_compiler()
+        lib = ctypes.CDLL(path)
+        lib.mgc_source_ops.restype = ctypes.c_char_p
+        lib.mgc_compile.argtypes = [ctypes.POINTER(_Input), ctypes.POINTER(ctypes.c_void_p)]
+        lib.mgc_compile.restype = ctypes.c_int
+        lib.mgc_error.argtypes = [ctypes.c_void_p]
+        lib.mgc_error.restype = ctypes.c_char_p
+        lib.mgc_code.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)]
+        lib.mgc_code.restype = ctypes.c_void_p
+        lib.mgc_table.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32),
+                                  ctypes.POINTER(ctypes.c_int32)]
+        lib.mgc_table.restype = ctypes.c_void_p
+        lib.mgc_meta.argtypes = [ctypes.c_void_p]
+        lib.mgc_meta.restype = ctypes.c_char_p
+        lib.mgc_free.argtypes = [ctypes.c_void_p]
+        names = lib.mgc_source_ops().decode().split("\n")
+        _OPS.update({n: i for i, n in enumerate(names)})
+        _OTHER = _OPS["?"]
+        _lib = lib
+    return _lib
+
+
+def _ptr(a):
+    return ctypes.addressof(ctypes.c_char.from_buffer(a)) if len(a) else None
+
+
+def compile_native(constraints: Sequence, probes: Sequence = (),
+                   table_sizes: Optional[Dict[str, int]] = None, default_entries: int = 2,
+                   nreg: int = I.NREG, extra_consts: Sequence[int] = (), leaf_pools: bool = False,
+                   const_keys: bool = False, solve: bool = False, leaf_remat: Optional[str] = None,
+                   keep_clean: Optional[bool] = None):
+    """``ir.compile_constraints`` through the native compiler."""
+    from . import ir
+    lib = load()
+    constraints, probes = list(constraints), list(probes)
+    nodes = topo_order(constraints + probes)
+    index = {n.id: i for i, n in enumerate(nodes)}
+    ops, OTHER = _OPS, _OTHER
+    op_a, sort_a, width_a, dom_a, str_a, cv_a = (array("i") for _ in range(6))
+    id_a, p0_a, p1_a = array("q"), array("q"), array("q")
+    off_a, args_a = array("i", [0]), array("i")
+    cval = bytearray()
+    strings: List[str] = []
+    sidx: Dict[str, int] = {}
+
+    def intern(s: str) -> int:
+        k = sidx.get(s)
+        if k is None:
+            k = sidx[s] = len(strings)
+            strings.append(s)
+        return k
+    for n in nodes:
+        op = n.op
+        code = ops.get(op, OTHER)
+        op_a.append(code)
+        sort_a.append(_SORT[n.sort])
+        width_a.append(n.width)
+        dom_a.append(n.dom or 0)
+        id_a.append(n.id)
+        for a in n.args:
+            args_a.append(index[a.id])
+        off_a.append(len(args_a))
+        p0 = p1 = 0
+        s = -1
+        c = -1
+        pr = n.params
+        if op == "bvnum":
+            c = len(cval) // 4
+            cval += pr[0].to_bytes(4 * ((n.width + 31) // 32), "little")
+        elif op in ("var", "array"):
+            s = intern(pr[0])
+        elif op == "apply":
+            s = intern(pr[0])
+            p0 = pr[1]
+        elif op == "extract":
+            p0, p1 = pr
+        elif op in ("zero_extend", "sign_extend"):
+            p0 = pr[0]
+        elif code == OTHER:
+            s = intern(op)
+        p0_a.append(p0)
+        p1_a.append(p1)
+        str_a.append(s)
+        cv_a.append(c)
+    cons_a = array("i", [index[c.id] for c in constraints])
+    probes_a = array("i", [index[p.id] for p in probes])
+    tsz = table_sizes or {}
+    tname_a = array("i", [intern(k) for k in tsz])
+    tsize_a = array("i", list(tsz.values()))
+    M = (1 << 256) - 1
+    extra = bytearray(b"".join((v & M).to_bytes(32, "little") for v in extra_consts))
+    blob = b"".join(s.encode() + b"\0" for s in strings)
+    remat = leaf_remat or ir.LEAF_REMAT
+    mode = _REMAT.get(remat, 1)
+    k = int(remat[7:]) if mode == 1 and remat[7:].isdigit() else 0
+    cval_buf = bytearray(cval)
+    inp = _Input(len(nodes), _ptr(op_a), _ptr(sort_a), _ptr(width_a), _ptr(dom_a), _ptr(id_a),
+                 _ptr(off_a), _ptr(args_a), _ptr(p0_a), _ptr(p1_a), _ptr(str_a), _ptr(cv_a),
+                 _ptr(cval_buf), blob, len(strings), len(cons_a), _ptr(cons_a),
+                 len(probes_a), _ptr(probes_a), len(tname_a), _ptr(tname_a), _ptr(tsize_a),
+                 default_entries, nreg, len(extra) // 32, _ptr(extra),
+                 int(leaf_pools), int(const_keys), int(solve), mode, k,
+                 int(ir.KEEP_CLEAN if keep_clean is None else keep_clean))
+    res = ctypes.c_void_p()
+    rc = lib.mgc_compile(ctypes.byref(inp), ctypes.byref(res))
+    try:
+        if rc != MGC_OK:
+            msg = lib.mgc_error(res).decode()
+            if rc == MGC_UNSUPPORTED:
+                raise ir.Unsupported(msg)
+            raise RuntimeError("native compiler: " + msg)
+        n = ctypes.c_int32()
+        p = lib.mgc_code(res, ctypes.byref(n))
+        code = np.frombuffer(ctypes.string_at(p, 16 * n.value), dtype=np.uint32).reshape(-1, 4).copy()
+        rows, ncv = ctypes.c_int32(), ctypes.c_int32()
+        p = lib.mgc_table(res, ctypes.byref(rows), ctypes.byref(ncv))
+        raw = ctypes.string_at(p, 32 * rows.value) if rows.value else b""
+        meta = json.loads(lib.mgc_meta(res))
+    finally:
+        lib.mgc_free(res)
+    consts = np.frombuffer(raw, dtype="<u4").reshape(-1, 8).astype(np.uint32)
+    values = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(rows.value)]
+    const_values = values[:ncv.value]
+    leaves = []
+    for name, width, kind, source, chunk, entry, po, pn in meta["leaves"]:
+        leaves.append(ir.Leaf(name, width, kind, source, chunk, entry,
+                              tuple(values[po:po + pn]) if pn else ()))
+    hist_counts = dict(meta["hist"])
+    stats = {"lnodes": meta["lnodes"], "n_ins": int(code.shape[0]), "spills": meta["spills"],
+             "reloads": meta["reloads"],
+             "hist": {I.OPNAME[op]: hist_counts[op] for op in meta["hist_order"]}}
+    return ir.Program(code, consts, const_values, leaves, meta["n_lds"], meta["n_probes"],
+                      meta["n_roots"], dict(meta["table_sizes"]), dict(meta["table_kinds"]),
+                      {k: [int(h, 16) for h in v] for k, v in meta["table_ckeys"]}, stats,
+                      [tuple(r) for r in meta["pool_ranges"]], dict(meta["derived"]),
+                      {k: v for k, v in meta["entry_keys"]}, meta["n_user_probes"])

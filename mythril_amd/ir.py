@@ -962,11 +962,32 @@ def lw_tables(constraints, probes) -> set:
     return out
 
 
+# Which compiler compile_constraints runs: "native" (include/mythcc.h, the
+# C++ port of this module and solve.py, identical output) or "py" (this
+# module; the specification the native one is tested against).
+COMPILER = _os.environ.get("MYTHRIL_GPU_COMPILER", "native")
+
+
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
                         extra_consts: Sequence[int] = (), leaf_pools: bool = False,
                         const_keys: bool = False, solve: bool = False) -> Program:
+    """Compile constraints (see :func:`compile_constraints_py`) with the
+    compiler ``COMPILER`` names."""
+    if COMPILER == "py":
+        return compile_constraints_py(constraints, probes, table_sizes, default_entries, nreg,
+                                      extra_consts, leaf_pools, const_keys, solve)
+    from .ccompile import compile_native
+    return compile_native(constraints, probes, table_sizes, default_entries, nreg, extra_consts,
+                          leaf_pools, const_keys, solve)
+
+
+def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] = (),
+                           table_sizes: Optional[Dict[str, int]] = None,
+                           default_entries: int = 2, nreg: int = I.NREG,
+                           extra_consts: Sequence[int] = (), leaf_pools: bool = False,
+                           const_keys: bool = False, solve: bool = False) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
     optional probe nodes (256-bit values written per assignment).  ``nreg``
     is the library's register-file size (``Engine.nreg``); ``extra_consts``

@@ -1,0 +1,125 @@
+"""The native host compiler (include/mythcc.h, mythril_amd/csrc/mg_compile.cpp)
+emits exactly the program the Python compiler (ir.compile_constraints_py +
+solve.py, the specification) emits: same instructions, constant table,
+leaves, pools, tables, derived values and statistics — on every named DAG
+case, C2 corpus DAGs, and every independent group of the C1 / C3 / C4
+stand-in query streams in both search (solve) and eval form.  CPU only."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from mythril_amd import build, ir
+from mythril_amd.ccompile import compile_native, load
+
+HDR = os.path.join(build.ROOT, "include", "mythcc.h")
+
+
+def _same(a, b):
+    assert np.array_equal(a.code, b.code)
+    assert np.array_equal(a.consts, b.consts)
+    for f in ("const_values", "n_lds", "n_probes", "n_roots", "table_sizes", "table_kinds",
+              "table_ckeys", "pool_ranges", "derived", "entry_keys", "n_user_probes", "stats"):
+        assert getattr(a, f) == getattr(b, f), f
+    assert a.leaves == b.leaves
+
+
+def _both(cons, probes=(), **kw):
+    try:
+        a = ir.compile_constraints_py(cons, probes, **kw)
+    except ir.Unsupported as e:
+        with pytest.raises(ir.Unsupported) as ei:
+            compile_native(cons, probes, **kw)
+        assert str(ei.value) == str(e)
+        return None
+    b = compile_native(cons, probes, **kw)
+    _same(a, b)
+    return b
+
+
+def test_library_exports_every_declared_symbol():
+    lib = load()
+    names = sorted(set(re.findall(r"^\s*(?:int|void|const char\*|const uint32_t\*)\s+(mgc_\w+)\s*\(",
+                                  open(HDR).read(), re.M)))
+    assert len(names) == 7
+    for n in names:
+        assert hasattr(lib, n), n
+    ops = lib.mgc_source_ops().decode().split("\n")
+    assert ops[0] == "bvnum" and ops[-1] == "?"
+
+
+def test_named_cases_identical():
+    import dag_cases
+    for name, (c, p, _, ts) in dag_cases.named_cases().items():
+        _both(c, p, table_sizes=ts or None)
+        _both(c, p, table_sizes=ts or None, leaf_pools=True, const_keys=True)
+
+
+def test_corpus_dags_identical():
+    from mythril_amd.corpus import make_dag
+    for d in list(range(12)) + [571, 1000, 4095]:
+        _both(make_dag(d)[0])
+
+
+@pytest.mark.parametrize("workload", ["c1", "c3", "c4"])
+def test_query_streams_identical(workload):
+    """Every group get_model searches (solve mode, with the ABI presets and
+    hints _compile_search_uncached adds) and its eval form."""
+    from mythril_amd import abi, workloads as W
+    import mythril_amd.model as M
+    n = 0
+    for q in W.queries(workload, 12):
+        for b in M.dependence_buckets(q):
+            hints = M.harvest_hints(b)
+            plan = abi.plan(b)
+            nodes = plan.apply(b) if plan is not None else b
+            _both(nodes, (), extra_consts=hints, leaf_pools=True, const_keys=True, solve=True)
+            _both(b)
+            n += 1
+    assert n >= 12
+
+
+def test_unsupported_and_errors():
+    from mythril_amd.smt import node as N
+    x = N.bv_var("x", 300)
+    y = N.bv_var("y", 300)
+    with pytest.raises(ir.Unsupported):          # arithmetic on a 300-bit value
+        compile_native([N.eq(N.bv_op("bvadd", x, y), x)])
+    _both([N.eq(N.bv_op("bvadd", x, y), x)])
+    a = N.array_var("A", 256, 256)
+    with pytest.raises(ir.Unsupported):
+        compile_native([N.eq(a, a)])
+
+
+def test_leaf_remat_policies_identical():
+    from mythril_amd.corpus import make_dag
+    roots = make_dag(3)[0]
+    saved = ir.LEAF_REMAT
+    try:
+        for pol in ("spill", "scratch", "scratch4", "always"):
+            ir.LEAF_REMAT = pol
+            _both(roots)
+    finally:
+        ir.LEAF_REMAT = saved
+
+
+def test_malformed_input_is_an_error_not_a_crash():
+    """Operands must precede their users: the C ABI checks indices."""
+    from mythril_amd.ccompile import _Input
+    lib = load()
+    i32 = lambda *v: (ctypes.c_int32 * len(v))(*v)  # noqa: E731
+    i64 = lambda *v: (ctypes.c_int64 * len(v))(*v)  # noqa: E731
+    keep = dict(op=i32(3, 3), sort=i32(1, 1), width=i32(1, 1), dom=i32(0, 0), id=i64(1, 2),
+                arg_off=i32(0, 1, 1), args=i32(1),          # node 0 names node 1 as operand
+                p0=i64(0, 0), p1=i64(0, 0), str=i32(-1, -1), cval_off=i32(-1, -1), cons=i32(0))
+    a = {k: ctypes.addressof(v) for k, v in keep.items()}
+    inp = _Input(2, a["op"], a["sort"], a["width"], a["dom"], a["id"], a["arg_off"], a["args"],
+                 a["p0"], a["p1"], a["str"], a["cval_off"], None, b"", 0, 1, a["cons"],
+                 0, None, 0, None, None, 2, 16, 0, None, 0, 0, 0, 1, 2, 1)
+    res = ctypes.c_void_p()
+    assert lib.mgc_compile(ctypes.byref(inp), ctypes.byref(res)) == 2
+    assert b"order" in lib.mgc_error(res)
+    lib.mgc_free(res)
