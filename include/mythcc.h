@@ -76,6 +76,16 @@ typedef struct mgc_input {
     int32_t remat_mode;        /* MGC_REMAT_*                                 */
     int32_t remat_k;
     int32_t keep_clean;
+    /* search mode (mythril_amd/model.py _compile_search_uncached):
+     * search_hints: add every numeral of the constraints (rounded up to a
+     *   multiple of 64, and small ones as 4-byte selectors) to the constant
+     *   pool (model.harvest_hints);
+     * abi_presets: pin the ABI offset words of calldata arrays read at
+     *   symbolic offsets and compile the query under those presets
+     *   (mythril_amd/abi.py plan / view); the presets come back in the
+     *   metadata ("presets"). */
+    int32_t search_hints;
+    int32_t abi_presets;
 } mgc_input;
 
 typedef struct mgc_result mgc_result;

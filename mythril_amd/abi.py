@@ -29,22 +29,62 @@ from .smt import node as N
 from .smt.node import Node, topo_order
 
 
+class View:
+    """A node of the query under the presets (:meth:`Plan.view`): the same
+    fields as ``smt.node.Node``, its id that of the node it stands for."""
+    __slots__ = ("op", "sort", "width", "dom", "args", "params", "id")
+
+    def __init__(self, op, sort, width, dom, args, params, nid):
+        self.op, self.sort, self.width, self.dom = op, sort, width, dom
+        self.args, self.params, self.id = args, params, nid
+
+    def is_bool(self) -> bool:
+        return self.sort == N.BOOL
+
+    def is_bv(self) -> bool:
+        return self.sort == N.BV
+
+    def is_array(self) -> bool:
+        return self.sort == N.ARRAY
+
+
 @dataclass
 class Plan:
     vars: Dict[str, int] = field(default_factory=dict)             # calldatasize
     arrays: Dict[str, Dict[int, int]] = field(default_factory=dict)  # offset bytes
-    subst: Dict[int, Node] = field(default_factory=dict)           # node id -> numeral
+    subst: Dict[int, int] = field(default_factory=dict)            # node id -> numeral value
 
     def apply(self, nodes: Sequence[Node]) -> List[Node]:
         """``nodes`` with the preset cells, the size and the pinned read
         keys replaced by numerals (hash-consed rebuild, linear)."""
         memo: Dict[int, Node] = {}
         for n in topo_order(list(nodes)):
-            r = self.subst.get(n.id)
-            if r is None:
+            v = self.subst.get(n.id)
+            if v is not None:
+                r = N.bv_num(v, n.width)
+            else:
                 args = tuple(memo[a.id] for a in n.args)
                 r = n if all(a is b for a, b in zip(args, n.args)) else \
                     N.mk(n.op, n.sort, n.width, args, n.params, dom=n.dom)
+            memo[n.id] = r
+        return [memo[n.id] for n in nodes]
+
+    def view(self, nodes: Sequence[Node]) -> List[object]:
+        """The query the search compiles (``ir.compile_constraints`` with
+        ``abi_presets``): like :meth:`apply`, but every replaced node keeps
+        the id of the node it replaces and nothing is hash-consed — so the
+        program's schedule (ordered by source ids) follows the original
+        query, and the native compiler (include/mythcc.h), which substitutes
+        in place, builds the same program."""
+        memo: Dict[int, object] = {}
+        for n in topo_order(list(nodes)):
+            v = self.subst.get(n.id)
+            if v is not None:
+                r = View("bvnum", N.BV, n.width, 0, (), (v % (1 << n.width),), n.id)
+            else:
+                args = tuple(memo[a.id] for a in n.args)
+                r = n if all(a is b for a, b in zip(args, n.args)) else \
+                    View(n.op, n.sort, n.width, n.dom, args, n.params, n.id)
             memo[n.id] = r
         return [memo[n.id] for n in nodes]
 
@@ -148,17 +188,17 @@ def plan(constraints: Sequence[Node]) -> Optional[Plan]:
             for i in range(32):
                 cells[off + i] = (val >> (8 * (31 - i))) & 0xFF
             for k, c in keys:
-                out.subst[k.id] = N.bv_num(val + c, k.width)
+                out.subst[k.id] = (val + c) % (1 << k.width)
             nxt = val + hi + 1
             size_var = size_var or size
         if size_var is not None:
             out.vars[size_var.params[0]] = nxt
-            out.subst[size_var.id] = N.bv_num(nxt, size_var.width)
+            out.subst[size_var.id] = nxt % (1 << size_var.width)
         out.arrays[arr.params[0]] = cells
         for n in nodes:
             if n.op == "select" and n.args[0] is arr and n.args[1].op == "bvnum" and \
                     n.args[1].params[0] in cells:
-                out.subst[n.id] = N.bv_num(cells[n.args[1].params[0]], n.width)
+                out.subst[n.id] = cells[n.args[1].params[0]] % (1 << n.width)
     return out if out.arrays else None
 
 

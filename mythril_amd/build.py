@@ -82,18 +82,35 @@ def build_jit_stub() -> str:
 CC_LIB = os.path.join(LIBDIR, "libmythcc.so")
 CC_SOURCES = [os.path.join(CSRC, "mg_compile.cpp"), os.path.join(ROOT, "include", "mythcc.h"),
               os.path.join(ROOT, "include", "mythgpu_ir.h")]
+CC_PY_SOURCE = os.path.join(CSRC, "mg_compile_py.cpp")
+
+
+def cc_ext_path() -> str:
+    import sysconfig
+    return os.path.join(LIBDIR, "_mythcc" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def _fresh(out, deps) -> bool:
+    return os.path.exists(out) and all(os.path.getmtime(f) <= os.path.getmtime(out) for f in deps)
 
 
 def build_compiler(force: bool = False) -> str:
-    """The native host compiler (include/mythcc.h): plain host C++, g++."""
-    if not force and os.path.exists(CC_LIB) and \
-            all(os.path.getmtime(f) <= os.path.getmtime(CC_LIB) for f in CC_SOURCES):
-        return CC_LIB
+    """The native host compiler (include/mythcc.h, plain host C++, g++): the
+    C-ABI library libmythcc.so and the CPython front-end _mythcc (the same
+    compiler plus a DAG walk over the Python objects)."""
+    import sysconfig
     os.makedirs(LIBDIR, exist_ok=True)
-    tmp = "%s.%d.tmp" % (CC_LIB, os.getpid())
-    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall",
-                    "-I" + os.path.join(ROOT, "include"), CC_SOURCES[0], "-o", tmp], check=True)
-    os.replace(tmp, CC_LIB)
+    flags = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I" + os.path.join(ROOT, "include")]
+    if force or not _fresh(CC_LIB, CC_SOURCES):
+        tmp = "%s.%d.tmp" % (CC_LIB, os.getpid())
+        subprocess.run(flags + [CC_SOURCES[0], "-o", tmp], check=True)
+        os.replace(tmp, CC_LIB)
+    ext = cc_ext_path()
+    if force or not _fresh(ext, CC_SOURCES + [CC_PY_SOURCE]):
+        tmp = "%s.%d.tmp" % (ext, os.getpid())
+        subprocess.run(flags + ["-I" + sysconfig.get_paths()["include"], CC_PY_SOURCE, CC_SOURCES[0],
+                                "-o", tmp], check=True)
+        os.replace(tmp, ext)
     return CC_LIB
 
 

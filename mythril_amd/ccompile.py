@@ -51,7 +51,8 @@ class _Input(ctypes.Structure):
          ("n_extra", ctypes.c_int32), ("extra", ctypes.c_void_p),
          ("leaf_pools", ctypes.c_int32), ("const_keys", ctypes.c_int32), ("solve", ctypes.c_int32),
          ("remat_mode", ctypes.c_int32), ("remat_k", ctypes.c_int32),
-         ("keep_clean", ctypes.c_int32)]
+         ("keep_clean", ctypes.c_int32), ("search_hints", ctypes.c_int32),
+         ("abi_presets", ctypes.c_int32)]
 
 
 def load():
@@ -89,12 +90,67 @@ def _ptr(a):
     return ctypes.addressof(ctypes.c_char.from_buffer(a)) if len(a) else None
 
 
+_ext = None
+
+
+def _load_ext():
+    """The CPython front-end (_mythcc: the compiler plus a C walk over the
+    Node objects), built with the C-ABI library."""
+    global _ext
+    if _ext is None:
+        import importlib.util
+        from .build import cc_ext_path
+        load()
+        spec = importlib.util.spec_from_file_location("_mythcc", cc_ext_path())
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _ext = mod
+    return _ext
+
+
 def compile_native(constraints: Sequence, probes: Sequence = (),
                    table_sizes: Optional[Dict[str, int]] = None, default_entries: int = 2,
                    nreg: int = I.NREG, extra_consts: Sequence[int] = (), leaf_pools: bool = False,
                    const_keys: bool = False, solve: bool = False, leaf_remat: Optional[str] = None,
-                   keep_clean: Optional[bool] = None):
-    """``ir.compile_constraints`` through the native compiler."""
+                   keep_clean: Optional[bool] = None, search_hints: bool = False,
+                   abi_presets: bool = False):
+    """``ir.compile_constraints`` through the native compiler: the DAG is
+    walked by the _mythcc front-end in C, compiled by mgc_compile."""
+    from . import ir
+    ext = _load_ext()
+    M = (1 << 256) - 1
+    extra = b"".join((v & M).to_bytes(32, "little") for v in extra_consts)
+    remat = leaf_remat or ir.LEAF_REMAT
+    mode = _REMAT.get(remat, 1)
+    k = int(remat[7:]) if mode == 1 and remat[7:].isdigit() else 0
+    rc, err, code_b, raw, ncv, meta = ext.compile(
+        list(constraints), list(probes), _OPS, list((table_sizes or {}).items()), default_entries,
+        nreg, extra, int(leaf_pools), int(const_keys), int(solve), mode, k,
+        int(ir.KEEP_CLEAN if keep_clean is None else keep_clean), int(search_hints),
+        int(abi_presets))
+    if rc != MGC_OK:
+        if rc == MGC_UNSUPPORTED:
+            raise ir.Unsupported(err)
+        raise RuntimeError("native compiler: " + err)
+    return _program(np.frombuffer(code_b, dtype=np.uint32).reshape(-1, 4).copy(), raw, ncv,
+                    json.loads(meta))
+
+
+def buckets(constraints: Sequence) -> List[int]:
+    """Independent-group label of each constraint (labels in order of first
+    occurrence), model.dependence_buckets' partition computed natively."""
+    return _load_ext().buckets(list(constraints))
+
+
+def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
+                          table_sizes: Optional[Dict[str, int]] = None, default_entries: int = 2,
+                          nreg: int = I.NREG, extra_consts: Sequence[int] = (),
+                          leaf_pools: bool = False, const_keys: bool = False, solve: bool = False,
+                          leaf_remat: Optional[str] = None, keep_clean: Optional[bool] = None,
+                          search_hints: bool = False, abi_presets: bool = False):
+    """The same compile through the plain C ABI (libmythcc.so, ctypes): the
+    DAG flattened in Python into mgc_input arrays — what another FFI host
+    does (INTEGRATION.md)."""
     from . import ir
     lib = load()
     constraints, probes = list(constraints), list(probes)
@@ -165,7 +221,8 @@ def compile_native(constraints: Sequence, probes: Sequence = (),
                  len(probes_a), _ptr(probes_a), len(tname_a), _ptr(tname_a), _ptr(tsize_a),
                  default_entries, nreg, len(extra) // 32, _ptr(extra),
                  int(leaf_pools), int(const_keys), int(solve), mode, k,
-                 int(ir.KEEP_CLEAN if keep_clean is None else keep_clean))
+                 int(ir.KEEP_CLEAN if keep_clean is None else keep_clean), int(search_hints),
+                 int(abi_presets))
     res = ctypes.c_void_p()
     rc = lib.mgc_compile(ctypes.byref(inp), ctypes.byref(res))
     try:
@@ -183,19 +240,27 @@ def compile_native(constraints: Sequence, probes: Sequence = (),
         meta = json.loads(lib.mgc_meta(res))
     finally:
         lib.mgc_free(res)
+    return _program(code, raw, ncv.value, meta)
+
+
+def _program(code, raw: bytes, ncv: int, meta):
+    from . import ir
     consts = np.frombuffer(raw, dtype="<u4").reshape(-1, 8).astype(np.uint32)
-    values = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(rows.value)]
-    const_values = values[:ncv.value]
-    leaves = []
-    for name, width, kind, source, chunk, entry, po, pn in meta["leaves"]:
-        leaves.append(ir.Leaf(name, width, kind, source, chunk, entry,
-                              tuple(values[po:po + pn]) if pn else ()))
+    const_values = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(ncv)]
+    Leaf = ir.Leaf
+    leaves = [Leaf(*row) for row in meta["leaves"]]
     hist_counts = dict(meta["hist"])
     stats = {"lnodes": meta["lnodes"], "n_ins": int(code.shape[0]), "spills": meta["spills"],
              "reloads": meta["reloads"],
              "hist": {I.OPNAME[op]: hist_counts[op] for op in meta["hist_order"]}}
-    return ir.Program(code, consts, const_values, leaves, meta["n_lds"], meta["n_probes"],
+    prog = ir.Program(code, consts, const_values, leaves, meta["n_lds"], meta["n_probes"],
                       meta["n_roots"], dict(meta["table_sizes"]), dict(meta["table_kinds"]),
                       {k: [int(h, 16) for h in v] for k, v in meta["table_ckeys"]}, stats,
                       [tuple(r) for r in meta["pool_ranges"]], dict(meta["derived"]),
                       {k: v for k, v in meta["entry_keys"]}, meta["n_user_probes"])
+    pre = meta.get("presets")
+    if pre is not None:
+        from .abi import Plan
+        prog.presets = Plan(vars={k: int(v, 16) for k, v in pre["vars"]},
+                            arrays={k: dict(cells) for k, cells in pre["arrays"]})
+    return prog

@@ -234,6 +234,9 @@ struct OMap {
     }
     void put(const K& k, const V& v) { setdefault(k, v) = v; }
     size_t size() const { return items.size(); }
+    void truncate(size_t n) {                // drop the entries inserted after the first n
+        while (items.size() > n) { idx.erase(items.back().first); items.pop_back(); }
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -296,9 +299,36 @@ static std::vector<int> topo(const std::vector<Src>& S, const std::vector<int>& 
 // ---------------------------------------------------------------------------
 // lowered DAG (ir.LNode)
 // ---------------------------------------------------------------------------
+// operand list of an LNode: up to three inline (every op but an n-ary AND),
+// so building and hashing nodes allocates nothing
+struct Args {
+    int n = 0;
+    int a[3] = {0, 0, 0};
+    std::vector<int> more;
+    Args() {}
+    Args(std::initializer_list<int> il) { assign(il.begin(), il.end()); }
+    Args(const std::vector<int>& v) { assign(v.data(), v.data() + v.size()); }
+    template <class It> void assign(It b, It e) {
+        n = (int)(e - b);
+        if (n <= 3) { std::copy(b, e, a); more.clear(); }
+        else more.assign(b, e);
+    }
+    const int* begin() const { return n <= 3 ? a : more.data(); }
+    const int* end() const { return begin() + n; }
+    int* begin() { return n <= 3 ? a : more.data(); }
+    int* end() { return begin() + n; }
+    size_t size() const { return (size_t)n; }
+    bool empty() const { return n == 0; }
+    int operator[](size_t i) const { return begin()[i]; }
+    int& operator[](size_t i) { return begin()[i]; }
+    int back() const { return begin()[n - 1]; }
+    bool operator==(const Args& o) const { return n == o.n && std::equal(begin(), end(), o.begin()); }
+    bool operator!=(const Args& o) const { return !(*this == o); }
+};
+
 struct LN {
     int op, width;
-    std::vector<int> args;
+    Args args;
     bool has_imm;
     U imm;
     int64_t birth;
@@ -328,7 +358,7 @@ typedef std::vector<int> Chunks;
 // hash-consing key of an LNode: (op, width, operand ids, imm)
 struct MkKey {
     int op, width;
-    Chunks args;
+    Args args;
     bool has_imm;
     U imm;
     bool operator==(const MkKey& o) const {
@@ -369,7 +399,7 @@ struct Lowerer {
     }
 
     // -- hash-consed constructors (ir._Lowerer.mk / const / leaf) --------------
-    int mk(int op, int width, Chunks args, bool has_imm = false, const U& imm = U()) {
+    int mk(int op, int width, Args args, bool has_imm = false, const U& imm = U()) {
         if (op == MG_CONCAT && width == MG_MAX_WIDTH && ln[args[0]].op == MG_EXTRACT &&
             ln[args[0]].imm.zero() && ln[ln[args[0]].args[0]].width == MG_MAX_WIDTH)
             args[0] = ln[args[0]].args[0];
@@ -383,7 +413,7 @@ struct Lowerer {
         table.emplace(std::move(key), id);
         return id;
     }
-    int mki(int op, int width, Chunks args, int64_t imm) { return mk(op, width, std::move(args), true, U::of((uint64_t)imm)); }
+    int mki(int op, int width, Args args, int64_t imm) { return mk(op, width, std::move(args), true, U::of((uint64_t)imm)); }
     int cnst(const U& value, int width) { return mk(MG_CONST, width, {}, true, value & mask(width)); }
     int cnst(uint64_t value, int width) { return cnst(U::of(value), width); }
     int leaf(const std::string& name, int width, int kind, const std::string& source, int chunk = 0, int entry = 0) {
@@ -955,6 +985,8 @@ struct Solver {
     std::unordered_map<int, int> depth;
     bool unsat = false;
 
+    std::vector<std::pair<int, bool>> rw_stack_;
+
     explicit Solver(Lowerer& l) : lw(l), ln(l.ln) {
         one = lw.cnst(1, 1);
         zero = lw.cnst(0, 1);
@@ -1004,7 +1036,7 @@ struct Solver {
         return -1;
     }
 
-    bool const_fold(int x, const Chunks& args, U& out) {
+    bool const_fold(int x, const Args& args, U& out) {
         int w = ln[x].width, op = ln[x].op;
         U m = mask(w);
         auto v = [&](int i) { return ln[args[i]].imm; };
@@ -1021,12 +1053,12 @@ struct Solver {
         }
     }
 
-    bool all_const(const Chunks& args) const {
+    bool all_const(const Args& args) const {
         for (int a : args) if (ln[a].op != MG_CONST) return false;
         return true;
     }
 
-    int fold(int x, const Chunks& args) {
+    int fold(int x, const Args& args) {
         int op = ln[x].op;
         if ((op == MG_CONCAT || op == MG_EXTRACT || op == MG_AND || op == MG_OR || op == MG_XOR ||
              op == MG_SUB || op == MG_MUL || op == MG_NOT) && all_const(args)) {
@@ -1100,7 +1132,11 @@ struct Solver {
 
     const Bits& depof(int n) {
         if ((size_t)n < has_dep.size() && has_dep[n]) return dep[n];
-        if (dep.size() < ln.size()) { dep.resize(ln.size()); has_dep.resize(ln.size(), 0); }
+        if (dep.size() < ln.size()) {           // geometric: nodes keep being created
+            size_t sz = std::max(ln.size(), 2 * dep.size());
+            dep.resize(sz);
+            has_dep.resize(sz, 0);
+        }
         std::vector<int> stack{n};
         while (!stack.empty()) {
             int x = stack.back();
@@ -1129,7 +1165,9 @@ struct Solver {
 
     int rewrite(int n, Memo& memo) {
         const Bits& dmask = defmask();
-        std::vector<std::pair<int, bool>> stack{{n, false}};
+        auto& stack = rw_stack_;
+        stack.clear();
+        stack.push_back({n, false});
         while (!stack.empty()) {
             auto [x, done] = stack.back();
             stack.pop_back();
@@ -1150,18 +1188,18 @@ struct Solver {
             if (!done) {
                 if (is_clean(x) && !depof(x).meets(dmask)) { memo.put(x, x); continue; }
                 stack.push_back({x, true});
-                Chunks args = ln[x].args;
+                Args args = ln[x].args;
                 for (int a : args) {
                     int r = memo.get(a);
                     if (r < 0 || depof(r).meets(dmask)) stack.push_back({a, false});
                 }
                 continue;
             }
-            Chunks args;
-            for (int a : ln[x].args) {
+            Args args = ln[x].args;
+            for (int& a : args) {
                 int r = memo.get(a);
                 if (r < 0) throw std::runtime_error("rewrite: operand missing");
-                args.push_back(r);
+                a = r;
             }
             int r = fold(x, args);
             set_clean(r);
@@ -1307,7 +1345,7 @@ struct Solver {
         return one;
     }
 
-    static bool contains(const Chunks& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); }
+    template <class V> static bool contains(const V& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); }
 
     Chunks atoms(int root, Memo& memo) {
         Chunks out;
@@ -1329,7 +1367,7 @@ struct Solver {
             if (op == MG_NOT && ln[x].width == 1) {
                 int y = ln[x].args[0];
                 if (ln[y].op == MG_OR && ln[y].width == 1) {
-                    Chunks ya = ln[y].args;
+                    Args ya = ln[y].args;
                     for (int a : ya) stack.push_back(not_(a));
                     continue;
                 }
@@ -1721,14 +1759,16 @@ struct Solver {
             int y = stack.back();
             stack.pop_back();
             if (ln[y].op == MG_OR && ln[y].width == 1) {
-                const Chunks& ya = ln[y].args;
+                const Args& ya = ln[y].args;
                 for (size_t i = ya.size(); i-- > 0;) stack.push_back(ya[i]);
             } else {
                 disj.push_back(y);
             }
         }
         if ((int)disj.size() > MAX_BRANCHES || n_branch >= MAX_OR) return 0;
-        OMap<int, int> saved = repl;
+        // definitions only append to repl: the state before the disjuncts
+        // is its length, and rolling back truncates (solve.py copies the dict)
+        const size_t saved = repl.size();
         bool unsat_saved = unsat;
         std::vector<OMap<int, int>> per;
         for (int d : disj) {
@@ -1740,9 +1780,9 @@ struct Solver {
             define(at);
             ranges(at);
             OMap<int, int> defs;
-            for (auto& kv : repl.items) if (!saved.has(kv.first)) defs.put(kv.first, kv.second);
+            for (size_t i = saved; i < repl.items.size(); i++) defs.put(repl.items[i].first, repl.items[i].second);
             per.push_back(std::move(defs));
-            repl = saved;
+            repl.truncate(saved);
             dm_valid = false;
         }
         unsat = unsat_saved;
@@ -1975,9 +2015,11 @@ struct Alloc {
     int nreg, trash;
     int remat_mode, remat_k;
     bool keep_clean;
-    std::unordered_map<int, std::vector<int>> uses;
-    std::unordered_map<int, size_t> ptr;
-    std::unordered_map<int, int> reg_of, lds_of;
+    // per LNode id: its uses (positions in order, CSR), the scan pointer
+    // into them, its register / spill slot (-1: none)
+    std::vector<int> use_off, use_pos, ptr, reg_of, lds_of;
+    bool has_reg(int v) const { return reg_of[v] >= 0; }
+    bool has_lds(int v) const { return lds_of[v] >= 0; }
     std::vector<std::pair<int, int>> holder;          // (reg, value), insertion order
     std::vector<int> free_regs;
     std::unordered_map<int, bool> reg_clean;
@@ -1992,14 +2034,12 @@ struct Alloc {
           keep_clean(kc) {}
 
     int64_t next_use(int v, int64_t i) {
-        auto it = uses.find(v);
-        if (it == uses.end()) return FAR;
-        const auto& u = it->second;
-        size_t& p = ptr[v];
-        while (p < u.size() && u[p] < i) p++;
-        return p < u.size() ? u[p] : FAR;
+        int b = use_off[v], e = use_off[v + 1];
+        int& p = ptr[v];
+        while (b + p < e && use_pos[b + p] < i) p++;
+        return b + p < e ? use_pos[b + p] : FAR;
     }
-    bool free_to_drop(int v) const { return ln[v].op == MG_CONST || lds_of.count(v); }
+    bool free_to_drop(int v) const { return ln[v].op == MG_CONST || has_lds(v); }
     bool droppable_when_full(int v) const { return free_to_drop(v) || ln[v].op == MG_LEAF; }
     bool clean_of(int r) const { auto it = reg_clean.find(r); return it != reg_clean.end() && it->second; }
     void holder_del(int r) {
@@ -2008,7 +2048,8 @@ struct Alloc {
     static bool in(const std::vector<int>& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); }
     static void remove(std::vector<int>& v, int x) { v.erase(std::find(v.begin(), v.end(), x)); }
 
-    int alloc_reg(int i, const std::unordered_set<int>& protect, bool oldest = false) {
+    static bool protects(const Args& p, int v) { for (int a : p) if (a == v) return true; return false; }
+    int alloc_reg(int i, const Args& protect, bool oldest = false) {
         if (!free_regs.empty()) {
             int r;
             if (oldest) { r = free_regs.front(); free_regs.erase(free_regs.begin()); }
@@ -2019,7 +2060,7 @@ struct Alloc {
         int64_t far = -1;
         for (auto& hv : holder) {
             int v = hv.second;
-            if (protect.count(v)) continue;
+            if (protects(protect, v)) continue;
             int64_t nu = next_use(v, i);
             if (nu > far) { victim = v; far = nu; }
         }
@@ -2028,17 +2069,17 @@ struct Alloc {
             victim = -1; far = -1;
             for (auto& hv : holder) {
                 int v = hv.second;
-                if (protect.count(v) || !droppable_when_full(v)) continue;
+                if (protects(protect, v) || !droppable_when_full(v)) continue;
                 int64_t nu = next_use(v, i);
                 if (nu > far) { victim = v; far = nu; }
             }
             if (victim < 0) throw Unsupported("spill budget exceeded");
         }
         int r = reg_of[victim];
-        reg_of.erase(victim);
+        reg_of[victim] = -1;
         holder_del(r);
         bool slots_left = !free_lds.empty() || n_lds < MAX_SPILL;
-        if (ln[victim].op == MG_LEAF && !lds_of.count(victim) && remat_mode != MGC_REMAT_SPILL) {
+        if (ln[victim].op == MG_LEAF && !has_lds(victim) && remat_mode != MGC_REMAT_SPILL) {
             int tier = LDS_TIER + (remat_mode == MGC_REMAT_SCRATCH ? remat_k : 0);
             bool cheap_free = (!free_lds.empty() && *std::min_element(free_lds.begin(), free_lds.end()) < tier) ||
                               n_lds < tier;
@@ -2063,7 +2104,7 @@ struct Alloc {
         reg_clean[r] = ln[v].width <= 32;
         if (ln[v].op == MG_CONST) {
             ins.push_back({MG_CONST, (uint32_t)ln[v].width, (uint32_t)r, 0, 0, 0, (uint32_t)const_index.at(ln[v].imm), 0});
-        } else if (lds_of.count(v)) {
+        } else if (has_lds(v)) {
             ins.push_back({MG_RELOAD, (uint32_t)ln[v].width, (uint32_t)r, 0, 0, 0, (uint32_t)lds_of[v], 0});
             n_reload++;
         } else {
@@ -2073,44 +2114,57 @@ struct Alloc {
 
     void release(int v, int i) {
         if (next_use(v, i + 1) >= FAR) {
-            auto it = reg_of.find(v);
-            if (it != reg_of.end()) {
-                int r = it->second;
-                reg_of.erase(it);
+            if (has_reg(v)) {
+                int r = reg_of[v];
+                reg_of[v] = -1;
                 holder_del(r);
                 free_regs.push_back(r);
             }
-            auto jt = lds_of.find(v);
-            if (jt != lds_of.end()) {
-                int s = jt->second;
-                lds_of.erase(jt);
+            if (has_lds(v)) {
+                int s = lds_of[v];
+                lds_of[v] = -1;
                 free_lds.push_back(s);
             }
         }
     }
 
     void run() {
+        size_t nn = ln.size();
+        use_off.assign(nn + 1, 0);
+        ptr.assign(nn, 0);
+        reg_of.assign(nn, -1);
+        lds_of.assign(nn, -1);
         for (size_t i = 0; i < order.size(); i++)
-            for (int a : ln[order[i]].args) uses[a].push_back((int)i);
+            for (int a : ln[order[i]].args) use_off[a + 1]++;
+        for (size_t v = 0; v < nn; v++) use_off[v + 1] += use_off[v];
+        use_pos.assign(use_off[nn], 0);
+        {
+            std::vector<int> fill(use_off.begin(), use_off.end() - 1);
+            for (size_t i = 0; i < order.size(); i++)
+                for (int a : ln[order[i]].args) use_pos[fill[a]++] = (int)i;
+        }
         for (int r = nreg - 1; r >= 0; r--) free_regs.push_back(r);
         for (size_t ii = 0; ii < order.size(); ii++) {
             int i = (int)ii;
             int n = order[ii];
             const LN& N = ln[n];
-            std::unordered_set<int> protect(N.args.begin(), N.args.end());
+            const Args& protect = N.args;
             for (int a : N.args) {
-                if (!reg_of.count(a)) {
+                if (!has_reg(a)) {
                     int r = alloc_reg(i, protect, ln[a].op != MG_CONST);
                     materialise(a, r);
                     reg_of[a] = r;
                     holder.push_back({r, a});
                 }
             }
-            std::vector<int> slots;
-            for (int a : N.args) slots.push_back(reg_of.at(a));
-            std::vector<int> uniq;
-            for (int a : N.args) if (!in(uniq, a)) uniq.push_back(a);
-            for (int a : uniq) release(a, i);
+            Args slots = N.args;
+            for (int& a : slots) a = reg_of[a];
+            for (size_t k = 0; k < N.args.size(); k++) {
+                int a = N.args[k];
+                bool seen = false;
+                for (size_t j = 0; j < k; j++) if (N.args[j] == a) { seen = true; break; }
+                if (!seen) release(a, i);
+            }
             if (N.op == MG_ROOT || N.op == MG_OUT) {
                 ins.push_back({(uint32_t)N.op, 1, (uint32_t)trash, (uint32_t)slots[0], 0, 0,
                                N.has_imm ? (uint32_t)N.imm.w[0] : 0u, 0});
@@ -2118,8 +2172,7 @@ struct Alloc {
             }
             uint32_t flags = fused.count(n) ? (uint32_t)MG_ROOT_FLAG : 0u;
             int d = -1;
-            auto ut = uses.find(n);
-            if (ut == uses.end() || ut->second.empty()) {
+            if (use_off[n] == use_off[n + 1]) {
                 if (!free_regs.empty()) {
                     d = free_regs.back();
                 } else {
@@ -2317,6 +2370,155 @@ static OMap<std::string, std::vector<Big>> scan_const_keys(const std::vector<Src
 }
 
 // ---------------------------------------------------------------------------
+// search-mode inputs: candidate hints (model.harvest_hints) and ABI presets
+// (abi.plan / Plan.view)
+// ---------------------------------------------------------------------------
+static void harvest_hints(const std::vector<Src>& S, const std::vector<int>& cons, std::vector<U>& out) {
+    U M256 = mask(256), low6 = ~U::of(63);
+    for (int n : topo(S, cons)) {
+        if (S[n].op != S_BVNUM || S[n].width < 8) continue;
+        U v = S[n].val.chunk(0);                         // (v + 63) & ~63, mod 2^256
+        out.push_back((v + U::of(63)) & M256 & low6);
+        const Big& b = S[n].val;
+        if (!b.l.empty() && b.l.size() == 1) out.push_back(shl(U::of(b.l[0]), 224));
+    }
+}
+
+struct Presets {
+    std::vector<std::pair<std::string, U>> vars;                       // size var -> value
+    std::vector<std::pair<std::string, std::vector<std::pair<int64_t, int>>>> arrays;   // offset -> byte
+    std::vector<std::pair<int, U>> subst;                              // node -> numeral
+};
+
+// abi._split_add: k as base + constant (bvadd chains with numerals)
+static bool split_add(const std::vector<Src>& S, int k, int& base, U& c) {
+    base = -1;
+    c = U();
+    std::vector<int> stack{k};
+    while (!stack.empty()) {
+        int x = stack.back();
+        stack.pop_back();
+        if (S[x].op == S_BVNUM) c = c + S[x].val.low384();
+        else if (S[x].op == S_BVADD) for (int a : S[x].args) stack.push_back(a);
+        else if (base < 0) base = x;
+        else return false;
+    }
+    if (base < 0) return false;
+    c = c & mask(S[k].width);
+    return true;
+}
+
+// abi._byte_cell: (offset, size var) of ite(p < size, A[p], 0) or A[p]
+static bool byte_cell(const std::vector<Src>& S, int x, int arr, int64_t& off, int& size) {
+    size = -1;
+    if (S[x].op == S_ITE && S[S[x].args[2]].op == S_BVNUM && S[S[x].args[2]].val.l.empty()) {
+        int c = S[x].args[0];
+        if (S[c].op != S_BVSLT || S[S[c].args[0]].op != S_BVNUM || S[S[c].args[1]].op != S_VAR) return false;
+        size = S[c].args[1];
+        x = S[x].args[1];
+    }
+    if (S[x].op == S_SELECT && S[x].args[0] == arr && S[S[x].args[1]].op == S_BVNUM) {
+        const Big& v = S[S[x].args[1]].val;
+        if (v.l.size() > 2) return false;
+        off = (int64_t)(v.l.empty() ? 0 : v.l[0]) | (v.l.size() > 1 ? (int64_t)v.l[1] << 32 : 0);
+        return true;
+    }
+    return false;
+}
+
+// abi._word: (first byte offset, size var) when base is the 32-byte word of arr
+static bool word_of(const std::vector<Src>& S, int base, int arr, int64_t& first, int& size) {
+    std::vector<int> parts, stack{base};
+    while (!stack.empty()) {
+        int x = stack.back();
+        stack.pop_back();
+        if (S[x].op == S_CONCAT) for (size_t i = S[x].args.size(); i-- > 0;) stack.push_back(S[x].args[i]);
+        else parts.push_back(x);
+    }
+    if (parts.size() != 32) return false;
+    size = -1;
+    std::vector<int64_t> offs;
+    for (int p : parts) {
+        int64_t o;
+        int s;
+        if (!byte_cell(S, p, arr, o, s) || (s >= 0 && size >= 0 && s != size)) return false;
+        if (s >= 0) size = s;
+        offs.push_back(o);
+    }
+    for (size_t i = 0; i < offs.size(); i++) if (offs[i] != offs[0] + (int64_t)i) return false;
+    first = offs[0];
+    return true;
+}
+
+static bool abi_plan(const std::vector<Src>& S, const std::vector<int>& cons, Presets& out) {
+    std::vector<int> nodes = topo(S, cons);
+    struct Arr { int arr; std::vector<Big> consts; std::vector<int> sym; };
+    OMap<int, Arr> by_arr;
+    for (int n : nodes) {
+        if (S[n].op != S_SELECT || S[S[n].args[0]].op != S_ARRAY) continue;
+        int arr = S[n].args[0], k = S[n].args[1];
+        Arr& d = by_arr.setdefault(arr, Arr{arr, {}, {}});
+        if (S[k].op == S_BVNUM) {
+            if (std::find(d.consts.begin(), d.consts.end(), S[k].val) == d.consts.end()) d.consts.push_back(S[k].val);
+        } else {
+            d.sym.push_back(k);
+        }
+    }
+    for (auto& kv : by_arr.items) {
+        const Arr& d = kv.second;
+        if (d.sym.empty() || d.consts.empty()) continue;
+        struct Base { int base; U lo, hi; int64_t off; std::vector<std::pair<int, U>> keys; int size; };
+        OMap<int, Base> bases;
+        bool ok = true;
+        for (int k : d.sym) {
+            int base;
+            U c;
+            if (!split_add(S, k, base, c) || nz(shr(c, 32))) { ok = false; break; }
+            Base* r = bases.find(base);
+            if (!r) {
+                int64_t off = 0;
+                int size = -1;
+                if (!word_of(S, base, d.arr, off, size)) { ok = false; break; }
+                r = &bases.setdefault(base, Base{base, c, c, off, {}, size});
+            }
+            r->lo = umin(r->lo, c);
+            r->hi = umax(r->hi, c);
+            r->keys.push_back({k, c});
+        }
+        if (!ok) continue;
+        int size_var = -1;
+        U nxt = std::max_element(d.consts.begin(), d.consts.end())->low384() + U::of(1);
+        std::vector<std::pair<int64_t, int>> cells;           // insertion-ordered (dict)
+        auto set_cell = [&](int64_t o, int b) {
+            for (auto& c : cells) if (c.first == o) { c.second = b; return; }
+            cells.push_back({o, b});
+        };
+        for (auto& bv : bases.items) {
+            const Base& b = bv.second;
+            U val = shl(sar(nxt - b.lo + U::of(31), 5), 5);    // 32-aligned, past nxt
+            for (int i = 0; i < 32; i++) set_cell(b.off + i, (int)(sar(val, 8 * (31 - i)).w[0] & 0xFF));
+            for (auto& kc : b.keys) out.subst.push_back({kc.first, (val + kc.second) & mask(S[kc.first].width)});
+            nxt = val + b.hi + U::of(1);
+            if (size_var < 0) size_var = b.size;
+        }
+        if (size_var >= 0) {
+            out.vars.push_back({S[size_var].str, nxt});
+            out.subst.push_back({size_var, nxt & mask(S[size_var].width)});
+        }
+        out.arrays.push_back({S[d.arr].str, cells});
+        for (int n : nodes) {
+            if (S[n].op != S_SELECT || S[n].args[0] != d.arr || S[S[n].args[1]].op != S_BVNUM) continue;
+            const Big& v = S[S[n].args[1]].val;
+            if (v.l.size() > 2) continue;
+            int64_t o = (int64_t)(v.l.empty() ? 0 : v.l[0]) | (v.l.size() > 1 ? (int64_t)v.l[1] << 32 : 0);
+            for (auto& c : cells)
+                if (c.first == o) { out.subst.push_back({n, U::of((uint64_t)c.second) & mask(S[n].width)}); break; }
+        }
+    }
+    return !out.arrays.empty();
+}
+
+// ---------------------------------------------------------------------------
 // JSON output
 // ---------------------------------------------------------------------------
 static void jstr(std::string& o, const std::string& s) {
@@ -2376,6 +2578,23 @@ static void compile(const mgc_input* in, mgc_result* res) {
     for (int p : probes) if (p < 0 || p >= in->n_nodes) throw std::runtime_error("probe index");
     std::vector<int> all = cons;
     all.insert(all.end(), probes.begin(), probes.end());
+
+    std::vector<U> hints;
+    if (in->search_hints) harvest_hints(S, cons, hints);
+    Presets presets;
+    bool have_presets = in->abi_presets && abi_plan(S, cons, presets);
+    if (have_presets) {
+        // the query under the presets (Plan.view): each pinned node becomes
+        // the numeral, keeping its id
+        for (auto& su : presets.subst) {
+            Src& s = S[su.first];
+            s.op = S_BVNUM;
+            s.args.clear();
+            s.str.clear();
+            s.p0 = s.p1 = 0;
+            s.val = big_of(su.second);
+        }
+    }
 
     Lowerer lw(S, in->default_entries);
     for (int t = 0; t < in->n_tables; t++) lw.table_sizes.put(strings.at(in->table_name[t]), in->table_size[t]);
@@ -2465,6 +2684,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
         for (int j = 0; j < 8; j++) v.w[j / 2] |= (uint64_t)in->extra[8 * i + j] << (32 * (j & 1));
         const_values.push_back(v);
     }
+    for (auto& h : hints) const_values.push_back(h & M256);
     std::sort(const_values.begin(), const_values.end());
     const_values.erase(std::unique(const_values.begin(), const_values.end()), const_values.end());
     std::unordered_map<U, int, UHash> const_index;
@@ -2481,13 +2701,11 @@ static void compile(const mgc_input* in, mgc_result* res) {
     }
     std::vector<U> table = const_values;
     std::vector<std::pair<int, int>> pool_ranges;
-    std::vector<std::pair<int, int>> leaf_pool(lw.leaves.size(), {-1, 0});
     if (in->leaf_pools) {
         auto pools = leaf_pools(lw.ln, order, lw.leaves);
         for (size_t li = 0; li < pools.size(); li++) {
             if (!pools[li].empty()) {
                 pool_ranges.push_back({(int)table.size(), (int)pools[li].size()});
-                leaf_pool[li] = {(int)table.size(), (int)pools[li].size()};
                 table.insert(table.end(), pools[li].begin(), pools[li].end());
             } else {
                 pool_ranges.push_back({0, (int)const_values.size()});
@@ -2512,8 +2730,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
         jstr(o, KIND_NAMES[L.kind]);
         o += ",";
         jstr(o, L.source);
-        o += "," + std::to_string(L.chunk) + "," + std::to_string(L.entry) + "," +
-             std::to_string(leaf_pool[i].first) + "," + std::to_string(leaf_pool[i].second) + "]";
+        o += "," + std::to_string(L.chunk) + "," + std::to_string(L.entry) + "]";
     }
     o += "],\"n_lds\":" + std::to_string(al.n_lds);
     o += ",\"n_probes\":" + std::to_string(probe_chunks);
@@ -2616,7 +2833,33 @@ static void compile(const mgc_input* in, mgc_result* res) {
         }
         o += "]]";
     }
-    o += "],\"n_user_probes\":" + std::to_string(n_user_probes) + "}";
+    o += "],\"n_user_probes\":" + std::to_string(n_user_probes);
+    if (have_presets) {
+        o += ",\"presets\":{\"vars\":[";
+        for (size_t i = 0; i < presets.vars.size(); i++) {
+            if (i) o += ",";
+            o += "[";
+            jstr(o, presets.vars[i].first);
+            o += ",";
+            jstr(o, (presets.vars[i].second.neg() ? "-" + hex(U() - presets.vars[i].second) : hex(presets.vars[i].second)));
+            o += "]";
+        }
+        o += "],\"arrays\":[";
+        for (size_t i = 0; i < presets.arrays.size(); i++) {
+            if (i) o += ",";
+            o += "[";
+            jstr(o, presets.arrays[i].first);
+            o += ",[";
+            for (size_t j = 0; j < presets.arrays[i].second.size(); j++) {
+                if (j) o += ",";
+                o += "[" + std::to_string(presets.arrays[i].second[j].first) + "," +
+                     std::to_string(presets.arrays[i].second[j].second) + "]";
+            }
+            o += "]]";
+        }
+        o += "]}";
+    }
+    o += "}";
 }
 
 }  // namespace

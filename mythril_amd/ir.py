@@ -87,7 +87,6 @@ class Leaf:
     source: str
     chunk: int = 0
     entry: int = 0
-    pool: Tuple[int, ...] = ()
 
 
 @dataclass
@@ -951,6 +950,21 @@ def scan_const_keys(nodes: Sequence[Node], cap: int = CKEY_CAP,
     return ck
 
 
+def harvest_hints(nodes: Sequence[Node]) -> List[int]:
+    """Extra candidate values: every numeral of the query rounded up to a
+    multiple of 64 (the keccak UF outputs are constrained to 64-aligned
+    intervals, keccak_function_manager.py:136-140) and byte-shifted selector
+    constants (calldata words are Concats of bytes)."""
+    out = set()
+    for n in topo_order(list(nodes)):
+        if n.op == "bvnum" and n.width >= 8:
+            v = n.params[0]
+            out.add((v + 63) & ~63)
+            if 0 < v < (1 << 32):
+                out.add(v << 224)       # 4-byte selector in the top of a word
+    return sorted(out)
+
+
 def lw_tables(constraints, probes) -> set:
     """Names of every free array / UF the nodes read."""
     out = set()
@@ -972,22 +986,26 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
                         extra_consts: Sequence[int] = (), leaf_pools: bool = False,
-                        const_keys: bool = False, solve: bool = False) -> Program:
+                        const_keys: bool = False, solve: bool = False, search_hints: bool = False,
+                        abi_presets: bool = False) -> Program:
     """Compile constraints (see :func:`compile_constraints_py`) with the
     compiler ``COMPILER`` names."""
     if COMPILER == "py":
         return compile_constraints_py(constraints, probes, table_sizes, default_entries, nreg,
-                                      extra_consts, leaf_pools, const_keys, solve)
+                                      extra_consts, leaf_pools, const_keys, solve, search_hints,
+                                      abi_presets)
     from .ccompile import compile_native
     return compile_native(constraints, probes, table_sizes, default_entries, nreg, extra_consts,
-                          leaf_pools, const_keys, solve)
+                          leaf_pools, const_keys, solve, search_hints=search_hints,
+                          abi_presets=abi_presets)
 
 
 def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] = (),
                            table_sizes: Optional[Dict[str, int]] = None,
                            default_entries: int = 2, nreg: int = I.NREG,
                            extra_consts: Sequence[int] = (), leaf_pools: bool = False,
-                           const_keys: bool = False, solve: bool = False) -> Program:
+                           const_keys: bool = False, solve: bool = False,
+                           search_hints: bool = False, abi_presets: bool = False) -> Program:
     """Compile Bool constraint nodes (their conjunction is the root bit) and
     optional probe nodes (256-bit values written per assignment).  ``nreg``
     is the library's register-file size (``Engine.nreg``); ``extra_consts``
@@ -1004,7 +1022,19 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
     (``_Lowerer._table``) and model construction (``mythril_amd/solve.py``);
     the computed model values come out as probes (``Program.derived`` /
     ``entry_keys``), so such a program is for search, not for evaluating
-    caller-supplied assignments."""
+    caller-supplied assignments.  ``search_hints`` adds the constraints'
+    numerals as candidates (:func:`harvest_hints`); ``abi_presets`` pins the
+    ABI offset words of calldata read at symbolic offsets (``abi.plan``) and
+    compiles the query under them (``Plan.view``, ``Program.presets``)."""
+    constraints, probes = list(constraints), list(probes)
+    if search_hints:
+        extra_consts = list(extra_consts) + harvest_hints(constraints)
+    plan = None
+    if abi_presets:
+        from . import abi
+        plan = abi.plan(constraints)
+        if plan is not None:
+            constraints, probes = plan.view(constraints), plan.view(probes)
     lw = _Lowerer(table_sizes or {}, default_entries)
     lw.solve = solve
     if const_keys or solve:
@@ -1090,7 +1120,6 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
             if p:
                 pool_ranges.append((len(table), len(p)))
                 table.extend(p)
-                lw.leaves[li].pool = tuple(p)
             else:
                 pool_ranges.append((0, len(const_values)))
     consts = np.frombuffer(b"".join(v.to_bytes(32, "little") for v in table),
@@ -1105,6 +1134,9 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
     for name in lw.solve_tables & set(lw.table_kinds):
         # no leaf-keyed entries: the model's entries are the argument-keyed ones
         tsizes[name] = len(lw.arg_entries.get(name, ()))
-    return Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
+    prog = Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
                    len(constraints), tsizes, lw.table_kinds, ckeys, stats, pool_ranges,
                    derived, entry_keys, n_user_probes)
+    if plan is not None:
+        prog.presets = plan
+    return prog

@@ -34,7 +34,7 @@ from typing import Dict, List, Optional, Sequence
 from . import z3bridge
 from .assign import Assignment, unpack
 from .engine import EngineError, EngineUnavailable, LeafGen, get_engine
-from .ir import Program, Unsupported, compile_constraints
+from .ir import Program, Unsupported, compile_constraints, harvest_hints  # noqa: F401
 from .smt import node as N
 
 log = logging.getLogger(__name__)
@@ -320,23 +320,16 @@ def _compile_search_uncached(nodes: Sequence[N.Node], probes: Sequence[N.Node] =
     its argument-keyed entries keep too many values live for the spill
     budget — the plain search form (every model value generated).
     ``probes`` are evaluated under each candidate's model."""
-    from . import abi
-    hints = harvest_hints(nodes)
-    plan = abi.plan(nodes)
     try:
-        if plan is not None:
-            # ABI offsets pinned (abi.py): a witness carries the presets
-            prog = compile_constraints(plan.apply(nodes), plan.apply(probes), extra_consts=hints,
-                                       leaf_pools=True, const_keys=True, solve=True)
-            prog.presets = plan
-            return prog
-        return compile_constraints(nodes, probes, extra_consts=hints, leaf_pools=True,
-                                   const_keys=True, solve=True)
+        # candidate hints from the query's numerals, ABI offsets pinned
+        # (abi.py: a witness carries the presets, Program.presets)
+        return compile_constraints(nodes, probes, leaf_pools=True, const_keys=True, solve=True,
+                                   search_hints=True, abi_presets=True)
     except Unsupported as e:
         if "spill budget" not in str(e):
             raise
-        return compile_constraints(nodes, probes, extra_consts=hints, leaf_pools=True,
-                                   const_keys=True)
+        return compile_constraints(nodes, probes, leaf_pools=True, const_keys=True,
+                                   search_hints=True)
 
 
 def _witness(eng, lp, hit) -> Assignment:
@@ -348,21 +341,6 @@ def _witness(eng, lp, hit) -> Assignment:
         leaves, probes = eng.witness(lp, SEARCH_SEED, idx)
         return unpack(prog, leaves, probes)
     return unpack(prog, leaves)
-
-
-def harvest_hints(nodes: Sequence[N.Node]) -> List[int]:
-    """Extra candidate values: every numeral of the query rounded up to a
-    multiple of 64 (the keccak UF outputs are constrained to 64-aligned
-    intervals, keccak_function_manager.py:136-140) and byte-shifted selector
-    constants (calldata words are Concats of bytes)."""
-    out = set()
-    for n in N.topo_order(list(nodes)):
-        if n.op == "bvnum" and n.width >= 8:
-            v = n.params[0]
-            out.add((v + 63) & ~63)
-            if 0 < v < (1 << 32):
-                out.add(v << 224)       # 4-byte selector in the top of a word
-    return sorted(out)
 
 
 _SYMS: "Dict[int, frozenset]" = {}
@@ -390,7 +368,25 @@ def dependence_buckets(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
     arrays and uninterpreted functions counted as symbols too (the reference
     only counts expression leaves; a GPU witness is a joint table per array /
     UF, so two groups reading one table are not independent here).  Groups
-    keep the constraints' order; a symbol-free constraint is its own group."""
+    keep the constraints' order; a symbol-free constraint is its own group.
+    The native front-end computes the same partition in one walk
+    (``_mythcc.buckets``); :func:`dependence_buckets_py` is its
+    specification."""
+    from . import ir
+    if ir.COMPILER != "py":
+        from .ccompile import buckets
+        nodes = list(nodes)
+        out: List[List[N.Node]] = []
+        for c, g in zip(nodes, buckets(nodes)):
+            if g == len(out):
+                out.append([])
+            out[g].append(c)
+        return out
+    return dependence_buckets_py(nodes)
+
+
+def dependence_buckets_py(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
+    """:func:`dependence_buckets` in Python (the specification)."""
     parent: Dict[object, object] = {}
 
     def find(k):

@@ -25,6 +25,9 @@ def _same(a, b):
               "table_ckeys", "pool_ranges", "derived", "entry_keys", "n_user_probes", "stats"):
         assert getattr(a, f) == getattr(b, f), f
     assert a.leaves == b.leaves
+    assert (a.presets is None) == (b.presets is None)
+    if a.presets is not None:
+        assert (a.presets.vars, a.presets.arrays) == (b.presets.vars, b.presets.arrays)
 
 
 def _both(cons, probes=(), **kw):
@@ -68,18 +71,20 @@ def test_corpus_dags_identical():
 def test_query_streams_identical(workload):
     """Every group get_model searches (solve mode, with the ABI presets and
     hints _compile_search_uncached adds) and its eval form."""
-    from mythril_amd import abi, workloads as W
+    from mythril_amd import workloads as W
     import mythril_amd.model as M
-    n = 0
+    n = presets = 0
     for q in W.queries(workload, 12):
         for b in M.dependence_buckets(q):
-            hints = M.harvest_hints(b)
-            plan = abi.plan(b)
-            nodes = plan.apply(b) if plan is not None else b
-            _both(nodes, (), extra_consts=hints, leaf_pools=True, const_keys=True, solve=True)
+            p = _both(b, (), leaf_pools=True, const_keys=True, solve=True, search_hints=True,
+                      abi_presets=True)
+            presets += p is not None and p.presets is not None
+            _both(b, (), leaf_pools=True, const_keys=True, search_hints=True)
             _both(b)
             n += 1
     assert n >= 12
+    if workload == "c3":
+        assert presets > 0          # BECToken batchTransfer reads _receivers at ABI offsets
 
 
 def test_unsupported_and_errors():
@@ -123,3 +128,31 @@ def test_malformed_input_is_an_error_not_a_crash():
     assert lib.mgc_compile(ctypes.byref(inp), ctypes.byref(res)) == 2
     assert b"order" in lib.mgc_error(res)
     lib.mgc_free(res)
+
+
+def test_c_abi_path_identical():
+    """The plain C ABI (Python-flattened mgc_input over ctypes) and the
+    CPython front-end compile the same program."""
+    from mythril_amd.ccompile import compile_native_ctypes
+    from mythril_amd import workloads as W
+    import mythril_amd.model as M
+    import dag_cases
+    for name, (c, p, _, ts) in list(dag_cases.named_cases().items())[:6]:
+        _same(compile_native(c, p, table_sizes=ts or None), compile_native_ctypes(c, p, table_sizes=ts or None))
+    for q in W.queries("c4", 3):
+        for b in M.dependence_buckets(q):
+            kw = dict(leaf_pools=True, const_keys=True, solve=True, search_hints=True, abi_presets=True)
+            _same(compile_native(b, (), **kw), compile_native_ctypes(b, (), **kw))
+
+
+def test_native_buckets_match_the_python_partition():
+    from mythril_amd import workloads as W
+    import mythril_amd.model as M
+    import dag_cases
+    qs = [q for wl in ("c1", "c3", "c4") for q in W.queries(wl, 8)]
+    qs += [c for c, _, _, _ in dag_cases.named_cases().values() if c]
+    for q in qs:
+        q = list(q) + list(q[:2])                 # repeated entries too
+        got = M.dependence_buckets(q)
+        want = M.dependence_buckets_py(q)
+        assert [[c.id for c in g] for g in got] == [[c.id for c in g] for g in want]
