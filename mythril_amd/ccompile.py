@@ -136,9 +136,10 @@ def compile_native(constraints: Sequence, probes: Sequence = (),
                     json.loads(meta))
 
 
-def buckets(constraints: Sequence) -> List[int]:
-    """Independent-group label of each constraint (labels in order of first
-    occurrence), model.dependence_buckets' partition computed natively."""
+def buckets(constraints: Sequence):
+    """(independent-group label of each constraint, labels in order of first
+    occurrence; DAG nodes per group): model.dependence_buckets' partition
+    computed natively, with the size the compile-cost gate estimates from."""
     return _load_ext().buckets(list(constraints))
 
 

@@ -265,8 +265,10 @@ PyObject* py_compile(PyObject*, PyObject* a) {
     return out;
 }
 
-// _mythcc.buckets(constraints) -> group label per constraint (labels in
-// order of first occurrence): constraints share a group iff they share a
+// _mythcc.buckets(constraints) -> (group label per constraint (labels in
+// order of first occurrence), DAG nodes per group (symbol-bearing nodes of
+// the group; 1 for a symbol-free constraint) — the compile-cost estimate of
+// model.gpu_search): constraints share a group iff they share a
 // free symbol — a variable by name, an array / uninterpreted function by
 // name (mythril_amd/model.py dependence_buckets, the reference's
 // IndependenceSolver DependenceMap, independence_solver.py:38-84).  One
@@ -364,21 +366,32 @@ PyObject* py_buckets(PyObject*, PyObject* a) {
     }
     PyObject* out = PyList_New(nc);
     std::unordered_map<int, long> label;
+    std::unordered_map<int, long> per_root;           // symbol-bearing nodes per set
+    for (auto& kv : idx) if (has_sym[kv.second]) per_root[uf.find(kv.second)]++;
+    std::vector<long> sizes;
     for (Py_ssize_t i = 0; i < nc; i++) {
         int e = idx.at(PySequence_Fast_GET_ITEM(seq, i));
         long l;
         if (!has_sym[e]) {
             l = (long)label.size();
             label[-1 - (int)i] = l;                     // symbol-free: a group of its own
+            sizes.push_back(1);
         } else {
             int root = uf.find(e);
             auto it = label.find(root);
-            l = it == label.end() ? (label[root] = (long)label.size()) : it->second;
+            if (it == label.end()) {
+                l = label[root] = (long)label.size();
+                sizes.push_back(per_root[root]);
+            } else {
+                l = it->second;
+            }
         }
         PyList_SET_ITEM(out, i, PyLong_FromLong(l));
     }
     Py_DECREF(seq);
-    return out;
+    PyObject* sz = PyList_New((Py_ssize_t)sizes.size());
+    for (size_t g = 0; g < sizes.size(); g++) PyList_SET_ITEM(sz, (Py_ssize_t)g, PyLong_FromLong(sizes[g]));
+    return Py_BuildValue("(NN)", out, sz);
 }
 
 PyMethodDef methods[] = {

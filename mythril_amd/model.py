@@ -372,17 +372,25 @@ def dependence_buckets(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
     The native front-end computes the same partition in one walk
     (``_mythcc.buckets``); :func:`dependence_buckets_py` is its
     specification."""
+    return dependence_buckets_sized(nodes)[0]
+
+
+def dependence_buckets_sized(nodes: Sequence[N.Node]):
+    """(:func:`dependence_buckets`, DAG nodes per group) — the size is what
+    the compile-cost gate prices (``COMPILE_MS_PER_NODE``)."""
     from . import ir
+    nodes = list(nodes)
     if ir.COMPILER != "py":
         from .ccompile import buckets
-        nodes = list(nodes)
+        labels, sizes = buckets(nodes)
         out: List[List[N.Node]] = []
-        for c, g in zip(nodes, buckets(nodes)):
+        for c, g in zip(nodes, labels):
             if g == len(out):
                 out.append([])
             out[g].append(c)
-        return out
-    return dependence_buckets_py(nodes)
+        return out, sizes
+    out = dependence_buckets_py(nodes)
+    return out, [len(N.topo_order(b)) for b in out]
 
 
 def dependence_buckets_py(nodes: Sequence[N.Node]) -> List[List[N.Node]]:
@@ -521,9 +529,12 @@ GROUP_MISS_SIZE = 1 << 14
 SUPERSET_SKIP = True
 _group_miss: "Dict[frozenset, int]" = {}
 _miss_index: "Dict[int, List[frozenset]]" = {}
-# compile-cost gate: estimated host compile time per source node of an
-# uncached group (Python compiler; measured ~0.035 ms/node on C3/C4 queries)
-COMPILE_MS_PER_NODE = 0.04
+# compile-cost gate: estimated host compile time per DAG node of an uncached
+# group — native compiler: 2.5 ms for the ~990-node C3 queries on the GPU
+# box (profiles/r03/search_r3_native.log); the Python one (MYTHRIL_GPU_
+# COMPILER=py) measured ~0.035 ms/node
+COMPILE_MS_PER_NODE = 0.004
+COMPILE_MS_PER_NODE_PY = 0.04
 
 
 def _group_key(nodes: Sequence[N.Node]) -> frozenset:
@@ -616,12 +627,11 @@ def clear_search_memos() -> None:
     _shape_stats.clear()
 
 
-def _compile_estimate_ms(buckets, keys) -> float:
+def _compile_estimate_ms(buckets, sizes) -> float:
+    from . import ir
     cache = _SEARCH_CACHE or {}
-    todo = [b for b, k in zip(buckets, keys) if (tuple(n.id for n in b), ()) not in cache]
-    if not todo:
-        return 0.0
-    return COMPILE_MS_PER_NODE * len(N.topo_order([n for b in todo for n in b]))
+    n = sum(sz for b, sz in zip(buckets, sizes) if (tuple(c.id for c in b), ()) not in cache)
+    return n * (COMPILE_MS_PER_NODE_PY if ir.COMPILER == "py" else COMPILE_MS_PER_NODE)
 
 
 def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
@@ -633,7 +643,7 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     no host round trip (mg_search / mg_batch_search).  The group-miss memo
     answers repeated (or extended) missed groups at once, and a query whose
     estimated compile time exceeds the budget is not searched."""
-    buckets = dependence_buckets(nodes)
+    buckets, sizes = dependence_buckets_sized(nodes)
     keys = [_group_key(b) for b in buckets]
     if any(_known_miss(k, SEARCH_CANDIDATES) for k in keys):
         stats.memo_misses += 1
@@ -642,7 +652,7 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     if not _shape_gate(shape):
         stats.shape_skipped += 1
         return None
-    if _compile_estimate_ms(buckets, keys) > budget_ms:
+    if _compile_estimate_ms(buckets, sizes) > budget_ms:
         stats.gated += 1
         return None
     with _Phase("compile"):
