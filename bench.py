@@ -81,14 +81,28 @@ def build_corpus(n_dags, workers, dag_ids=None, workload="c2", start="fork"):
         return sorted(pool.map(compile_unit, items, chunksize=16), key=lambda t: t[0])
 
 
-def kernel_key(lib_digest, workload, dags, assign_log2, jit):
+def programs_digest(corpus) -> str:
+    """Digest of the IR programs themselves (instructions and constant
+    tables, in DAG order): whichever compiler built them, the same digest
+    means the same programs."""
+    import hashlib
+    h = hashlib.sha1()
+    for dag_id, prog, _, _ in sorted(corpus, key=lambda u: u[0]):
+        h.update(b"%d:" % dag_id + prog.code.tobytes() + prog.consts.tobytes())
+    return h.hexdigest()[:16]
+
+
+def kernel_key(lib_digest, workload, dags, assign_log2, jit, corpus=None):
     """What a traffic measurement (profiles/traffic.json) is valid for: the
     generated assembly, the allocator's leaf policy, the code path (and for
-    compiled programs the digest of the sources that generate them) and the
-    workload.  bench.py reports ``traffic`` only when every field matches."""
+    compiled programs the digest of the sources that specialise them), the
+    workload and the programs evaluated (``programs_digest``).  bench.py
+    reports ``traffic`` only when every field matches."""
     from mythril_amd import ir
     key = {"asm_digest": lib_digest, "leaf_remat": ir.LEAF_REMAT, "jit": bool(jit),
            "workload": workload, "dags": dags, "assign_log2": assign_log2}
+    if corpus is not None:
+        key["programs"] = programs_digest(corpus)
     if jit:                           # the compiled programs' own code
         from mythril_amd import jit as J
         key["jit_code"] = J.code_digest()
@@ -302,7 +316,7 @@ def main():
         ops_launch = weight_per_lane * n_assign
         achieved = ops_launch / (kern_ms / 1000.0)
         key = kernel_key(eng.lib.mg_asm_digest().decode(), args.workload, args.dags,
-                         args.assign_log2, args.jit)
+                         args.assign_log2, args.jit, corpus)
         traffic, traffic_note = None, "no profiles/traffic.json"
         if os.path.exists(args.traffic_json):
             try:

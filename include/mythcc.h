@@ -34,6 +34,8 @@ extern "C" {
 #define MGC_UNSUPPORTED 1      /* the group needs z3 (ir.Unsupported)          */
 #define MGC_ERROR 2            /* malformed input / internal error            */
 
+#define MGC_MAX_SOURCE_WIDTH 65536   /* widths outside [1, this] are rejected */
+
 #define MGC_SORT_BV 0
 #define MGC_SORT_BOOL 1
 #define MGC_SORT_ARRAY 2
@@ -86,6 +88,8 @@ typedef struct mgc_input {
      *   metadata ("presets"). */
     int32_t search_hints;
     int32_t abi_presets;
+    int32_t n_cval;            /* length of cval (limbs)                       */
+    int32_t n_string_bytes;    /* length of strings (bytes)                    */
 } mgc_input;
 
 typedef struct mgc_result mgc_result;

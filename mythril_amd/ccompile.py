@@ -52,7 +52,8 @@ class _Input(ctypes.Structure):
          ("leaf_pools", ctypes.c_int32), ("const_keys", ctypes.c_int32), ("solve", ctypes.c_int32),
          ("remat_mode", ctypes.c_int32), ("remat_k", ctypes.c_int32),
          ("keep_clean", ctypes.c_int32), ("search_hints", ctypes.c_int32),
-         ("abi_presets", ctypes.c_int32)]
+         ("abi_presets", ctypes.c_int32), ("n_cval", ctypes.c_int32),
+         ("n_string_bytes", ctypes.c_int32)]
 
 
 def load():
@@ -143,24 +144,20 @@ def buckets(constraints: Sequence):
     return _load_ext().buckets(list(constraints))
 
 
-def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
-                          table_sizes: Optional[Dict[str, int]] = None, default_entries: int = 2,
-                          nreg: int = I.NREG, extra_consts: Sequence[int] = (),
-                          leaf_pools: bool = False, const_keys: bool = False, solve: bool = False,
-                          leaf_remat: Optional[str] = None, keep_clean: Optional[bool] = None,
-                          search_hints: bool = False, abi_presets: bool = False):
-    """The same compile through the plain C ABI (libmythcc.so, ctypes): the
-    DAG flattened in Python into mgc_input arrays — what another FFI host
-    does (INTEGRATION.md)."""
-    from . import ir
-    lib = load()
+def flatten(constraints: Sequence, probes: Sequence = (),
+            table_sizes: Optional[Dict[str, int]] = None, extra_consts: Sequence[int] = ()):
+    """The mgc_input arrays of a DAG, built in Python (what another FFI host
+    does): node arrays in topological order, the numerals' limbs, the
+    NUL-separated names, constraint / probe / table indices, extra
+    constants as 32-byte rows."""
+    load()
     constraints, probes = list(constraints), list(probes)
     nodes = topo_order(constraints + probes)
     index = {n.id: i for i, n in enumerate(nodes)}
     ops, OTHER = _OPS, _OTHER
-    op_a, sort_a, width_a, dom_a, str_a, cv_a = (array("i") for _ in range(6))
-    id_a, p0_a, p1_a = array("q"), array("q"), array("q")
-    off_a, args_a = array("i", [0]), array("i")
+    f = {k: array("i") for k in ("op", "sort", "width", "dom", "str", "cval_off", "args")}
+    f.update({k: array("q") for k in ("id", "p0", "p1")})
+    f["arg_off"] = array("i", [0])
     cval = bytearray()
     strings: List[str] = []
     sidx: Dict[str, int] = {}
@@ -174,14 +171,14 @@ def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
     for n in nodes:
         op = n.op
         code = ops.get(op, OTHER)
-        op_a.append(code)
-        sort_a.append(_SORT[n.sort])
-        width_a.append(n.width)
-        dom_a.append(n.dom or 0)
-        id_a.append(n.id)
+        f["op"].append(code)
+        f["sort"].append(_SORT[n.sort])
+        f["width"].append(n.width)
+        f["dom"].append(n.dom or 0)
+        f["id"].append(n.id)
         for a in n.args:
-            args_a.append(index[a.id])
-        off_a.append(len(args_a))
+            f["args"].append(index[a.id])
+        f["arg_off"].append(len(f["args"]))
         p0 = p1 = 0
         s = -1
         c = -1
@@ -200,30 +197,48 @@ def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
             p0 = pr[0]
         elif code == OTHER:
             s = intern(op)
-        p0_a.append(p0)
-        p1_a.append(p1)
-        str_a.append(s)
-        cv_a.append(c)
-    cons_a = array("i", [index[c.id] for c in constraints])
-    probes_a = array("i", [index[p.id] for p in probes])
+        f["p0"].append(p0)
+        f["p1"].append(p1)
+        f["str"].append(s)
+        f["cval_off"].append(c)
+    f["cons"] = array("i", [index[c.id] for c in constraints])
+    f["probes"] = array("i", [index[p.id] for p in probes])
     tsz = table_sizes or {}
-    tname_a = array("i", [intern(k) for k in tsz])
-    tsize_a = array("i", list(tsz.values()))
+    f["table_name"] = array("i", [intern(k) for k in tsz])
+    f["table_size"] = array("i", list(tsz.values()))
     M = (1 << 256) - 1
-    extra = bytearray(b"".join((v & M).to_bytes(32, "little") for v in extra_consts))
-    blob = b"".join(s.encode() + b"\0" for s in strings)
+    f["extra"] = bytearray(b"".join((v & M).to_bytes(32, "little") for v in extra_consts))
+    f["cval"] = bytearray(cval)
+    f["strings"] = b"".join(s.encode() + b"\0" for s in strings)
+    f["n_nodes"], f["n_strings"] = len(nodes), len(strings)
+    return f
+
+
+def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
+                          table_sizes: Optional[Dict[str, int]] = None, default_entries: int = 2,
+                          nreg: int = I.NREG, extra_consts: Sequence[int] = (),
+                          leaf_pools: bool = False, const_keys: bool = False, solve: bool = False,
+                          leaf_remat: Optional[str] = None, keep_clean: Optional[bool] = None,
+                          search_hints: bool = False, abi_presets: bool = False):
+    """The same compile through the plain C ABI (libmythcc.so, ctypes): the
+    DAG flattened in Python (:func:`flatten`) into mgc_input arrays — what
+    another FFI host does."""
+    from . import ir
+    lib = load()
+    f = flatten(constraints, probes, table_sizes, extra_consts)
     remat = leaf_remat or ir.LEAF_REMAT
     mode = _REMAT.get(remat, 1)
     k = int(remat[7:]) if mode == 1 and remat[7:].isdigit() else 0
-    cval_buf = bytearray(cval)
-    inp = _Input(len(nodes), _ptr(op_a), _ptr(sort_a), _ptr(width_a), _ptr(dom_a), _ptr(id_a),
-                 _ptr(off_a), _ptr(args_a), _ptr(p0_a), _ptr(p1_a), _ptr(str_a), _ptr(cv_a),
-                 _ptr(cval_buf), blob, len(strings), len(cons_a), _ptr(cons_a),
-                 len(probes_a), _ptr(probes_a), len(tname_a), _ptr(tname_a), _ptr(tsize_a),
-                 default_entries, nreg, len(extra) // 32, _ptr(extra),
-                 int(leaf_pools), int(const_keys), int(solve), mode, k,
-                 int(ir.KEEP_CLEAN if keep_clean is None else keep_clean), int(search_hints),
-                 int(abi_presets))
+    P = {n: _ptr(f[n]) for n in ("op", "sort", "width", "dom", "id", "arg_off", "args", "p0", "p1",
+                                  "str", "cval_off", "cval", "cons", "probes", "table_name",
+                                  "table_size", "extra")}
+    inp = _Input(f["n_nodes"], P["op"], P["sort"], P["width"], P["dom"], P["id"], P["arg_off"],
+                 P["args"], P["p0"], P["p1"], P["str"], P["cval_off"], P["cval"], f["strings"],
+                 f["n_strings"], len(f["cons"]), P["cons"], len(f["probes"]), P["probes"],
+                 len(f["table_name"]), P["table_name"], P["table_size"], default_entries, nreg,
+                 len(f["extra"]) // 32, P["extra"], int(leaf_pools), int(const_keys), int(solve),
+                 mode, k, int(ir.KEEP_CLEAN if keep_clean is None else keep_clean),
+                 int(search_hints), int(abi_presets), len(f["cval"]) // 4, len(f["strings"]))
     res = ctypes.c_void_p()
     rc = lib.mgc_compile(ctypes.byref(inp), ctypes.byref(res))
     try:

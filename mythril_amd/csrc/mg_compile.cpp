@@ -77,7 +77,9 @@ static U operator*(const U& a, const U& b) {
     }
     return r;
 }
+struct BadShift : std::runtime_error { BadShift() : std::runtime_error("negative shift") {} };
 static U shl(const U& a, int k) {
+    if (k < 0) throw BadShift();
     U r; if (k >= 64 * U::N) return r;
     int q = k >> 6, s = k & 63;
     for (int i = U::N - 1; i >= q; i--) {
@@ -88,6 +90,7 @@ static U shl(const U& a, int k) {
     return r;
 }
 static U shr(const U& a, int k) {      // logical
+    if (k < 0) throw BadShift();
     U r; if (k >= 64 * U::N) return r;
     int q = k >> 6, s = k & 63;
     for (int i = 0; i + q < U::N; i++) {
@@ -2544,33 +2547,85 @@ struct mgc_result {
 namespace {
 
 static void compile(const mgc_input* in, mgc_result* res) {
-    // -- decode the source DAG ---------------------------------------------------
+    // -- decode and check the source DAG ----------------------------------------
+    // (the C ABI takes arrays from any caller: every index, count and width
+    // is checked before use, so a malformed DAG is an error, never a wild
+    // access — tests/fuzz_compile.cpp runs mutated inputs under ASan/UBSan)
+    auto bad = [](const char* what) { throw std::runtime_error(what); };
+    if (in->n_nodes < 0 || in->n_cons < 0 || in->n_probes < 0 || in->n_strings < 0 ||
+        in->n_tables < 0 || in->n_extra < 0 || in->n_cval < 0 || in->n_string_bytes < 0)
+        bad("negative count");
+    if (in->n_nodes && (!in->op || !in->sort || !in->width || !in->dom || !in->id || !in->arg_off ||
+                        !in->p0 || !in->p1 || !in->str || !in->cval_off))
+        bad("missing node array");
+    if ((in->n_cons && !in->cons) || (in->n_probes && !in->probes) ||
+        (in->n_tables && (!in->table_name || !in->table_size)) || (in->n_extra && !in->extra) ||
+        (in->n_cval && !in->cval) || (in->n_string_bytes && !in->strings))
+        bad("missing array");
+    if (in->nreg < 2 || in->nreg > 256 || in->default_entries < 0 || in->default_entries > 4096)
+        bad("nreg / default_entries out of range");
     std::vector<std::string> strings;
     {
         const char* p = in->strings;
-        for (int i = 0; i < in->n_strings; i++) { strings.emplace_back(p); p += strings.back().size() + 1; }
+        const char* end = in->strings + in->n_string_bytes;
+        for (int i = 0; i < in->n_strings; i++) {
+            const char* z = p < end ? (const char*)std::memchr(p, 0, (size_t)(end - p)) : nullptr;
+            if (!z) bad("string table overrun");
+            strings.emplace_back(p, (size_t)(z - p));
+            p = z + 1;
+        }
     }
+    if (in->n_nodes && in->arg_off[0] != 0) bad("arg_off[0] != 0");
     std::vector<Src> S(in->n_nodes);
     for (int i = 0; i < in->n_nodes; i++) {
         Src& s = S[i];
         s.op = in->op[i]; s.sort = in->sort[i]; s.width = in->width[i]; s.dom = in->dom[i];
         s.id = in->id[i];
+        if (s.op < 0 || s.op > S_OTHER) bad("bad op code");
+        if (s.sort < 0 || s.sort > MGC_SORT_ARRAY) bad("bad sort");
+        if (s.width < 1 || s.width > MGC_MAX_SOURCE_WIDTH || s.dom < 0 || s.dom > MGC_MAX_SOURCE_WIDTH)
+            bad("width out of range");
+        if (in->arg_off[i + 1] < in->arg_off[i]) bad("arg_off not monotonic");
+        if (in->arg_off[i + 1] > 0 && !in->args) bad("missing args array");
         for (int k = in->arg_off[i]; k < in->arg_off[i + 1]; k++) {
             int a = in->args[k];
-            if (a < 0 || a >= i) throw std::runtime_error("operand index out of order");
+            if (a < 0 || a >= i) bad("operand index out of order");
             s.args.push_back(a);
         }
         s.p0 = in->p0[i]; s.p1 = in->p1[i];
         if (in->str[i] >= 0) {
-            if (in->str[i] >= in->n_strings) throw std::runtime_error("string index out of range");
+            if (in->str[i] >= in->n_strings) bad("string index out of range");
             s.str = strings[in->str[i]];
         }
-        if (in->cval_off[i] >= 0) {
-            int nl = (s.width + 31) / 32;
+        if (s.op == S_BVNUM) {
+            int64_t nl = (s.width + 31) / 32;
+            if (in->cval_off[i] < 0 || (int64_t)in->cval_off[i] + nl > in->n_cval) bad("numeral limbs out of range");
             s.val.l.assign(in->cval + in->cval_off[i], in->cval + in->cval_off[i] + nl);
             s.val.norm();
         }
-        if (s.op < 0 || s.op > S_OTHER) throw std::runtime_error("bad op code");
+        // operand counts the lowering reads (smt/node.py constructors' arities)
+        size_t na = s.args.size(), need_min = 0, need_max = (size_t)-1;
+        switch (s.op) {
+        case S_BVNUM: case S_TRUE: case S_FALSE: case S_VAR: case S_ARRAY: need_max = 0; break;
+        case S_BVNEG: case S_BVNOT: case S_NOT: case S_EXTRACT: case S_ZEXT: case S_SEXT: case S_K:
+        case S_APPLY: need_min = need_max = 1; break;
+        case S_BVSUB: case S_BVUDIV: case S_BVUREM: case S_BVSDIV: case S_BVSREM: case S_BVSMOD:
+        case S_BVSHL: case S_BVLSHR: case S_BVASHR: case S_XOR: case S_IMPLIES: case S_BVULT:
+        case S_BVULE: case S_BVUGT: case S_BVUGE: case S_BVSLT: case S_BVSLE: case S_BVSGT:
+        case S_BVSGE: case S_UMULNO: case S_SELECT: need_min = need_max = 2; break;
+        case S_ITE: case S_STORE: need_min = need_max = 3; break;
+        case S_BVADD: case S_BVMUL: case S_BVAND: case S_BVOR: case S_BVXOR: case S_AND: case S_OR:
+        case S_CONCAT: need_min = 1; break;
+        case S_EQ: case S_DISTINCT: need_min = 2; break;
+        default: break;
+        }
+        if (na < need_min || na > need_max) bad("operand count");
+        if (s.op == S_EXTRACT && (s.p1 < 0 || s.p0 < s.p1 || s.p0 >= S[s.args[0]].width ||
+                                  s.width != s.p0 - s.p1 + 1))
+            bad("extract bounds");
+        if ((s.op == S_ZEXT || s.op == S_SEXT) && (s.p0 < 0 || s.width != S[s.args[0]].width + s.p0))
+            bad("extension width");
+        if (s.op == S_APPLY && s.p0 != S[s.args[0]].width) bad("function domain");
     }
     std::vector<int> cons(in->cons, in->cons + in->n_cons);
     std::vector<int> probes(in->probes, in->probes + in->n_probes);
@@ -2597,7 +2652,12 @@ static void compile(const mgc_input* in, mgc_result* res) {
     }
 
     Lowerer lw(S, in->default_entries);
-    for (int t = 0; t < in->n_tables; t++) lw.table_sizes.put(strings.at(in->table_name[t]), in->table_size[t]);
+    for (int t = 0; t < in->n_tables; t++) {
+        if (in->table_name[t] < 0 || in->table_name[t] >= in->n_strings || in->table_size[t] < 0 ||
+            in->table_size[t] > 4096)
+            bad("table entry out of range");
+        lw.table_sizes.put(strings[in->table_name[t]], in->table_size[t]);
+    }
     lw.solve = in->solve != 0;
     if (in->const_keys || in->solve) {
         std::unordered_map<std::string, int> sym_counts;
@@ -2877,6 +2937,9 @@ int mgc_compile(const mgc_input* in, mgc_result** out) {
     } catch (Unsupported& e) {
         r->error = e.what();
         return MGC_UNSUPPORTED;
+    } catch (BadShift& e) {
+        r->error = e.what();
+        return MGC_ERROR;
     } catch (std::exception& e) {
         r->error = e.what();
         return MGC_ERROR;

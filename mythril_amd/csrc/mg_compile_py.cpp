@@ -244,6 +244,7 @@ PyObject* py_compile(PyObject*, PyObject* a) {
     in.leaf_pools = leaf_pools; in.const_keys = const_keys; in.solve = solve;
     in.remat_mode = remat_mode; in.remat_k = remat_k; in.keep_clean = keep_clean;
     in.search_hints = search_hints; in.abi_presets = abi_presets;
+    in.n_cval = (int32_t)f.cval.size(); in.n_string_bytes = (int32_t)f.strings.size();
     mgc_result* res = nullptr;
     int rc;
     Py_BEGIN_ALLOW_THREADS

@@ -1181,14 +1181,16 @@ def source_digest() -> str:
     return h.hexdigest()[:16]
 
 
-CODE_FILES = ("jit.py", "asmgen.py", "ir.py", "irdefs.py", "corpus.py", "engine.py",
-              "csrc/mg_host.cpp", "csrc/mg_api.cpp")
+CODE_FILES = ("jit.py", "asmgen.py", "irdefs.py", "engine.py", "csrc/mg_host.cpp",
+              "csrc/mg_api.cpp")
 
 
 def code_digest() -> str:
-    """Digest of the sources that decide a bench program's compiled code
-    (generator, specialiser, compiler, corpus, translator): bench.py keys
-    traffic measurements on it (profiles/traffic.json)."""
+    """Digest of the sources that turn an IR program into compiled code
+    (handler generator, specialiser, leaf-generator parameters, record
+    translator); the programs themselves are keyed by content
+    (bench.programs_digest).  bench.py keys traffic measurements on both
+    (profiles/traffic.json)."""
     import hashlib
     h = hashlib.sha1(ARCH.encode())
     pkg = os.path.dirname(os.path.abspath(__file__))

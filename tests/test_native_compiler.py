@@ -156,3 +156,58 @@ def test_native_buckets_match_the_python_partition():
         got = M.dependence_buckets(q)
         want = M.dependence_buckets_py(q)
         assert [[c.id for c in g] for g in got] == [[c.id for c in g] for g in want]
+
+
+def _corpus_record(f, solve):
+    """One fuzz_compile.cpp corpus record of flatten()'s arrays."""
+    import struct
+    hdr = [f["n_nodes"], f["n_strings"], len(f["cons"]), len(f["probes"]), len(f["table_name"]),
+           2, 16, len(f["extra"]) // 32, int(solve), int(solve), int(solve), 1, 2, 1, int(solve),
+           int(solve), len(f["cval"]) // 4, len(f["strings"]), len(f["args"])]
+    out = struct.pack("<19i", *hdr)
+    for k in ("op", "sort", "width", "dom", "id", "arg_off", "args", "p0", "p1", "str", "cval_off"):
+        out += f[k].tobytes()
+    out += bytes(f["cval"]) + f["strings"]
+    for k in ("cons", "probes", "table_name", "table_size"):
+        out += f[k].tobytes()
+    return out + bytes(f["extra"])
+
+
+def test_mutated_inputs_under_asan_ubsan(tmp_path):
+    """The C ABI checks every index and count: real DAGs compile, and
+    thousands of mutations of them end in a status code — never in an
+    out-of-bounds access or undefined behaviour (ASan + UBSan build)."""
+    import json
+    import shutil
+    import subprocess
+    from mythril_amd import workloads as W
+    from mythril_amd.ccompile import flatten
+    from mythril_amd.corpus import make_dag
+    import dag_cases
+    import mythril_amd.model as M
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    recs = []
+    for c, p, _, ts in list(dag_cases.named_cases().values())[:8]:
+        recs.append(_corpus_record(flatten(c, p, ts or None), False))
+    recs.append(_corpus_record(flatten(make_dag(5)[0]), False))
+    for wl in ("c1", "c3", "c4"):
+        for b in M.dependence_buckets(W.queries(wl, 2)[1])[:2]:
+            recs.append(_corpus_record(flatten(b), True))
+    corpus = tmp_path / "corpus.bin"
+    corpus.write_bytes(b"".join(recs))
+    exe = str(tmp_path / "fuzz_compile")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
+                    "-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-static-libasan",
+                    "-I" + os.path.join(build.ROOT, "include"),
+                    os.path.join(build.ROOT, "tests", "fuzz_compile.cpp"),
+                    os.path.join(build.ROOT, "mythril_amd", "csrc", "mg_compile.cpp"), "-o", exe],
+                   check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe, str(corpus), "150"], capture_output=True, text=True, env=env, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    st = json.loads(r.stdout.strip().splitlines()[-1])
+    assert st["inputs"] == len(recs) and st["valid_ok"] == len(recs)
+    assert st["mutated_error"] > 0 and st["mutated_ok"] > 0
