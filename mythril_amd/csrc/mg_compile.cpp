@@ -116,11 +116,13 @@ static bool operator>=(const U& a, const U& b) { return !(a < b); }
 static U umin(const U& a, const U& b) { return b < a ? b : a; }
 static U umax(const U& a, const U& b) { return a < b ? b : a; }
 static U mask_slow(int w) { return shl(U::of(1), w) - U::of(1); }
-static const U* mask_table() {
-    static U t[64 * U::N + 1];
-    static bool init = false;
-    if (!init) { for (int w = 0; w <= 64 * U::N; w++) t[w] = mask_slow(w); init = true; }
-    return t;
+static const U* mask_table() {          // (function-local static: thread-safe)
+    static const std::vector<U> t = [] {
+        std::vector<U> v(64 * U::N + 1);
+        for (int w = 0; w <= 64 * U::N; w++) v[w] = mask_slow(w);
+        return v;
+    }();
+    return t.data();
 }
 static const U* const MASKS = mask_table();
 static inline const U& mask(int w) { return MASKS[w < 0 ? 0 : (w > 64 * U::N ? 64 * U::N : w)]; }
@@ -519,17 +521,20 @@ struct Lowerer {
     }
 
     std::string opname(int s) {
-        static std::vector<std::string> names;
-        if (names.empty()) {
+        // built once, thread-safely (compiles may run on several threads:
+        // the CPython front-end releases the GIL)
+        static const std::vector<std::string> names = [] {
+            std::vector<std::string> v;
             std::string all(SOP_NAMES);
             size_t p = 0;
             while (true) {
                 size_t q = all.find('\n', p);
-                names.push_back(all.substr(p, q == std::string::npos ? std::string::npos : q - p));
+                v.push_back(all.substr(p, q == std::string::npos ? std::string::npos : q - p));
                 if (q == std::string::npos) break;
                 p = q + 1;
             }
-        }
+            return v;
+        }();
         return S[s].op == S_OTHER ? S[s].str : names[S[s].op];
     }
 

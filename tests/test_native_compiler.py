@@ -211,3 +211,28 @@ def test_mutated_inputs_under_asan_ubsan(tmp_path):
     st = json.loads(r.stdout.strip().splitlines()[-1])
     assert st["inputs"] == len(recs) and st["valid_ok"] == len(recs)
     assert st["mutated_error"] > 0 and st["mutated_ok"] > 0
+
+
+def test_concurrent_compiles_agree():
+    """The front-end releases the GIL during the compile: programs compiled
+    on several threads at once equal the sequential ones."""
+    import threading
+    from mythril_amd.corpus import make_dag
+    dags = [make_dag(d)[0] for d in range(6)]
+    want = [compile_native(r) for r in dags]
+    got = [None] * (4 * len(dags))
+    errs = []
+
+    def work(k):
+        try:
+            got[k] = compile_native(dags[k % len(dags)])
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(len(got))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errs
+    for k, p in enumerate(got):
+        _same(p, want[k % len(dags)])
