@@ -980,8 +980,26 @@ struct Solver {
     int stamp_gen_ = 0;
     int new_stamp() { return ++stamp_gen_; }
     bool stamped(int x, int g) { if ((size_t)x >= stamp_.size()) stamp_.resize(std::max<size_t>(x + 1, 2 * stamp_.size()), 0); if (stamp_[x] == g) return true; stamp_[x] = g; return false; }
-    std::vector<Bits> dep;
+    // leaf dependency sets, one row of dep_w words per LNode in one arena
+    // (no allocation per node; re-laid out when a leaf index outgrows it)
+    int dep_w = 0;
+    std::vector<uint64_t> dep;
     std::vector<char> has_dep;
+    struct DepRow {
+        const uint64_t* p;
+        int w;
+        bool meets(const Bits& o) const {
+            int n = std::min(w, (int)o.w.size());
+            for (int i = 0; i < n; i++) if (p[i] & o.w[i]) return true;
+            return false;
+        }
+        template <class F> void each(F f) const {
+            for (int i = 0; i < w; i++) {
+                uint64_t x = p[i];
+                while (x) { int b = __builtin_ctzll(x); f(64 * i + b); x &= x - 1; }
+            }
+        }
+    };
     std::vector<Interval> ivl_;
     std::vector<char> has_ivl_;
     std::unordered_set<std::string> joint_done;
@@ -1138,29 +1156,48 @@ struct Solver {
         return lw.mk(op, ln[x].width, args, ln[x].has_imm, ln[x].imm);
     }
 
-    const Bits& depof(int n) {
-        if ((size_t)n < has_dep.size() && has_dep[n]) return dep[n];
-        if (dep.size() < ln.size()) {           // geometric: nodes keep being created
-            size_t sz = std::max(ln.size(), 2 * dep.size());
-            dep.resize(sz);
-            has_dep.resize(sz, 0);
+    void dep_layout(size_t rows, int w) {          // grow rows and / or width
+        if (w != dep_w) {
+            std::vector<uint64_t> d(rows * (size_t)w, 0);
+            for (size_t r = 0; r < has_dep.size(); r++)
+                if (has_dep[r]) std::copy(dep.begin() + r * dep_w, dep.begin() + r * dep_w + dep_w, d.begin() + r * w);
+            dep.swap(d);
+            dep_w = w;
+        } else {
+            dep.resize(rows * (size_t)w, 0);
         }
-        std::vector<int> stack{n};
-        while (!stack.empty()) {
-            int x = stack.back();
-            if (has_dep[x]) { stack.pop_back(); continue; }
+        has_dep.resize(rows, 0);
+    }
+
+    DepRow depof(int n) {
+        if ((size_t)n < has_dep.size() && has_dep[n]) return DepRow{dep.data() + (size_t)n * dep_w, dep_w};
+        int need_w = (int)(lw.leaves.size() + 63) / 64 + 1;
+        if (has_dep.size() < ln.size() || need_w > dep_w)   // geometric: nodes keep being created
+            dep_layout(std::max(ln.size(), 2 * has_dep.size()), std::max(dep_w, need_w));
+        dep_stack_.clear();
+        dep_stack_.push_back(n);
+        while (!dep_stack_.empty()) {
+            int x = dep_stack_.back();
+            if (has_dep[x]) { dep_stack_.pop_back(); continue; }
             bool pend = false;
-            for (int a : ln[x].args) if (!has_dep[a]) { stack.push_back(a); pend = true; }
+            for (int a : ln[x].args) if (!has_dep[a]) { dep_stack_.push_back(a); pend = true; }
             if (pend) continue;
-            stack.pop_back();
-            Bits v;
-            if (ln[x].op == MG_LEAF) v.set((int)ln[x].imm.w[0]);
-            else for (int a : ln[x].args) v.orw(dep[a]);
-            dep[x] = std::move(v);
+            dep_stack_.pop_back();
+            uint64_t* row = dep.data() + (size_t)x * dep_w;
+            if (ln[x].op == MG_LEAF) {
+                int li = (int)ln[x].imm.w[0];
+                row[li >> 6] |= 1ull << (li & 63);
+            } else {
+                for (int a : ln[x].args) {
+                    const uint64_t* src = dep.data() + (size_t)a * dep_w;
+                    for (int i = 0; i < dep_w; i++) row[i] |= src[i];
+                }
+            }
             has_dep[x] = 1;
         }
-        return dep[n];
+        return DepRow{dep.data() + (size_t)n * dep_w, dep_w};
     }
+    std::vector<int> dep_stack_;
 
     const Bits& defmask() {
         if (!dm_valid) {
@@ -1833,7 +1870,7 @@ struct Solver {
 
     bool reads_own(int y, const std::string& name) {
         bool own = false, bad = false;
-        const Bits& d = depof(y);
+        DepRow d = depof(y);
         d.each([&](int li) {
             if (bad) return;
             const Leaf& leaf = lw.leaves[li];
@@ -2242,87 +2279,111 @@ static std::vector<std::vector<U>> leaf_pools(const std::vector<LN>& ln, const s
     values.erase(std::unique(values.begin(), values.end()), values.end());
     std::unordered_map<U, int, UHash> cidx;
     for (size_t i = 0; i < values.size(); i++) cidx[values[i]] = (int)i;
-    std::vector<Bits> under_l(ln.size()), under_c(ln.size());
+    // the leaves / constants under every node: one row of bits per node of
+    // the order, in two arenas (ir._leaf_pools' Python int bit sets)
+    const size_t wl = (leaves.size() + 63) / 64 + 1, wc = (values.size() + 63) / 64 + 1;
+    std::vector<int> row(ln.size(), -1);
+    for (size_t i = 0; i < order.size(); i++) row[order[i]] = (int)i;
+    std::vector<uint64_t> under_l(order.size() * wl, 0), under_c(order.size() * wc, 0);
+    std::vector<uint64_t> done(leaves.size() * wc, 0);      // constants already drawn from
     std::vector<std::vector<U>> pools(leaves.size());
     // pool membership: values below 2^16 in a per-leaf bitmap (narrow leaves
     // draw mostly byte slices, nearly all duplicates), the rest hashed
     // (open addressing over indices into the pool: at most POOL_CAP entries)
     std::vector<std::vector<int16_t>> pool_set(leaves.size());
     std::vector<std::vector<uint64_t>> pool_small(leaves.size());
-    std::vector<Bits> done(leaves.size());
     std::unordered_map<int64_t, std::vector<U>> pv;
     U M256 = mask(256);
-    static const Bits empty;
-    for (int n : order) {
+    for (size_t i = 0; i < order.size(); i++) {
+        int n = order[i];
         const LN& N = ln[n];
+        uint64_t* ls = &under_l[i * wl];
+        uint64_t* cs = &under_c[i * wc];
         if (N.op == MG_LEAF) {
-            under_l[n].set((int)N.imm.w[0]);
+            int li = (int)N.imm.w[0];
+            ls[li >> 6] |= 1ull << (li & 63);
             continue;
         }
         if (N.op == MG_CONST) {
-            under_c[n].set(cidx[N.imm]);
+            int ci = cidx[N.imm];
+            cs[ci >> 6] |= 1ull << (ci & 63);
             continue;
         }
-        Bits ls, cs;
         for (int a : N.args) {
-            ls.orw(under_l[a]);
-            cs.orw(under_c[a]);
+            const uint64_t* al = &under_l[(size_t)row[a] * wl];
+            const uint64_t* ac = &under_c[(size_t)row[a] * wc];
+            for (size_t k = 0; k < wl; k++) ls[k] |= al[k];
+            for (size_t k = 0; k < wc; k++) cs[k] |= ac[k];
         }
-        if (cs.count() > POOL_CAP) {
-            Bits keep;
-            int k = 0;
-            cs.each([&](int ci) { if (k < POOL_CAP) keep.set(ci); k++; });
-            cs = std::move(keep);
+        int cnt = 0;
+        for (size_t k = 0; k < wc; k++) cnt += __builtin_popcountll(cs[k]);
+        if (cnt > POOL_CAP) {                    // keep the POOL_CAP smallest constants
+            int kept = 0;
+            for (size_t k = 0; k < wc; k++) {
+                uint64_t x = cs[k], keep = 0;
+                while (x && kept < POOL_CAP) { uint64_t b = x & (~x + 1); keep |= b; x ^= b; kept++; }
+                cs[k] = keep;
+            }
         }
-        if (is_cmp(N.op) && cs.any()) {
-            ls.each([&](int li) {
+        bool any_c = false;
+        for (size_t k = 0; k < wc; k++) any_c |= cs[k] != 0;
+        if (!is_cmp(N.op) || !any_c) continue;
+        for (size_t kl = 0; kl < wl; kl++) {
+            uint64_t lx = ls[kl];
+            while (lx) {
+                int li = (int)(64 * kl + __builtin_ctzll(lx));
+                lx &= lx - 1;
                 auto& p = pools[li];
+                if ((int)p.size() >= POOL_CAP) continue;
+                uint64_t* dn = &done[(size_t)li * wc];
+                bool fresh_c = false;
+                for (size_t k = 0; k < wc; k++) fresh_c |= (cs[k] & ~dn[k]) != 0;
+                if (!fresh_c) continue;
                 auto& ps = pool_set[li];
                 auto& small = pool_small[li];
                 if (small.empty()) { small.assign(1024, 0); ps.assign(4 * POOL_CAP, -1); }
-                if ((int)p.size() >= POOL_CAP) return;
-                if (!cs.any_minus(done[li])) return;
-                Bits nw = cs.minus(done[li]);
-                done[li].orw(nw);
                 int w = leaves[li].width;
                 bool full = false;
-                nw.each([&](int ci) {
-                    if (full) return;
-                    const U& c = values[ci];
-                    int64_t key = (int64_t)ci * 4096 + w;
-                    auto it = pv.find(key);
-                    if (it == pv.end()) {
-                        std::vector<U> vals = pool_values(c, w);
-                        for (auto& v : vals) v = v & M256;
-                        it = pv.emplace(key, std::move(vals)).first;
-                    }
-                    for (auto& v : it->second) {
-                        bool fresh;
-                        if (!(v.w[0] >> 16) && !v.w[1] && !v.w[2] && !v.w[3] && !v.w[4] && !v.w[5]) {
-                            uint64_t& word = small[v.w[0] >> 6];
-                            uint64_t bit = 1ull << (v.w[0] & 63);
-                            fresh = !(word & bit);
-                            word |= bit;
-                        } else {
-                            uint64_t h = v.w[0] * 0x9E3779B97F4A7C15ull ^ v.w[1] * 0xC2B2AE3D27D4EB4Full ^
-                                         v.w[2] * 0x165667B19E3779F9ull ^ v.w[3] * 0x27D4EB2F165667C5ull;
-                            size_t slot = (h ^ (h >> 32)) & (ps.size() - 1);
-                            fresh = true;
-                            while (ps[slot] >= 0) {
-                                if (p[ps[slot]] == v) { fresh = false; break; }
-                                slot = (slot + 1) & (ps.size() - 1);
-                            }
-                            if (fresh) ps[slot] = (int16_t)p.size();
+                for (size_t k = 0; k < wc && !full; k++) {
+                    uint64_t nw = cs[k] & ~dn[k];
+                    dn[k] |= nw;
+                    while (nw && !full) {
+                        int ci = (int)(64 * k + __builtin_ctzll(nw));
+                        nw &= nw - 1;
+                        const U& c = values[ci];
+                        int64_t key = (int64_t)ci * 4096 + w;
+                        auto it = pv.find(key);
+                        if (it == pv.end()) {
+                            std::vector<U> vals = pool_values(c, w);
+                            for (auto& v : vals) v = v & M256;
+                            it = pv.emplace(key, std::move(vals)).first;
                         }
-                        if (fresh) p.push_back(v);
-                        if ((int)p.size() >= POOL_CAP) break;
+                        for (auto& v : it->second) {
+                            bool fresh;
+                            if (!(v.w[0] >> 16) && !v.w[1] && !v.w[2] && !v.w[3] && !v.w[4] && !v.w[5]) {
+                                uint64_t& word = small[v.w[0] >> 6];
+                                uint64_t bit = 1ull << (v.w[0] & 63);
+                                fresh = !(word & bit);
+                                word |= bit;
+                            } else {
+                                uint64_t h = v.w[0] * 0x9E3779B97F4A7C15ull ^ v.w[1] * 0xC2B2AE3D27D4EB4Full ^
+                                             v.w[2] * 0x165667B19E3779F9ull ^ v.w[3] * 0x27D4EB2F165667C5ull;
+                                size_t slot = (h ^ (h >> 32)) & (ps.size() - 1);
+                                fresh = true;
+                                while (ps[slot] >= 0) {
+                                    if (p[ps[slot]] == v) { fresh = false; break; }
+                                    slot = (slot + 1) & (ps.size() - 1);
+                                }
+                                if (fresh) ps[slot] = (int16_t)p.size();
+                            }
+                            if (fresh) p.push_back(v);
+                            if ((int)p.size() >= POOL_CAP) break;
+                        }
+                        if ((int)p.size() >= POOL_CAP) full = true;
                     }
-                    if ((int)p.size() >= POOL_CAP) full = true;
-                });
-            });
+                }
+            }
         }
-        under_l[n] = std::move(ls);
-        under_c[n] = std::move(cs);
     }
     return pools;
 }
