@@ -107,7 +107,18 @@ const uint32_t* mgc_code(const mgc_result* r, int32_t* n_ins);
 /* constant table: n_rows x 8 limbs; the first n_const_values rows are the
  * CONST values (ascending), the rest the leaf pools */
 const uint32_t* mgc_table(const mgc_result* r, int32_t* n_rows, int32_t* n_const_values);
-/* everything else (leaves, tables, probes, statistics) as one JSON object */
+/* everything else as one JSON object:
+ *   leaves        [[name, width, kind, source, chunk, entry], ...] in leaf
+ *                 index order (kind: var | key | val | else | cval | aux)
+ *   n_lds, n_probes, n_roots, n_user_probes
+ *   table_sizes   [[name, entries], ...]; table_kinds [[name, array|func]]
+ *   table_ckeys   [[name, [hex key, ...]], ...] (constant-keyed entries)
+ *   pool_ranges   [[offset, count], ...] per leaf, rows of the table
+ *   derived       [[leaf index, probe index], ...] (search mode)
+ *   entry_keys    [[table, [[probe index per 256-bit key chunk], ...]], ...]
+ *   lnodes, spills, reloads, hist [[op, count]], hist_order [op, ...]
+ *   presets       {"vars": [[name, hex]], "arrays": [[name, [[offset, byte]]]]}
+ *                 (abi_presets, when offsets were pinned) */
 const char* mgc_meta(const mgc_result* r);
 void mgc_free(mgc_result* r);
 
