@@ -360,30 +360,15 @@ static bool is_order(int op) { return op == MG_ULT || op == MG_ULE || op == MG_S
 
 typedef std::vector<int> Chunks;
 
-// hash-consing key of an LNode: (op, width, operand ids, imm)
-struct MkKey {
-    int op, width;
-    Args args;
-    bool has_imm;
-    U imm;
-    bool operator==(const MkKey& o) const {
-        return op == o.op && width == o.width && has_imm == o.has_imm && args == o.args &&
-               (!has_imm || imm == o.imm);
-    }
-};
-struct MkHash {
-    size_t operator()(const MkKey& k) const {
-        uint64_t h = (uint64_t)k.op * 0x9E3779B97F4A7C15ull ^ (uint64_t)k.width * 0xC2B2AE3D27D4EB4Full;
-        for (int a : k.args) h = (h ^ (uint64_t)a) * 0x100000001B3ull;
-        if (k.has_imm) for (int i = 0; i < U::N; i++) h = (h ^ k.imm.w[i]) * 0x100000001B3ull;
-        return (size_t)(h ^ (h >> 29));
-    }
-};
 
 struct Lowerer {
     const std::vector<Src>& S;
     std::vector<LN> ln;
-    std::unordered_map<MkKey, int, MkHash> table;
+    // hash-consing table: open addressing over node ids (a node's key is
+    // its own fields, so the table stores ids and hashes only)
+    std::vector<int> slot_id;
+    std::vector<uint64_t> slot_hash;
+    size_t n_slots_used = 0;
     std::vector<Leaf> leaves;
     std::unordered_map<std::string, int> leaf_ids;
     std::vector<Chunks> memo;
@@ -404,18 +389,50 @@ struct Lowerer {
     }
 
     // -- hash-consed constructors (ir._Lowerer.mk / const / leaf) --------------
+    static uint64_t key_hash(int op, int width, const Args& args, bool has_imm, const U& imm) {
+        uint64_t h = (uint64_t)op * 0x9E3779B97F4A7C15ull ^ (uint64_t)width * 0xC2B2AE3D27D4EB4Full;
+        for (int a : args) h = (h ^ (uint64_t)(uint32_t)a) * 0x100000001B3ull;
+        if (has_imm) for (int i = 0; i < U::N; i++) h = (h ^ imm.w[i]) * 0x100000001B3ull;
+        h ^= h >> 29;
+        return h | 1;                                  // 0 marks an empty slot
+    }
+    void rehash(size_t n) {
+        std::vector<int> ids(n, -1);
+        std::vector<uint64_t> hs(n, 0);
+        for (size_t i = 0; i < slot_id.size(); i++) {
+            if (slot_id[i] < 0) continue;
+            size_t j = slot_hash[i] & (n - 1);
+            while (ids[j] >= 0) j = (j + 1) & (n - 1);
+            ids[j] = slot_id[i];
+            hs[j] = slot_hash[i];
+        }
+        slot_id.swap(ids);
+        slot_hash.swap(hs);
+    }
     int mk(int op, int width, Args args, bool has_imm = false, const U& imm = U()) {
         if (op == MG_CONCAT && width == MG_MAX_WIDTH && ln[args[0]].op == MG_EXTRACT &&
             ln[args[0]].imm.zero() && ln[ln[args[0]].args[0]].width == MG_MAX_WIDTH)
             args[0] = ln[args[0]].args[0];
-        MkKey key{op, width, std::move(args), has_imm, has_imm ? imm : U()};
-        auto it = table.find(key);
-        if (it != table.end()) return it->second;
+        const U key_imm = has_imm ? imm : U();
+        if (2 * (n_slots_used + 1) > slot_id.size()) rehash(slot_id.empty() ? 4096 : 2 * slot_id.size());
+        uint64_t h = key_hash(op, width, args, has_imm, key_imm);
+        size_t j = h & (slot_id.size() - 1);
+        while (slot_id[j] >= 0) {
+            if (slot_hash[j] == h) {
+                const LN& o = ln[slot_id[j]];
+                if (o.op == op && o.width == width && o.has_imm == has_imm && o.args == args &&
+                    (!has_imm || o.imm == key_imm))
+                    return slot_id[j];
+            }
+            j = (j + 1) & (slot_id.size() - 1);
+        }
         int64_t b = birth;
-        for (int a : key.args) if (ln[a].birth > b) b = ln[a].birth;
+        for (int a : args) if (ln[a].birth > b) b = ln[a].birth;
         int id = (int)ln.size();
-        ln.push_back(LN{op, width, key.args, has_imm, key.imm, b});
-        table.emplace(std::move(key), id);
+        ln.push_back(LN{op, width, std::move(args), has_imm, key_imm, b});
+        slot_id[j] = id;
+        slot_hash[j] = h;
+        n_slots_used++;
         return id;
     }
     int mki(int op, int width, Args args, int64_t imm) { return mk(op, width, std::move(args), true, U::of((uint64_t)imm)); }
