@@ -1690,6 +1690,9 @@ def shift_core(a: Asm, kind: str, fa: int, fb: int, fw: int, masked: bool):
 # Registers: u = X, v = Y on entry; un = X ++ R ++ [T0]; vn = Y;
 # b/c = T2/T3 (b kept for the remainder); digit temps T4..T11.
 
+# dividend normalisation order (A/B knob: MYTHGPU_DIV_BITS_FIRST=0 shifts
+# limbs first, then 17 limbs of bits — the round-2 order)
+DIV_BITS_FIRST = os.environ.get("MYTHGPU_DIV_BITS_FIRST", "1") != "0"
 DIV_M = {4: 48, 2: 50, 1: 52}   # limb-shift stage masks (bank B: free in heavy bodies)
 DIV_Z6 = 54                     # lanes with vn[0..5] == 0 (bank B)
 DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm:
@@ -1751,10 +1754,18 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     lab = exec_begin(a, z, S_T)
     moves(a, X, [None] * 8)
     exec_end(a, lab, S_T)
-    live = 8
-    for st in (4, 2, 1):
-        live = _stage(a, un, st, 16, True, DIV_M[st], live)
-    bitshift_left(a, un, c, bz, 17, S_T)
+    if DIV_BITS_FIRST:
+        # the dividend's bits first (9 limbs: u << b, the top limb un[8] = 0
+        # on entry), then its limbs: 9 funnels instead of 17 after the barrel
+        bitshift_left(a, un, c, bz, 9, S_T)
+        live = 9
+        for st in (4, 2, 1):
+            live = _stage(a, un, st, 17, True, DIV_M[st], live)
+    else:
+        live = 8
+        for st in (4, 2, 1):
+            live = _stage(a, un, st, 16, True, DIV_M[st], live)
+        bitshift_left(a, un, c, bz, 17, S_T)
     # lanes whose normalised divisor has its low 4 / 6 digits zero: a
     # quotient digit's multiply-subtract starts at digit 4 / 6 when every
     # lane with a nonzero digit is one of them (qh * 0 changes nothing)

@@ -17,7 +17,10 @@ import numpy as np
 
 from .ir import Program
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmythgpu.so")
+# (MYTHGPU_LIB: an A/B build of the same ABI, with the asmgen knobs it was
+# built under set in the environment)
+_LIB_PATH = os.environ.get("MYTHGPU_LIB") or \
+    os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmythgpu.so")
 
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
