@@ -681,6 +681,9 @@ class Wave:
     def i_v_cmp_eq_u64(self, a, pc):
         self._cmp(a, lambda x, y: x == y, width=64)
 
+    def i_v_cmp_lt_u64(self, a, pc):
+        self._cmp(a, lambda x, y: x < y, width=64)
+
     def i_v_cmp_gt_u64(self, a, pc):
         self._cmp(a, lambda x, y: x > y, width=64)
 
