@@ -47,6 +47,24 @@ struct mg_ctx {
     // its launches on the context stream; mg_last_kernel_ms)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     float last_ms = 0.f;
+    // device blocks of programs and batches (dev_alloc): power-of-two size
+    // classes; classes below MG_SLAB_CLASS_MAX are carved from slabs, larger
+    // ones are whole allocations; freed blocks wait on a per-class list, so
+    // a get_model query's loads and frees make no hipMalloc / hipFree (each
+    // costs tens of microseconds, and hipFree synchronises the device)
+    std::map<size_t, std::vector<void*>> free_blocks;
+    std::vector<void*> slabs, large;
+    uint8_t* slab_cur = nullptr;
+    size_t slab_left = 0;
+    // the last launch on a caller's stream (mg_batch_eval_gen): a block is
+    // reused only after it completed
+    hipEvent_t ext_ev = nullptr;
+    bool ext_pending = false;
+    // pinned host staging for program uploads (grow-only): the blob is
+    // assembled in place and copied at pinned-DMA rate; a leaf-pool-heavy
+    // search program is ~1 MB (the pools' (v-1, v, v+1) triples)
+    uint8_t* h_stage = nullptr;
+    size_t h_stage_size = 0;
 };
 
 static void timing_begin(mg_ctx* ctx) {
@@ -68,7 +86,9 @@ static void timing_read(mg_ctx* ctx) {
 struct mg_prog {
     mg_ctx* ctx = nullptr;
     void* d_blob = nullptr;         // code | consts | gen | desc | xcode
+    size_t blob_cls = 0;            // its dev_alloc size class
     mg_pdesc* d_desc = nullptr;
+    mg_pdesc h_desc;                // host copy (batches copy it from here)
     uint32_t n_ins = 0, n_consts = 0, n_leaves = 0, n_lds = 0, n_probes = 0;
     uint64_t rec_fp = 0;            // records' fingerprint (rec_fingerprint)
 };
@@ -109,6 +129,7 @@ struct mg_jit {
 struct mg_batch {
     mg_ctx* ctx = nullptr;
     mg_pdesc* d_descs = nullptr;
+    size_t descs_cls = 0;
     uint32_t n = 0;
     uint32_t max_lds = 0;
     uint32_t max_leaves = 0;
@@ -131,6 +152,59 @@ static int fail(mg_ctx* ctx, int code, const char* fmt, ...) {
             return fail(ctx, MG_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),  \
                         __FILE__, __LINE__);                                            \
     } while (0)
+
+#define MG_SLAB_BYTES ((size_t)4 << 20)
+#define MG_SLAB_CLASS_MAX ((size_t)256 << 10)
+#define MG_BLOCK_MIN ((size_t)4 << 10)
+
+static size_t block_class(size_t bytes) {
+    size_t c = MG_BLOCK_MIN;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+// A device block of at least `bytes` (256-byte aligned); *cls receives its
+// size class for dev_release.
+static hipError_t dev_alloc(mg_ctx* ctx, size_t bytes, void** out, size_t* cls) {
+    const size_t c = block_class(bytes);
+    *cls = c;
+    auto it = ctx->free_blocks.find(c);
+    if (it != ctx->free_blocks.end() && !it->second.empty()) {
+        *out = it->second.back();
+        it->second.pop_back();
+        return hipSuccess;
+    }
+    if (c > MG_SLAB_CLASS_MAX) {
+        hipError_t e = hipMalloc(out, c);
+        if (e == hipSuccess) ctx->large.push_back(*out);
+        return e;
+    }
+    if (ctx->slab_left < c) {
+        void* slab = nullptr;
+        hipError_t e = hipMalloc(&slab, MG_SLAB_BYTES);
+        if (e != hipSuccess) return e;
+        ctx->slabs.push_back(slab);
+        ctx->slab_cur = (uint8_t*)slab;
+        ctx->slab_left = MG_SLAB_BYTES;
+    }
+    *out = ctx->slab_cur;                   // classes are powers of two <= the slab
+    ctx->slab_cur += c;
+    ctx->slab_left -= c;
+    return hipSuccess;
+}
+
+// Back to its class list once no queued launch can still read it: the
+// context stream and the last caller-stream launch are waited for (what the
+// hipFree this replaces did by synchronising the device).
+static void dev_release(mg_ctx* ctx, void* p, size_t cls) {
+    if (!p) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->ext_pending) {
+        (void)hipEventSynchronize(ctx->ext_ev);
+        ctx->ext_pending = false;
+    }
+    ctx->free_blocks[cls].push_back(p);
+}
 
 static int workspace(mg_ctx* ctx, size_t bytes, void** out) {
     if (bytes > ctx->ws_size) {
@@ -220,7 +294,8 @@ int mg_init(int device, mg_ctx** out) {
         delete ctx;
         return MG_E_HIP;
     }
-    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ext_ev, hipEventDisableTiming) != hipSuccess) {
         mg_free(ctx);
         return MG_E_HIP;
     }
@@ -249,8 +324,13 @@ int mg_init(int device, mg_ctx** out) {
 void mg_free(mg_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->ws) (void)hipFree(ctx->ws);
     if (ctx->d_btab) (void)hipFree(ctx->d_btab);
+    for (void* q : ctx->slabs) (void)hipFree(q);
+    for (void* q : ctx->large) (void)hipFree(q);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->ext_ev) (void)hipEventDestroy(ctx->ext_ev);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -284,22 +364,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     std::vector<uint32_t> rec;
     MaskPool pool;
     mg_translate_records(ctx->hoff, code, n_ins, n_consts, kernel_lds_slots(ctx, n_spill_slots), rec, pool);
-    // generator pools expanded to (v - 1, v, v + 1) triples (mod 2^256), so
-    // the pool class is one indexed load (pool[e] + delta - 1, gen_ref.py)
     const uint32_t n_masks = (uint32_t)(pool.words.size() / 8);
-    std::vector<uint32_t> pm(consts ? (size_t)n_consts * 24 : 0);
-    for (uint32_t c = 0; c < n_consts; ++c) {
-        const uint32_t* v = consts + (size_t)c * 8;
-        uint32_t* o = pm.data() + (size_t)c * 24;
-        uint64_t bm = 1, bp = 1;                 // borrow of v - 1, carry of v + 1
-        for (int j = 0; j < 8; ++j) {
-            o[j] = v[j] - (uint32_t)bm;
-            bm = bm && v[j] == 0;
-            o[8 + j] = v[j];
-            o[16 + j] = v[j] + (uint32_t)bp;
-            bp = bp && v[j] == 0xFFFFFFFFu;
-        }
-    }
     const uint32_t n_const_all = n_consts + n_masks + n_consts * 3;
     // device leaf descriptors: byte pool offsets and the per-leaf stream salt
     std::vector<mg_leafgen_dev> gdev(n_leaves);
@@ -340,19 +405,43 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     const size_t off_const = align(code_b), off_gen = off_const + align(const_b),
                  off_desc = off_gen + align(gen_b), off_rec = off_desc + align(sizeof(mg_pdesc)),
                  total = off_rec + align(rec_b);
-    std::vector<uint8_t> blob(total, 0);
-    if (n_ins) memcpy(blob.data(), code, (size_t)n_ins * 16);   // + zeroed NOP padding
-    if (n_consts) memcpy(blob.data() + off_const, consts, (size_t)n_consts * 32);
+    if (total > ctx->h_stage_size) {
+        if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+        ctx->h_stage = nullptr;
+        ctx->h_stage_size = 0;
+        size_t sz = (size_t)4 << 20;
+        while (sz < total) sz <<= 1;
+        HIPCHECK(ctx, hipHostMalloc((void**)&ctx->h_stage, sz, hipHostMallocDefault));
+        ctx->h_stage_size = sz;
+    }
+    uint8_t* blob = ctx->h_stage;   // free: every upload below is synchronous
+    memset(blob, 0, total);
+    if (n_ins) memcpy(blob, code, (size_t)n_ins * 16);   // + zeroed NOP padding
+    if (n_consts) memcpy(blob + off_const, consts, (size_t)n_consts * 32);
     if (!pool.words.empty())
-        memcpy(blob.data() + off_const + (size_t)n_consts * 32, pool.words.data(),
-               pool.words.size() * 4);
-    if (!pm.empty())
-        memcpy(blob.data() + off_const + (size_t)(n_consts + n_masks) * 32, pm.data(),
-               pm.size() * 4);
-    if (gen_b) memcpy(blob.data() + off_gen, gdev.data(), gen_b);
-    memcpy(blob.data() + off_rec, rec.data(), rec_b);
+        memcpy(blob + off_const + (size_t)n_consts * 32, pool.words.data(), pool.words.size() * 4);
+    // generator pools expanded to (v - 1, v, v + 1) triples (mod 2^256), so
+    // the pool class is one indexed load (pool[e] + delta - 1, gen_ref.py)
+    {
+        uint32_t* pm = (uint32_t*)(blob + off_const + (size_t)(n_consts + n_masks) * 32);
+        for (uint32_t c = 0; c < n_consts; ++c) {
+            const uint32_t* v = consts + (size_t)c * 8;
+            uint32_t* o = pm + (size_t)c * 24;
+            uint64_t bm = 1, bp = 1;             // borrow of v - 1, carry of v + 1
+            for (int j = 0; j < 8; ++j) {
+                o[j] = v[j] - (uint32_t)bm;
+                bm = bm && v[j] == 0;
+                o[8 + j] = v[j];
+                o[16 + j] = v[j] + (uint32_t)bp;
+                bp = bp && v[j] == 0xFFFFFFFFu;
+            }
+        }
+    }
+    if (gen_b) memcpy(blob + off_gen, gdev.data(), gen_b);
+    memcpy(blob + off_rec, rec.data(), rec_b);
     void* d = nullptr;
-    HIPCHECK(ctx, hipMalloc(&d, total));
+    size_t cls = 0;
+    HIPCHECK(ctx, dev_alloc(ctx, total, &d, &cls));
     uint8_t* db = (uint8_t*)d;
     mg_pdesc desc;
     memset(&desc, 0, sizeof desc);
@@ -366,17 +455,20 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     desc.prog_seed = prog_seed;
     desc.xcode = (const uint32_t*)(db + off_rec);
     desc.btab = ctx->d_btab;
-    memcpy(blob.data() + off_desc, &desc, sizeof desc);
-    hipError_t e = hipMemcpy(d, blob.data(), total, hipMemcpyHostToDevice);
+    memcpy(blob + off_desc, &desc, sizeof desc);
+    hipError_t e = hipMemcpyAsync(d, blob, total, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
-        (void)hipFree(d);
+        dev_release(ctx, d, cls);
         return fail(ctx, MG_E_HIP, "upload: %s", hipGetErrorString(e));
     }
     mg_prog* p = new mg_prog();
     p->ctx = ctx;
     p->rec_fp = rec_fp;
     p->d_blob = d;
+    p->blob_cls = cls;
     p->d_desc = (mg_pdesc*)(db + off_desc);
+    p->h_desc = desc;
     p->n_ins = n_ins;
     p->n_consts = n_consts;
     p->n_leaves = n_leaves;
@@ -389,7 +481,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
 void mg_free_program(mg_prog* p) {
     if (!p) return;
     (void)hipSetDevice(p->ctx->device);
-    (void)hipFree(p->d_blob);
+    dev_release(p->ctx, p->d_blob, p->blob_cls);
     delete p;
 }
 
@@ -534,8 +626,7 @@ int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, 
     uint32_t max_lds = 0, max_leaves = 0;
     for (uint32_t i = 0; i < n_progs; ++i) {
         if (!progs[i] || progs[i]->ctx != ctx) return fail(ctx, MG_E_ARG, "program %u", i);
-        HIPCHECK(ctx, hipMemcpy(&descs[i], progs[i]->d_desc, sizeof(mg_pdesc),
-                                hipMemcpyDeviceToHost));
+        descs[i] = progs[i]->h_desc;
         if (progs[i]->n_lds > max_lds) max_lds = progs[i]->n_lds;
         if (progs[i]->n_leaves > max_leaves) max_leaves = progs[i]->n_leaves;
     }
@@ -545,12 +636,14 @@ int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, 
     b->max_lds = max_lds;
     b->max_leaves = max_leaves;
     if (n_progs) {
-        hipError_t e = hipMalloc(&b->d_descs, sizeof(mg_pdesc) * n_progs);
+        void* d = nullptr;
+        hipError_t e = dev_alloc(ctx, sizeof(mg_pdesc) * n_progs, &d, &b->descs_cls);
+        b->d_descs = (mg_pdesc*)d;
         if (e == hipSuccess)
             e = hipMemcpy(b->d_descs, descs.data(), sizeof(mg_pdesc) * n_progs,
                           hipMemcpyHostToDevice);
         if (e != hipSuccess) {
-            if (b->d_descs) (void)hipFree(b->d_descs);
+            if (b->d_descs) dev_release(ctx, b->d_descs, b->descs_cls);
             delete b;
             return fail(ctx, MG_E_HIP, "batch upload: %s", hipGetErrorString(e));
         }
@@ -562,7 +655,7 @@ int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, 
 void mg_batch_free(mg_batch* b) {
     if (!b) return;
     (void)hipSetDevice(b->ctx->device);
-    if (b->d_descs) (void)hipFree(b->d_descs);
+    if (b->d_descs) dev_release(b->ctx, b->d_descs, b->descs_cls);
     delete b;
 }
 
@@ -583,6 +676,10 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
         run.seed = seed;
         run.first_index = first_index;
         HIPCHECK(ctx, launch(ctx, 1, b->d_descs + p0, np, run, b->max_lds, s));
+    }
+    if (s != ctx->stream) {
+        HIPCHECK(ctx, hipEventRecord(ctx->ext_ev, s));
+        ctx->ext_pending = true;
     }
     return MG_OK;
 }
@@ -703,6 +800,7 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
         const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)row[2 * i];
         e = hipMemcpy((uint8_t*)progs[i]->d_desc + offsetof(mg_pdesc, jit_entry), &entry,
                       sizeof entry, hipMemcpyHostToDevice);
+        if (e == hipSuccess) memcpy(&progs[i]->h_desc.jit_entry, &entry, sizeof entry);
         if (e != hipSuccess) {
             mg_jit_detach(j);
             return fail(ctx, MG_E_HIP, "JIT attach: %s", hipGetErrorString(e));
@@ -720,9 +818,11 @@ void mg_jit_detach(mg_jit* j) {
     if (!j) return;
     (void)hipSetDevice(j->ctx->device);
     const uint64_t zero = 0;
-    for (mg_prog* p : j->progs)
+    for (mg_prog* p : j->progs) {
         (void)hipMemcpy((uint8_t*)p->d_desc + offsetof(mg_pdesc, jit_entry), &zero, sizeof zero,
                         hipMemcpyHostToDevice);
+        memcpy(&p->h_desc.jit_entry, &zero, sizeof zero);
+    }
     (void)hipDeviceSynchronize();
     if (j->module) (void)hipModuleUnload(j->module);
     delete j;
