@@ -2842,24 +2842,33 @@ static void compile(const mgc_input* in, mgc_result* res) {
         res->code[4 * k + 2] = x.imm;
         res->code[4 * k + 3] = 0;
     }
-    std::vector<U> table = const_values;
+    // constant table: the CONST values, then every non-empty leaf pool,
+    // written straight as limbs
     std::vector<std::pair<int, int>> pool_ranges;
+    std::vector<std::vector<U>> pools;
+    size_t n_rows = const_values.size();
     if (in->leaf_pools) {
-        auto pools = leaf_pools(lw.ln, order, lw.leaves);
+        pools = leaf_pools(lw.ln, order, lw.leaves);
         for (size_t li = 0; li < pools.size(); li++) {
             if (!pools[li].empty()) {
-                pool_ranges.push_back({(int)table.size(), (int)pools[li].size()});
-                table.insert(table.end(), pools[li].begin(), pools[li].end());
+                pool_ranges.push_back({(int)n_rows, (int)pools[li].size()});
+                n_rows += pools[li].size();
             } else {
                 pool_ranges.push_back({0, (int)const_values.size()});
             }
         }
     }
-    res->n_rows = (int32_t)table.size();
+    res->n_rows = (int32_t)n_rows;
     res->n_const_values = (int32_t)const_values.size();
-    res->table.resize(8 * table.size());
-    for (size_t r = 0; r < table.size(); r++)
-        for (int j = 0; j < 8; j++) res->table[8 * r + j] = (uint32_t)(table[r].w[j / 2] >> (32 * (j & 1)));
+    res->table.resize(8 * n_rows);
+    uint32_t* row = res->table.data();
+    auto put = [&row](const U& u) {
+        for (int j = 0; j < 8; j++) row[j] = (uint32_t)(u.w[j / 2] >> (32 * (j & 1)));
+        row += 8;
+    };
+    for (const U& u : const_values) put(u);
+    for (const auto& pl : pools)
+        for (const U& u : pl) put(u);
 
     // -- metadata ---------------------------------------------------------------
     std::string& o = res->meta;
