@@ -113,6 +113,54 @@ def test_corpus_dag_generated_lanes(engine, dag_id):
         assert bool(bits[a]) == bool(want), (dag_id, a)
 
 
+def test_device_blocks_reused_across_loads(engine):
+    """Programs of several sizes loaded and freed in turn reuse the
+    context's device blocks (mg_api.cpp dev_alloc / dev_release): every
+    program loaded into a recycled block evaluates exactly like the oracle,
+    including after a batch ran on a caller's stream (the block is reused
+    only once that launch completed)."""
+    import ctypes as C
+    # the caller's stream and output buffer come from the library's own HIP
+    # runtime (torch bundles another one, which cannot share this process's
+    # device once the engine holds it)
+    hip = C.CDLL("libamdhip64.so.7", mode=C.RTLD_GLOBAL)
+    dag_ids = [3, 40, 5, 600, 3, 41, 4000, 6]
+    progs = {d: compile_constraints(make_dag(d)[0]) for d in set(dag_ids)}
+    seed, first, n = 0xB10C, 777, 128
+
+    def check(d, lp):
+        bits, _, leaves = engine.eval_gen(lp, seed, first, n, want_leaves=True)
+        roots = make_dag(d)[0]
+        for a in range(0, n, 9):
+            asg = unpack(progs[d], leaves[:, :, a])
+            want = R.eval_constraints(roots, R.Assignment(asg.vars, asg.arrays, asg.funcs))
+            assert bool(bits[a]) == bool(want), (d, a)
+
+    for rnd in range(3):
+        for d in dag_ids:
+            lp = engine.load(progs[d], prog_seed=d)
+            check(d, lp)
+            del lp                                  # back to the block cache
+    # a batch on a caller's stream, its programs freed right after the launch
+    stream, d_bits = C.c_void_p(), C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(stream)) == 0
+    words = (1 << 16) // 64
+    assert hip.hipMalloc(C.byref(d_bits), C.c_size_t(4 * words * 8)) == 0
+    try:
+        loaded = [engine.load(progs[d], prog_seed=d) for d in dag_ids[:4]]
+        batch = engine.batch_create(loaded)
+        engine.batch_eval_gen(batch, seed, first, 1 << 16, d_bits.value, 0, stream.value)
+        engine.batch_free(batch)
+        del loaded
+        for d in dag_ids[4:]:
+            lp = engine.load(progs[d], prog_seed=d)
+            check(d, lp)
+    finally:
+        hip.hipStreamSynchronize(stream)
+        hip.hipFree(d_bits)
+        hip.hipStreamDestroy(stream)
+
+
 def test_full_size_sampled_and_deterministic(engine):
     roots, _ = make_dag(42)
     prog = compile_constraints(roots)
