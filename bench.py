@@ -33,6 +33,9 @@ sys.path.insert(0, ROOT)
 SEED = 0x6D797468
 # stand-in query streams (mythril_amd/workloads.py): distinct queries per step
 STREAM_QUERIES = 256
+# LDS spill tier of the context (mg_api.cpp reads the same variable): the
+# compiled programs are translated for it
+LDS_SLOTS = int(os.environ.get("MYTHGPU_LDS_SLOTS", "6"))
 _STREAM = None
 
 
@@ -251,8 +254,9 @@ def main():
         t0 = time.time()
         ids = [d for d, _, _, _ in corpus]
         image, jit_cached = jit.cached_image(
-            "%s_%d_%d_%d_%d" % (args.workload, len(ids), ids[0], ids[-1], sum(ids)),
-            lambda: jit.compile_batch([(p, None, d) for d, p, _, _ in corpus], workers=workers))
+            "%s_%d_%d_%d_%d_lds%d" % (args.workload, len(ids), ids[0], ids[-1], sum(ids), LDS_SLOTS),
+            lambda: jit.compile_batch([(p, None, d) for d, p, _, _ in corpus], workers=workers,
+                                      lds_slots=LDS_SLOTS))
         t_jit = time.time() - t0
     if args.jit_build_only:
         print("jit image %.1f MB in %.1f s (cached: %s)" % (len(image or b"") / 1e6, t_jit,
