@@ -83,8 +83,11 @@ static void timing_read(mg_ctx* ctx) {
         ctx->last_ms = ms;
 }
 
+struct mg_jit;
+
 struct mg_prog {
     mg_ctx* ctx = nullptr;
+    mg_jit* jit = nullptr;          // the compiled-program image it is attached to
     void* d_blob = nullptr;         // code | consts | gen | desc | xcode
     size_t blob_cls = 0;            // its dev_alloc size class
     mg_pdesc* d_desc = nullptr;
@@ -481,6 +484,10 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
 void mg_free_program(mg_prog* p) {
     if (!p) return;
     (void)hipSetDevice(p->ctx->device);
+    if (p->jit) {                   // a later detach must not write into a reused block
+        auto& v = p->jit->progs;
+        v.erase(std::remove(v.begin(), v.end(), p), v.end());
+    }
     dev_release(p->ctx, p->d_blob, p->blob_cls);
     delete p;
 }
@@ -805,6 +812,11 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
             mg_jit_detach(j);
             return fail(ctx, MG_E_HIP, "JIT attach: %s", hipGetErrorString(e));
         }
+        if (progs[i]->jit && progs[i]->jit != j) {    // re-attached: the old image lets go
+            auto& v = progs[i]->jit->progs;
+            v.erase(std::remove(v.begin(), v.end(), progs[i]), v.end());
+        }
+        progs[i]->jit = j;
         j->progs.push_back(progs[i]);
     }
     *out = j;
@@ -822,6 +834,7 @@ void mg_jit_detach(mg_jit* j) {
         (void)hipMemcpy((uint8_t*)p->d_desc + offsetof(mg_pdesc, jit_entry), &zero, sizeof zero,
                         hipMemcpyHostToDevice);
         memcpy(&p->h_desc.jit_entry, &zero, sizeof zero);
+        p->jit = nullptr;
     }
     (void)hipDeviceSynchronize();
     if (j->module) (void)hipModuleUnload(j->module);

@@ -152,3 +152,23 @@ def test_jit_attach_refuses_code_compiled_for_other_records(engine):
         engine.jit_attach([lp1], image)
     lp1 = engine.load(p1, default_leafgen(p1), prog_seed=d1)
     engine.jit_detach(engine.jit_attach([lp1], image))
+
+
+def test_program_freed_while_attached_leaves_its_image(engine):
+    """A program freed before its image is detached drops out of the image's
+    list (mg_free_program), so the detach cannot write into the device block
+    the next program reuses: that program keeps evaluating like the
+    interpreter did before the detach."""
+    from mythril_amd import jit
+    d1, p1, _, _ = bench.compile_unit(("c2", 1))
+    d2, p2, _, _ = bench.compile_unit(("c2", 2))
+    image = jit.compile_batch([(p1, None, d1)])
+    lp1 = engine.load(p1, default_leafgen(p1), prog_seed=d1)
+    h = engine.jit_attach([lp1], image)
+    del lp1                                       # freed while attached
+    lp2 = engine.load(p2, default_leafgen(p2), prog_seed=d2)
+    before = engine.eval_gen(lp2, bench.SEED, 5, 4096, want_probes=True)
+    engine.jit_detach(h)
+    after = engine.eval_gen(lp2, bench.SEED, 5, 4096, want_probes=True)
+    assert np.array_equal(before[0], after[0])
+    assert (before[1] is None and after[1] is None) or np.array_equal(before[1], after[1])
