@@ -919,7 +919,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
     results = []
     for cs in sets:
         try:
-            # the call form of Constraints.is_possible (constraints.py:33), so
+            # the call form of Constraints.is_possible (constraints.py:32), so
             # the lru_cache entry is the one the per-state loop would hit
             if enforce_execution_time:
                 get_model(cs)
