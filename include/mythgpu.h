@@ -115,7 +115,10 @@ int mg_search(mg_ctx* ctx, const mg_prog* prog, const mg_gen* gen, uint64_t n_ca
  * resident benchmarking; stream is a hipStream_t (NULL = the context's own
  * stream, which the synchronous calls also use).
  *   d_root_bits : device [n_progs][ceil(n_assign/64)] u64 (may be NULL)
- *   d_first_sat : device [n_progs] u64, atomicMin'ed (preset to ~0)     */
+ *   d_first_sat : device [n_progs] u64, atomicMin'ed (preset to ~0)
+ * Launches may be queued on several caller streams: freeing a program or a
+ * batch waits for the last launch on every stream the context has seen
+ * before its device block is reused.                                       */
 int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, mg_batch** out);
 void mg_batch_free(mg_batch* batch);
 int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* batch, uint64_t seed, uint64_t first_index,
@@ -137,14 +140,20 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_
 /* Compiled programs (batch path without interpretive dispatch; built on the
  * host by mythril_amd/jit.py): ``image`` is a gfx950 code object holding the
  * straight-line code of programs[0..n_progs) and their entry table
- * ``mg_jit_table`` (row i: entry offset from the table, fingerprint of the
- * records program i was compiled from).  Attaching points each program's
- * descriptor at its code; evaluations of those programs — and batches
- * created afterwards — then run the code instead of dispatching records
- * (same results, same kernel).  MG_E_ARG when a row's fingerprint is not the
- * loaded program's (code compiled for other records is never entered).
+ * ``mg_jit_table``: row 0 = (MG_JIT_MAGIC, the first 16 hex digits of
+ * mg_asm_digest() of the interpreter the code was generated for — pinned
+ * registers, descriptor layout), row i + 1 = (entry offset of program i from
+ * the table, fingerprint of the records program i was compiled from: every
+ * word of its records with handler ids in word 0).  Attaching points each
+ * program's descriptor at its code; evaluations of those programs — and
+ * batches created afterwards — then run the code instead of dispatching
+ * records (same results, same kernel).  MG_E_ARG when the header names
+ * another interpreter, an entry lies outside the image's executable sections
+ * or a row's fingerprint is not the loaded program's (code compiled for other
+ * records — another opcode, variant, operand or constant — is never entered).
  * Same role as mg_load_program for Optimize.add (solver.py:28-37),
  * specialised for the batched evaluation (laser/smt/model.py:44-59). */
+#define MG_JIT_MAGIC 0x4D474A4954763033ull   /* "MGJITv03" */
 int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const void* image,
                   size_t image_size, mg_jit** out);
 /* Back to the interpreter for those programs; unloads the code object.

@@ -15,6 +15,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <map>
+#include <elf.h>
 
 #include "mythgpu.h"
 #include "mythgpu_ir.h"
@@ -56,10 +57,11 @@ struct mg_ctx {
     std::vector<void*> slabs, large;
     uint8_t* slab_cur = nullptr;
     size_t slab_left = 0;
-    // the last launch on a caller's stream (mg_batch_eval_gen): a block is
-    // reused only after it completed
-    hipEvent_t ext_ev = nullptr;
-    bool ext_pending = false;
+    // the last launch on each caller stream (mg_batch_eval_gen), one event
+    // per stream: a freed block is reused only after every launch that
+    // might read it completed, on whichever streams they were queued
+    struct ext_stream { hipStream_t stream; hipEvent_t ev; bool pending; };
+    std::vector<ext_stream> ext;
     // pinned host staging for program uploads (grow-only): the blob is
     // assembled in place and copied at pinned-DMA rate; a leaf-pool-heavy
     // search program is ~1 MB (the pools' (v-1, v, v+1) triples)
@@ -96,19 +98,34 @@ struct mg_prog {
     uint64_t rec_fp = 0;            // records' fingerprint (rec_fingerprint)
 };
 
-// Fingerprint of a program's uploaded records: sum of the operand words
-// (words 1..7 of each record; word 0 is this library's handler offset) times
-// successive powers of 0x100000001B3 mod 2^64, plus the record count
-// (mythril_amd/jit.py records_fingerprint).  A compiled-program image carries
-// it per entry, so mg_jit_attach refuses code built for other records.
+// Fingerprint of a program's records with HANDLER IDS in word 0 (the
+// translator run with the identity table, before word 0 becomes this
+// library's handler offset): every word times successive powers of
+// 0x100000001B3 mod 2^64, plus the record count (mythril_amd/jit.py
+// records_fingerprint).  The handler id names the operation and its variant,
+// so two programs whose records differ only in an opcode (ADD / SUB, ULT /
+// SLT) differ here.  A compiled-program image carries it per entry, so
+// mg_jit_attach refuses code built for other records.
 static uint64_t rec_fingerprint(const std::vector<uint32_t>& rec) {
     uint64_t h = 0, p = 1;
     for (size_t r = 0; r + 8 <= rec.size(); r += 8)
-        for (int k = 1; k < 8; ++k) {
+        for (int k = 0; k < 8; ++k) {
             p *= 0x100000001B3ull;
             h += (uint64_t)rec[r + k] * p;
         }
     return h + rec.size() / 8;
+}
+
+// The identity handler table: the translator then writes handler ids into
+// word 0 (fingerprinted, then mapped through the context's offsets).
+static const uint32_t* identity_handlers() {
+    static uint32_t t[MGA_NUM_HANDLERS];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t h = 0; h < MGA_NUM_HANDLERS; ++h) t[h] = h;
+        init = true;
+    }
+    return t;
 }
 
 static uint32_t kernel_lds_slots(const mg_ctx* ctx, uint32_t n_lds) {
@@ -197,16 +214,34 @@ static hipError_t dev_alloc(mg_ctx* ctx, size_t bytes, void** out, size_t* cls) 
 }
 
 // Back to its class list once no queued launch can still read it: the
-// context stream and the last caller-stream launch are waited for (what the
-// hipFree this replaces did by synchronising the device).
+// context stream and the last launch on every caller stream are waited for
+// (what the hipFree this replaces did by synchronising the device).
 static void dev_release(mg_ctx* ctx, void* p, size_t cls) {
     if (!p) return;
     (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->ext_pending) {
-        (void)hipEventSynchronize(ctx->ext_ev);
-        ctx->ext_pending = false;
-    }
+    for (auto& x : ctx->ext)
+        if (x.pending) {
+            (void)hipEventSynchronize(x.ev);
+            x.pending = false;
+        }
     ctx->free_blocks[cls].push_back(p);
+}
+
+// Note a launch on a caller stream (its event is recorded after it).
+static hipError_t ext_launched(mg_ctx* ctx, hipStream_t s) {
+    for (auto& x : ctx->ext)
+        if (x.stream == s) {
+            x.pending = true;
+            return hipEventRecord(x.ev, s);
+        }
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) {                 // no event: fall back to waiting now
+        (void)hipStreamSynchronize(s);
+        return e;
+    }
+    ctx->ext.push_back({s, ev, true});
+    return hipEventRecord(ev, s);
 }
 
 static int workspace(mg_ctx* ctx, size_t bytes, void** out) {
@@ -297,8 +332,7 @@ int mg_init(int device, mg_ctx** out) {
         delete ctx;
         return MG_E_HIP;
     }
-    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->ext_ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
         mg_free(ctx);
         return MG_E_HIP;
     }
@@ -333,7 +367,10 @@ void mg_free(mg_ctx* ctx) {
     for (void* q : ctx->slabs) (void)hipFree(q);
     for (void* q : ctx->large) (void)hipFree(q);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
-    if (ctx->ext_ev) (void)hipEventDestroy(ctx->ext_ev);
+    for (auto& x : ctx->ext) {
+        (void)hipEventSynchronize(x.ev);
+        (void)hipEventDestroy(x.ev);
+    }
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -363,10 +400,12 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
                       n_probes);
     if (rc) return rc;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
-    // assembly records + translator masks (appended to the constant table)
+    // assembly records + translator masks (appended to the constant table);
+    // word 0 holds handler ids until the fingerprint is taken
     std::vector<uint32_t> rec;
     MaskPool pool;
-    mg_translate_records(ctx->hoff, code, n_ins, n_consts, kernel_lds_slots(ctx, n_spill_slots), rec, pool);
+    mg_translate_records(identity_handlers(), code, n_ins, n_consts,
+                         kernel_lds_slots(ctx, n_spill_slots), rec, pool);
     const uint32_t n_masks = (uint32_t)(pool.words.size() / 8);
     const uint32_t n_const_all = n_consts + n_masks + n_consts * 3;
     // device leaf descriptors: byte pool offsets and the per-leaf stream salt
@@ -382,25 +421,22 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     // LEAFD records carry their leaf's generator parameters (asmgen.py
     // LEAFD_*: no descriptor load in the handler): pool offset, salt, pool
     // size and the class thresholds packed one per byte
-    {
-        std::vector<uint32_t> leafd_off;
-        for (uint32_t var = 0; var < MG_NREG; ++var)
-            for (uint32_t w = 0; w < 2; ++w)
-                for (int bank = 0; bank < 2; ++bank)
-                    leafd_off.push_back(ctx->hoff[MGA_HID(MGA_LEAFD, var | (w ? MGA_V_WAITD : 0), bank)]);
-        for (size_t r = 0; r + 8 <= rec.size(); r += 8) {
-            if (std::find(leafd_off.begin(), leafd_off.end(), rec[r]) == leafd_off.end()) continue;
-            const uint32_t li = rec[r + 4];
-            if (li >= n_leaves) continue;            // eval mode only (no generator)
-            const mg_leafgen_dev& g = gdev[li];
-            rec[r + 1] = g.pool_off_b;
-            rec[r + 2] = g.salt_lo;
-            rec[r + 3] = g.salt_hi;
-            rec[r + 5] = g.pool_n;
-            rec[r + 7] = g.pct_uniform | g.pct_small << 8 | g.pct_boundary << 16;
-        }
+    for (size_t r = 0; r + 8 <= rec.size(); r += 8) {
+        if (rec[r] >= MGA_NUM_HANDLERS || rec[r] / (2 * MGA_NVAR) != MGA_LEAFD) continue;
+        const uint32_t li = rec[r + 4];
+        if (li >= n_leaves) continue;            // eval mode only (no generator)
+        const mg_leafgen_dev& g = gdev[li];
+        rec[r + 1] = g.pool_off_b;
+        rec[r + 2] = g.salt_lo;
+        rec[r + 3] = g.salt_hi;
+        rec[r + 5] = g.pool_n;
+        rec[r + 7] = g.pct_uniform | g.pct_small << 8 | g.pct_boundary << 16;
     }
     const uint64_t rec_fp = rec_fingerprint(rec);
+    // handler ids -> this library's handler offsets (the zeroed pad record
+    // stays zero)
+    for (size_t r = 0; r + 8 <= rec.size(); r += 8)
+        if (r + 8 < rec.size() || rec[r] != 0) rec[r] = ctx->hoff[rec[r] % MGA_NUM_HANDLERS];
     // 8 zeroed NOPs after the IR code: the C++ interpreter prefetches ahead
     const size_t code_b = (size_t)(n_ins + 8) * 16, const_b = (size_t)n_const_all * 32,
                  gen_b = gdev.size() * sizeof(mg_leafgen_dev), rec_b = rec.size() * 4;
@@ -684,10 +720,7 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
         run.first_index = first_index;
         HIPCHECK(ctx, launch(ctx, 1, b->d_descs + p0, np, run, b->max_lds, s));
     }
-    if (s != ctx->stream) {
-        HIPCHECK(ctx, hipEventRecord(ctx->ext_ev, s));
-        ctx->ext_pending = true;
-    }
+    if (s != ctx->stream) HIPCHECK(ctx, ext_launched(ctx, s));
     return MG_OK;
 }
 
@@ -752,13 +785,60 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
     return MG_OK;
 }
 
+// The byte range of the executable sections of a code object and the
+// address of its mg_jit_table symbol (both as link-time virtual addresses),
+// read from the ELF itself with every offset bounds-checked: the entries an
+// image names must lie in its code.
+struct jit_layout {
+    std::vector<std::pair<uint64_t, uint64_t>> text;   // [begin, end) of SHF_EXECINSTR sections
+    uint64_t table = 0;
+    bool found = false;
+};
+
+static bool elf_layout(const uint8_t* img, size_t n, jit_layout* out) {
+    if (n < sizeof(Elf64_Ehdr) || memcmp(img, ELFMAG, SELFMAG) != 0 || img[EI_CLASS] != ELFCLASS64)
+        return false;
+    Elf64_Ehdr eh;
+    memcpy(&eh, img, sizeof eh);
+    if (eh.e_shentsize != sizeof(Elf64_Shdr) || eh.e_shoff > n ||
+        (uint64_t)eh.e_shnum * sizeof(Elf64_Shdr) > n - eh.e_shoff)
+        return false;
+    std::vector<Elf64_Shdr> sh(eh.e_shnum);
+    if (eh.e_shnum) memcpy(sh.data(), img + eh.e_shoff, eh.e_shnum * sizeof(Elf64_Shdr));
+    for (const Elf64_Shdr& s : sh)
+        if ((s.sh_flags & SHF_EXECINSTR) && s.sh_size)
+            out->text.push_back({s.sh_addr, s.sh_addr + s.sh_size});
+    for (const Elf64_Shdr& s : sh) {
+        if ((s.sh_type != SHT_SYMTAB && s.sh_type != SHT_DYNSYM) || s.sh_link >= sh.size() ||
+            s.sh_entsize != sizeof(Elf64_Sym) || s.sh_offset > n || s.sh_size > n - s.sh_offset)
+            continue;
+        const Elf64_Shdr& st = sh[s.sh_link];
+        if (st.sh_offset > n || st.sh_size > n - st.sh_offset) continue;
+        const char* names = (const char*)img + st.sh_offset;
+        for (uint64_t k = 0; k < s.sh_size / sizeof(Elf64_Sym); ++k) {
+            Elf64_Sym sym;
+            memcpy(&sym, img + s.sh_offset + k * sizeof(Elf64_Sym), sizeof sym);
+            static const char want[] = "mg_jit_table";
+            if (sym.st_name + sizeof want > st.sh_size) continue;
+            if (memcmp(names + sym.st_name, want, sizeof want) == 0) {
+                out->table = sym.st_value;
+                out->found = true;
+                return true;
+            }
+        }
+    }
+    return true;
+}
+
 // Compiled programs: load the code object, read its entry table
-// (mg_jit_table: each program's entry relative to the table) and point the
-// programs' descriptors at their code.  Batches created afterwards copy the
-// entries; the interpreter kernel then calls the code instead of
-// dispatching records.  Every entry must lie inside the image's text, ahead
-// of the table (checked) so a malformed image cannot send the kernel to an
-// arbitrary address.
+// (mg_jit_table: a header row (MG_JIT_MAGIC, the asm digest of the
+// interpreter the code was generated with: pinned registers, descriptor
+// layout), then per program its entry relative to the table and its records'
+// fingerprint) and point the programs' descriptors at their code.  Batches
+// created afterwards copy the entries; the interpreter kernel then calls the
+// code instead of dispatching records.  Every entry must lie inside an
+// executable section of the image (read from its ELF headers) so a malformed
+// image cannot send the kernel to an arbitrary address.
 int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const void* image,
                   size_t image_size, mg_jit** out) {
     if (!ctx || !out || !image || !image_size || (n_progs && !progs))
@@ -766,45 +846,56 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
     *out = nullptr;
     for (uint32_t i = 0; i < n_progs; ++i)
         if (!progs[i] || progs[i]->ctx != ctx) return fail(ctx, MG_E_ARG, "program %u", i);
+    jit_layout lay;
+    if (!elf_layout((const uint8_t*)image, image_size, &lay) || !lay.found || lay.text.empty())
+        return fail(ctx, MG_E_ARG, "JIT image: not a code object with mg_jit_table and code");
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     hipModule_t mod = nullptr;
     HIPCHECK(ctx, hipModuleLoadData(&mod, image));
     hipDeviceptr_t d_table = nullptr;
     size_t table_b = 0;
     hipError_t e = hipModuleGetGlobal(&d_table, &table_b, mod, "mg_jit_table");
-    // rows: (entry - table, records' fingerprint)
-    std::vector<int64_t> row(2 * (size_t)n_progs);
-    if (e == hipSuccess && table_b != (size_t)n_progs * 16) e = hipErrorInvalidValue;
-    if (e == hipSuccess && n_progs)
-        e = hipMemcpy(row.data(), d_table, table_b, hipMemcpyDeviceToHost);
+    // row 0: header; rows 1..n: (entry - table, records' fingerprint)
+    std::vector<int64_t> row(2 * ((size_t)n_progs + 1));
+    if (e == hipSuccess && table_b != ((size_t)n_progs + 1) * 16) e = hipErrorInvalidValue;
+    if (e == hipSuccess) e = hipMemcpy(row.data(), d_table, table_b, hipMemcpyDeviceToHost);
     if (e != hipSuccess) {
         (void)hipModuleUnload(mod);
         return fail(ctx, MG_E_HIP, "JIT image: %s (table %zu bytes for %u programs)",
                     hipGetErrorString(e), table_b, n_progs);
     }
-    // (segment alignment can place the table past the file size; the bound
-    // only guards against garbage)
+    const uint64_t want_digest = strtoull(mg_asm_digest(), nullptr, 16);
+    if ((uint64_t)row[0] != MG_JIT_MAGIC || (uint64_t)row[1] != want_digest) {
+        (void)hipModuleUnload(mod);
+        return fail(ctx, MG_E_ARG, "JIT image: built for another interpreter (header %016llx, "
+                    "asm digest %016llx; this library %016llx)", (unsigned long long)row[0],
+                    (unsigned long long)row[1], (unsigned long long)want_digest);
+    }
     for (uint32_t i = 0; i < n_progs; ++i) {
-        const int64_t rel = row[2 * i];
-        if (rel == 0 && row[2 * i + 1] == 0) continue;     // not compiled: interpreter
-        if (rel >= 0 || -rel > 2 * (int64_t)image_size + (1 << 20) || (rel & 3)) {
+        const int64_t rel = row[2 * (i + 1)];
+        const uint64_t fp = (uint64_t)row[2 * (i + 1) + 1];
+        if (rel == 0 && fp == 0) continue;                  // not compiled: interpreter
+        const uint64_t at = lay.table + (uint64_t)rel;
+        bool inside = false;
+        for (const auto& t : lay.text) inside |= at >= t.first && at + 4 <= t.second;
+        if (!inside || (rel & 3)) {
             (void)hipModuleUnload(mod);
             return fail(ctx, MG_E_ARG, "JIT image: entry %u at %lld outside the code", i,
                         (long long)rel);
         }
-        if ((uint64_t)row[2 * i + 1] != progs[i]->rec_fp) {
+        if (fp != progs[i]->rec_fp) {
             (void)hipModuleUnload(mod);
             return fail(ctx, MG_E_ARG, "JIT image: entry %u was compiled for other records "
                         "(fingerprint %016llx, loaded program %016llx)", i,
-                        (unsigned long long)row[2 * i + 1], (unsigned long long)progs[i]->rec_fp);
+                        (unsigned long long)fp, (unsigned long long)progs[i]->rec_fp);
         }
     }
     mg_jit* j = new mg_jit();
     j->ctx = ctx;
     j->module = mod;
     for (uint32_t i = 0; i < n_progs; ++i) {
-        if (row[2 * i] == 0) continue;                      // stays on the interpreter
-        const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)row[2 * i];
+        if (row[2 * (i + 1)] == 0) continue;                // stays on the interpreter
+        const uint64_t entry = (uint64_t)(uintptr_t)d_table + (uint64_t)row[2 * (i + 1)];
         e = hipMemcpy((uint8_t*)progs[i]->d_desc + offsetof(mg_pdesc, jit_entry), &entry,
                       sizeof entry, hipMemcpyHostToDevice);
         if (e == hipSuccess) memcpy(&progs[i]->h_desc.jit_entry, &entry, sizeof entry);

@@ -13,7 +13,7 @@
 #include "mythgpu_ir.h"
 #include "mg_asm_handlers.h"
 
-#define MG_VERSION 2
+#define MG_VERSION 3
 
 // Translator mask entries, appended to a program's constant table.
 struct MaskPool {

@@ -956,18 +956,22 @@ def decode(h: int) -> Tuple[str, int]:
 FP_MUL = 0x100000001B3
 
 
+JIT_MAGIC = 0x4D474A4954763033             # include/mythgpu.h MG_JIT_MAGIC
+
+
 def records_fingerprint(rec) -> int:
-    """Fingerprint of a program's records as mg_load_program uploads them
-    (zeroed pad record included): sum of the operand words (words 1..7 of
-    every record; word 0 is the library's handler offset) times successive
-    powers of FP_MUL, mod 2^64, plus the record count.  mg_jit_attach refuses
-    an image entry whose fingerprint is not the loaded program's
+    """Fingerprint of a program's records as mg_load_program fingerprints
+    them (handler ids in word 0, LEAFD records patched, zeroed pad record
+    included): every word times successive powers of FP_MUL, mod 2^64, plus
+    the record count.  The handler id carries the operation and its variant,
+    so records that differ only in an opcode differ here.  mg_jit_attach
+    refuses an image entry whose fingerprint is not the loaded program's
     (mg_api.cpp rec_fingerprint)."""
-    w = np.ascontiguousarray(np.asarray(rec, dtype=np.uint64).reshape(-1, 8)[:, 1:]).reshape(-1)
+    w = np.ascontiguousarray(np.asarray(rec, dtype=np.uint64)).reshape(-1)
     with np.errstate(over="ignore"):
         pw = np.cumprod(np.full(w.size, FP_MUL, dtype=np.uint64), dtype=np.uint64)
         h = int(np.sum(w * pw, dtype=np.uint64))
-    return (h + len(w) // 7) & ((1 << 64) - 1)
+    return (h + len(w) // 8) & ((1 << 64) - 1)
 
 
 def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6, full: bool = False):
@@ -1134,17 +1138,20 @@ def chunk_asm(items, first: int, lds_slots: int = 6, fps: Optional[List[int]] = 
 
 
 def table_asm(fps: Sequence[Optional[int]]) -> str:
-    """The stub kernel and ``mg_jit_table``: row i = (mg_jp<i> - table,
-    fingerprint of program i's records), or (0, 0) for a program that was
-    not compiled (JitUnsupported: mg_jit_attach leaves it on the
-    interpreter)."""
+    """The stub kernel and ``mg_jit_table``: a header row (JIT_MAGIC, the
+    interpreter's asm digest: the code is generated from its handlers and
+    assumes its pinned registers and descriptor layout), then row i + 1 =
+    (mg_jp<i> - table, fingerprint of program i's records), or (0, 0) for a
+    program that was not compiled (JitUnsupported: mg_jit_attach leaves it on
+    the interpreter)."""
     stub = open(STUB).read()
     cut = stub.index("\t.ident")
-    rows = "".join(("\t.quad mg_jp%d - . + %d\n\t.quad 0x%x\n" % (i, 16 * i, fp)) if fp is not None
-                   else "\t.quad 0\n\t.quad 0\n" for i, fp in enumerate(fps))
+    head = "\t.quad 0x%x\n\t.quad 0x%s\n" % (JIT_MAGIC, G.digest()[:16])
+    rows = "".join(("\t.quad mg_jp%d - . + %d\n\t.quad 0x%x\n" % (i, 16 * (i + 1), fp))
+                   if fp is not None else "\t.quad 0\n\t.quad 0\n" for i, fp in enumerate(fps))
     return (stub[:cut] + "\t.data\n\t.globl mg_jit_table\n\t.protected mg_jit_table\n"
-            "\t.type mg_jit_table,@object\n\t.p2align 3\nmg_jit_table:\n" + rows +
-            "\t.size mg_jit_table, %d\n" % (16 * len(fps)) + stub[cut:])
+            "\t.type mg_jit_table,@object\n\t.p2align 3\nmg_jit_table:\n" + head + rows +
+            "\t.size mg_jit_table, %d\n" % (16 * (len(fps) + 1)) + stub[cut:])
 
 
 def _as(text: str, obj: str) -> None:
@@ -1167,17 +1174,24 @@ def _chunk_job(args):
 
 def source_digest() -> str:
     """Digest of everything a compiled image depends on: the Python compiler
-    and generator sources and the C++ translator (the records)."""
+    and generator sources, the C++ translator (the records), the public
+    headers (IR and descriptor layout), the generated interpreter's own
+    digest, and the environment knobs that change rendered handler bodies or
+    programs (a cached image must not survive an A/B knob)."""
     import hashlib
     h = hashlib.sha1(ARCH.encode())
     pkg = os.path.dirname(os.path.abspath(__file__))
-    for sub in ("", "smt", "csrc"):
-        d = os.path.join(pkg, sub)
+    inc = os.path.join(os.path.dirname(pkg), "include")
+    for d in (pkg, os.path.join(pkg, "smt"), os.path.join(pkg, "csrc"), inc):
         for f in sorted(os.listdir(d)):
             if f.endswith((".py", ".cpp", ".h")):
                 with open(os.path.join(d, f), "rb") as fh:
                     h.update(f.encode() + fh.read())
-    h.update(("coalesce=%d flush=%d" % (COALESCE, COLD_FLUSH)).encode())
+    from . import ir
+    knobs = {"coalesce": COALESCE, "flush": COLD_FLUSH, "asm": G.digest(),
+             "div_bits_first": G.DIV_BITS_FIRST, "probe": G._PROBE,
+             "leaf_remat": ir.LEAF_REMAT, "keep_clean": ir.KEEP_CLEAN}
+    h.update(repr(sorted(knobs.items())).encode())
     return h.hexdigest()[:16]
 
 

@@ -548,7 +548,10 @@ def _known_miss(key: frozenset, n_cand: int) -> bool:
         return False
     for c in key:
         for m in _miss_index.get(c, ()):
-            if len(m) < len(key) and m <= key:        # a proper subset missed
+            # a proper subset missed, searched at least as far as this query
+            # would be (a small batch_is_possible miss must not stop a full
+            # get_model search of its supersets)
+            if len(m) < len(key) and m <= key and _group_miss.get(m, -1) >= n_cand:
                 return True
     return False
 
@@ -792,8 +795,9 @@ def _take(d: dict, key):
 _engine_failed: Optional[str] = None
 
 
-def _prefilter(key, constraints, timeout: int):
-    """GPU path of get_model: a model, or None (miss / rejected witness)."""
+def _prefilter(key, constraints, timeout: int, enforce_execution_time: bool = False):
+    """GPU path of get_model: a model, or None (miss / rejected witness).
+    The witness check gets what is left of the execution time (``_deadline``)."""
     global _engine_failed
     hit = _take(_batch_witness, key)
     if hit is None:
@@ -811,6 +815,10 @@ def _prefilter(key, constraints, timeout: int):
         finally:
             stats.gpu_time += time.perf_counter() - t0
         if hit is None:
+            return None
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:                      # get_model's fallback raises UnsatError
             return None
     m = _accept(constraints, hit[0], hit[1], timeout)
     if m is not None:
@@ -833,7 +841,7 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
 
     if not minimize and not maximize:
         try:
-            m = _prefilter(key, constraints, timeout)
+            m = _prefilter(key, constraints, timeout, enforce_execution_time)
             if m is not None:
                 return m
         except Unsupported as e:
@@ -845,8 +853,23 @@ def get_model(constraints, minimize=(), maximize=(), enforce_execution_time=True
         stats.fallbacks += 1
     # the fallback gets the reference's own timeout (support/model.py:26-31),
     # not what the pre-filter left of it: a GPU miss must not turn a query z3
-    # solves near its timeout into an ``unknown`` -> UnsatError prune
+    # solves near its timeout into an ``unknown`` -> UnsatError prune.  Under
+    # enforce_execution_time it is still capped by the execution time left
+    # NOW (minus the reference's 500 ms), so the GPU phase cannot push the
+    # analysis past --execution-timeout
+    timeout = _deadline(timeout, enforce_execution_time)
     return _z3_check(constraints, minimize, maximize, timeout)
+
+
+def _deadline(timeout: int, enforce_execution_time: bool) -> int:
+    """``timeout`` capped by the execution time left at this moment minus
+    500 ms (the reference's rule, support/model.py:26-31, re-applied after
+    the GPU phase); <= 0 raises UnsatError exactly as at the entry."""
+    if enforce_execution_time:
+        timeout = min(timeout, time_handler.time_remaining() - 500)
+        if timeout <= 0:
+            raise UnsatError
+    return timeout
 
 
 def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool]:

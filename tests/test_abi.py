@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_without_gpu():
-    assert load_library().mg_version() == 2
+    assert load_library().mg_version() == 3
 
 
 def test_ir_header_matches_python_table():

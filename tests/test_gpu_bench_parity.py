@@ -172,3 +172,100 @@ def test_program_freed_while_attached_leaves_its_image(engine):
     after = engine.eval_gen(lp2, bench.SEED, 5, 4096, want_probes=True)
     assert np.array_equal(before[0], after[0])
     assert (before[1] is None and after[1] is None) or np.array_equal(before[1], after[1])
+
+
+def test_jit_attach_refuses_an_opcode_twin(engine):
+    """programs whose records differ only in an operation (ADD vs
+    XOR, the handler id in word 0) must not share a fingerprint: the image of
+    one is refused for the other, and accepted for itself."""
+    from mythril_amd import jit
+    from mythril_amd.engine import EngineError
+    from test_jit import opcode_twins
+    p_add, p_xor = opcode_twins()
+    image = jit.compile_batch([(p_add, None, 1)])
+    with pytest.raises(EngineError, match="other records"):
+        engine.jit_attach([engine.load(p_xor, default_leafgen(p_xor), prog_seed=1)], image)
+    lp = engine.load(p_add, default_leafgen(p_add), prog_seed=1)
+    engine.jit_detach(engine.jit_attach([lp], image))
+
+
+def test_jit_attach_refuses_another_interpreter_and_stray_entries(engine, monkeypatch):
+    """The table header carries the asm digest of the interpreter the code
+    was generated for (pinned registers, descriptor layout): an image made
+    for another one is refused.  An entry pointing outside the image's
+    executable sections (here: into the table itself) is refused too."""
+    from mythril_amd import jit
+    from mythril_amd.engine import EngineError
+    d1, p1, _, _ = bench.compile_unit(("c2", 1))
+    lp = engine.load(p1, default_leafgen(p1), prog_seed=d1)
+    real = jit.table_asm
+    monkeypatch.setattr(jit.G, "digest", lambda *a: "0123456789abcdef")
+    stale = jit.compile_batch([(p1, None, d1)])
+    monkeypatch.undo()
+    with pytest.raises(EngineError, match="another interpreter"):
+        engine.jit_attach([lp], stale)
+
+    def stray(fps):
+        return real(fps).replace("\t.quad mg_jp0 - . + 16\n", "\t.quad 16\n")
+    monkeypatch.setattr(jit, "table_asm", stray)
+    bad = jit.compile_batch([(p1, None, d1)])
+    monkeypatch.undo()
+    with pytest.raises(EngineError, match="outside the code"):
+        engine.jit_attach([lp], bad)
+    engine.jit_detach(engine.jit_attach([lp], jit.compile_batch([(p1, None, d1)])))
+
+
+def test_free_waits_for_launches_on_every_caller_stream(engine):
+    """a long batch queued on caller stream A, then a short one on
+    stream B; the first batch and its programs are freed at once and new
+    programs are loaded into the recycled device blocks.  The free must wait
+    for A too (not only the last stream), so A's results equal a clean run."""
+    hip = C.CDLL("libamdhip64.so.7")
+    ids_a, ids_b, ids_c = range(0, 48), range(48, 50), range(100, 148)
+    progs = {d: bench.compile_unit(("c2", d))[1] for d in list(ids_a) + list(ids_b) + list(ids_c)}
+    n = 1 << 17
+    words = n // 64
+
+    def run_on(stream, ids, d_bits, d_first, free_after=False):
+        loaded = [engine.load(progs[d], default_leafgen(progs[d]), prog_seed=d) for d in ids]
+        batch = engine.batch_create(loaded)
+        engine.batch_eval_gen(batch, SEED, 7, n, d_bits, d_first, stream)
+        return loaded, batch
+
+    def dev(nbytes):
+        p = C.c_void_p()
+        assert hip.hipMalloc(C.byref(p), C.c_size_t(nbytes)) == 0
+        return p
+
+    bits_a, first_a = dev(len(ids_a) * words * 8), dev(len(ids_a) * 8)
+    bits_b, first_b = dev(len(ids_b) * words * 8), dev(len(ids_b) * 8)
+    sa, sb = C.c_void_p(), C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(sa)) == 0 and hip.hipStreamCreate(C.byref(sb)) == 0
+    try:
+        ones = np.full(len(ids_a), shard.NONE, dtype=np.int64)
+        # reference: the same batch alone, completed
+        assert hip.hipMemcpy(first_a, ones.ctypes.data_as(C.c_void_p), C.c_size_t(ones.nbytes), 1) == 0
+        la, ba = run_on(sa.value, ids_a, bits_a.value, first_a.value)
+        assert hip.hipStreamSynchronize(sa) == 0
+        want = np.zeros((len(ids_a), words), dtype=np.uint64)
+        assert hip.hipMemcpy(want.ctypes.data_as(C.c_void_p), bits_a, C.c_size_t(want.nbytes), 2) == 0
+        engine.batch_free(ba)
+        del la
+        # the race: A long, B short, free A's blocks, reuse them at once
+        assert hip.hipMemsetAsync(bits_a, 0, C.c_size_t(want.nbytes), sa) == 0
+        la, ba = run_on(sa.value, ids_a, bits_a.value, first_a.value)
+        lb, bb = run_on(sb.value, ids_b, bits_b.value, first_b.value)
+        engine.batch_free(ba)
+        del la
+        lc = [engine.load(progs[d], default_leafgen(progs[d]), prog_seed=d) for d in ids_c]
+        assert hip.hipDeviceSynchronize() == 0
+        got = np.zeros_like(want)
+        assert hip.hipMemcpy(got.ctypes.data_as(C.c_void_p), bits_a, C.c_size_t(got.nbytes), 2) == 0
+        assert np.array_equal(got, want)
+        engine.batch_free(bb)
+        del lb, lc
+    finally:
+        for p in (bits_a, first_a, bits_b, first_b):
+            hip.hipFree(p)
+        hip.hipStreamDestroy(sa)
+        hip.hipStreamDestroy(sb)

@@ -78,12 +78,13 @@ def test_jit_text_has_no_scalar_stores_and_fits_the_register_budget():
 
 def test_records_fingerprint_matches_the_c_definition():
     """records_fingerprint (numpy, wrapping uint64) against a plain restatement
-    of mg_api.cpp's rec_fingerprint loop."""
+    of mg_api.cpp's rec_fingerprint loop: every word, word 0 (the handler id)
+    included."""
     rng = np.random.default_rng(5)
     rec = rng.integers(0, 1 << 32, size=8 * 37, dtype=np.uint64)
     h, p = 0, 1
     for r in range(0, len(rec), 8):
-        for k in range(1, 8):
+        for k in range(8):
             p = p * 0x100000001B3 % (1 << 64)
             h = (h + int(rec[r + k]) * p) % (1 << 64)
     assert jit.records_fingerprint(rec) == (h + 37) % (1 << 64)
@@ -91,8 +92,34 @@ def test_records_fingerprint_matches_the_c_definition():
     rec2[8 * 5 + 3] ^= 1
     assert jit.records_fingerprint(rec2) != jit.records_fingerprint(rec)
     rec2 = rec.copy()
-    rec2[8 * 5] ^= 1                          # word 0 (handler offset) is not hashed
-    assert jit.records_fingerprint(rec2) == jit.records_fingerprint(rec)
+    rec2[8 * 5] ^= 1                          # word 0 (the handler id) is hashed
+    assert jit.records_fingerprint(rec2) != jit.records_fingerprint(rec)
+
+
+def opcode_twins():
+    """Two programs whose records differ ONLY in one handler id (ADD vs XOR:
+    same operands, same variant rules, no constants)."""
+    from mythril_amd import smt
+    x, y, z = (smt.symbol_factory.BitVecSym(n, 256) for n in "xyz")
+    p_add = compile_constraints([((x + y) == z).raw])
+    p_xor = compile_constraints([((x ^ y) == z).raw])
+    return p_add, p_xor
+
+
+def test_fingerprint_tells_opcode_twins_apart():
+    """the fingerprint skipped word 0, so programs differing only
+    in an opcode shared it and an image for one was accepted for the other."""
+    from mythril_amd.engine import translate_records
+    p_add, p_xor = opcode_twins()
+    ra, _ = translate_records(p_add)
+    rx, _ = translate_records(p_xor)
+    ra, rx = ra.reshape(-1, 8), rx.reshape(-1, 8)
+    assert ra.shape == rx.shape
+    diff = np.argwhere(ra != rx)
+    assert diff.size and set(diff[:, 1].tolist()) == {0}      # only handler ids differ
+    fa = jit.records_fingerprint(jit.program_records(p_add, default_leafgen(p_add), 1, full=True)[0])
+    fx = jit.records_fingerprint(jit.program_records(p_xor, default_leafgen(p_xor), 1, full=True)[0])
+    assert fa != fx
 
 
 def test_jit_image_entries_point_at_each_program():
@@ -109,7 +136,7 @@ def test_jit_image_entries_point_at_each_program():
         fh.write(image)
     syms = subprocess.run([jit.LLVM_BIN + "/llvm-readelf", "-s", "/tmp/_mg_jit_test.hsaco"],
                           capture_output=True, text=True, check=True).stdout
-    tab = int(re.search(r"([0-9a-f]+)\s+80 OBJECT\s+GLOBAL\s+\w+\s+\d+ mg_jit_table", syms).group(1), 16)
+    tab = int(re.search(r"([0-9a-f]+)\s+96 OBJECT\s+GLOBAL\s+\w+\s+\d+ mg_jit_table", syms).group(1), 16)
     data = subprocess.run([jit.LLVM_BIN + "/llvm-objdump", "-s", "-j", ".data",
                            "/tmp/_mg_jit_test.hsaco"], capture_output=True, text=True,
                           check=True).stdout
@@ -127,11 +154,14 @@ def test_jit_image_entries_point_at_each_program():
         m = re.search(r"^\s+(\S+).*//\s*([0-9A-F]+):", line)
         if m:
             at[int(m.group(2), 16)] = m.group(1)
+    assert words[tab] | words[tab + 4] << 32 == jit.JIT_MAGIC
+    assert words[tab + 8] | words[tab + 12] << 32 == int(jit.G.digest()[:16], 16)
     for i, (p, g, s) in enumerate(items):
-        rel = words[tab + 16 * i] | words[tab + 16 * i + 4] << 32
+        row = tab + 16 * (i + 1)
+        rel = words[row] | words[row + 4] << 32
         rel -= 1 << 64 if rel >> 63 else 0
         assert rel < 0
-        fp = words[tab + 16 * i + 8] | words[tab + 16 * i + 12] << 32
+        fp = words[row + 8] | words[row + 12] << 32
         full, _ = jit.program_records(p, g, s, full=True)
         assert fp == jit.records_fingerprint(full)
         text = jit.program_asm(p, g, s, "x", tag="p%d" % i)

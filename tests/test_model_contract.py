@@ -290,6 +290,58 @@ def test_gpu_miss_does_not_shorten_the_z3_timeout(monkeypatch, fresh, reset_engi
     assert seen["z3_timeout"] == 400
 
 
+def test_fallback_is_capped_by_the_execution_time_left(monkeypatch, fresh, reset_engine_memo):
+    """the fallback keeps the full solver timeout when time allows,
+    but under enforce_execution_time it is capped by what is left of the
+    execution time after the GPU phase (minus the reference's 500 ms), and
+    no time left at that point raises UnsatError as at the entry."""
+    import time
+    seen = {}
+
+    def slow_miss(nodes, budget_ms):
+        time.sleep(0.3)
+        return None
+
+    def fake_z3(constraints, minimize, maximize, timeout):
+        seen["z3_timeout"] = timeout
+        raise M.UnsatError
+    monkeypatch.setattr(M, "gpu_search", slow_miss)
+    monkeypatch.setattr(M, "_z3_check", fake_z3)
+    M.args.solver_timeout = 10000
+    M.time_handler.start_execution(1.5)          # 1500 ms: 1000 ms budget at entry
+    with pytest.raises(M.UnsatError):
+        M.get_model((c_sat(),))
+    assert 500 <= seen["z3_timeout"] <= 750       # 1500 - 300 (GPU) - 500, clock slack
+    M.get_model.cache_clear()
+    seen.clear()
+    M.time_handler.start_execution(0.8)          # 300 ms at entry, none after the GPU
+    with pytest.raises(M.UnsatError):
+        M.get_model((c_sat(),))
+    assert "z3_timeout" not in seen               # raised before asking z3
+    M.get_model.cache_clear()
+    seen.clear()
+    M.time_handler.start_execution(0.8)
+    with pytest.raises(M.UnsatError):             # enforce_execution_time=False: full timeout
+        M.get_model((c_sat(),), enforce_execution_time=False)
+    assert seen["z3_timeout"] == 10000
+
+
+def test_superset_skip_needs_a_subset_searched_as_far(monkeypatch):
+    """a miss recorded at a small candidate count (a batch) does
+    not stop a full search of a superset group; one at >= the count does."""
+    M.clear_search_memos()
+    small, full = 1 << 16, M.SEARCH_CANDIDATES
+    sub = frozenset({101, 102})
+    sup = frozenset({101, 102, 103})
+    M._note_miss(sub, small)
+    assert not M._known_miss(sup, full)
+    assert M._known_miss(sup, small)
+    M._note_miss(sub, full)
+    assert M._known_miss(sup, full)
+    assert not M._known_miss(frozenset({101, 104}), small)      # not a superset
+    M.clear_search_memos()
+
+
 def test_batch_witness_is_handed_to_get_model(batch_env, monkeypatch, reset_engine_memo):
     eng, z3_calls = batch_env
     searches = []
