@@ -27,6 +27,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -112,6 +114,42 @@ def kernel_key(lib_digest, workload, dags, assign_log2, jit, corpus=None):
     return key
 
 
+def node_image(workload, corpus, workers, world):
+    """(compiled-program image of ``corpus``, was it cached).  At world > 1
+    the ranks of a node share ONE build (jit.cached_image: the first rank to
+    take the file lock assembles with up to 64 host workers, the others wait
+    and read it), in ``$MYTHGPU_JIT_CACHE`` or a per-user directory under the
+    node's temp dir; at world 1 the image is built in process (timed as
+    ``jit_s``) unless ``$MYTHGPU_JIT_CACHE`` is set."""
+    import tempfile
+    from mythril_amd import jit
+    ids = [d for d, _, _, _ in corpus]
+    key = "%s_%d_%d_%d_%d_lds%d" % (workload, len(ids), ids[0], ids[-1], sum(ids), LDS_SLOTS)
+    cache = os.environ.get("MYTHGPU_JIT_CACHE") or (
+        os.path.join(tempfile.gettempdir(), "mythgpu_jit_%d" % os.getuid()) if world > 1 else None)
+    nw = max(workers, min(os.cpu_count() or 1, 64)) if world > 1 else workers
+    return jit.cached_image(key, lambda: jit.compile_batch(
+        [(p, None, d) for d, p, _, _ in corpus], workers=nw, lds_slots=LDS_SLOTS), cache)
+
+
+def same_image(image, world, device=None) -> str:
+    """Digest of the image (and of the sources that generate compiled code);
+    at world > 1 every rank must hold the same one (assignment axis: all
+    ranks run the same programs) — raises otherwise."""
+    import hashlib
+    from mythril_amd import jit
+    dg = hashlib.sha1(image + jit.code_digest().encode()).hexdigest()[:15]
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        v = int(dg, 16)
+        t = torch.tensor([v, -v], dtype=torch.int64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        if int(t[0]) != v or -int(t[1]) != v:
+            raise RuntimeError("ranks hold different compiled-program images (this rank %s)" % dg)
+    return dg
+
+
 def my_dags(mode, n_dags, rank, world, workload="c2"):
     """DAG ids this rank evaluates: every DAG (assignment axis) or its LPT
     share of a ``n_dags x world`` corpus (corpus axis)."""
@@ -174,21 +212,38 @@ def all_sum(values, world, device=None):
     return t.tolist()
 
 
-def cpu_baseline(corpus, budget_s=20.0, workload="c2"):
+def sample_indices(corpus):
+    """Positions (in the corpus list) of the DAGs the CPU leg times and the
+    self-check compares: a stride of 64 over the corpus."""
+    return list(range(0, len(corpus), max(1, len(corpus) // 64)))[:64]
+
+
+def cpu_baseline(corpus, budget_s=20.0, workload="c2", check=None):
     """Time the C restatement oracle on a bounded sample of the same workload
-    (same DAGs, same generator) with all host cores."""
+    (same DAGs, same generator) with all host cores.
+
+    ``check`` = (first_index, n_assign, rows, firsts): the GPU's root-bit rows
+    (uint64, full width) and per-DAG first satisfying index of the LAST timed
+    step for the sampled DAGs.  The oracle then evaluates exactly those
+    candidates (indices first_index ...), so the timed CPU work doubles as a
+    bit-exact self-check of the timed process's own output: every root bit of
+    the sampled prefix, and every first index (consistent with the GPU's full
+    row, and checked by the oracle at that lane).  Returns (baseline dict,
+    selfcheck dict or None)."""
     from oracle import build as obuild
     from oracle import evalref
     obuild.build()
     # the host-core share (the GPU box exports OMP_NUM_THREADS=16 for one
     # GPU; os.cpu_count() there is the whole machine)
     threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count() or 1, 64))
+    first, n_max = (check[0], check[1]) if check is not None else (0, None)
     # calibrate on the first DAG (long enough to amortise thread start-up),
     # then spread the budget over a DAG sample
-    sample = corpus[:: max(1, len(corpus) // 64)][:64]
+    sample = [corpus[k] for k in sample_indices(corpus)]
     total_nodes = 0
     t_total = 0.0
     per_dag = None
+    outs = []
     for dag_id, prog, nodes, _ in sample:
         roots = workload_roots(workload, dag_id)
         S = evalref.serialize(roots, prog)
@@ -197,16 +252,39 @@ def cpu_baseline(corpus, budget_s=20.0, workload="c2"):
             t0 = time.perf_counter()
             evalref.run_gen(S, prog, SEED, dag_id, 0, n_cal, threads)
             rate = n_cal * nodes / max(time.perf_counter() - t0, 1e-6)
-            per_dag = max(256, int(rate * budget_s / len(sample) / max(nodes, 1)))
+            per_dag = max(4096, int(rate * budget_s / len(sample) / max(nodes, 1)))
+            if n_max is not None:
+                per_dag = min(per_dag, n_max)
         t0 = time.perf_counter()
-        evalref.run_gen(S, prog, SEED, dag_id, 0, per_dag, threads)
+        want = evalref.run_gen(S, prog, SEED, dag_id, first, per_dag, threads)
         t_total += time.perf_counter() - t0
         total_nodes += nodes * per_dag
-    return {"value": total_nodes / t_total, "unit": "node-evals/s", "cores": threads,
+        outs.append((dag_id, prog, S, want))
+    base = {"value": total_nodes / t_total, "unit": "node-evals/s", "cores": threads,
             "kind": "port",
             "sample": "%d %s DAGs x %d generated assignments (%.3g node-evals, %.1f s); "
                       "oracle/evalref.c restates z3 model evaluation (z3 not installed)"
                       % (len(sample), workload, per_dag, total_nodes, t_total)}
+    if check is None:
+        return base, None
+    from mythril_amd.engine import unpack_bits
+    _, n_assign, rows, firsts = check
+    bad_bits = bad_first = 0
+    for (dag_id, prog, S, want), row, f in zip(outs, rows, firsts):
+        got = unpack_bits(row, n_assign)
+        bad_bits += int(np.count_nonzero(got[:per_dag] != want))
+        hit = np.flatnonzero(got)
+        gpu_first = first + int(hit[0]) if hit.size else -1
+        if int(f) != gpu_first:                   # d_first disagrees with the bits
+            bad_first += 1
+        elif hit.size and int(hit[0]) >= per_dag:  # beyond the compared prefix:
+            if not evalref.run_gen(S, prog, SEED, dag_id, gpu_first, 1, threads)[0]:
+                bad_first += 1                    # the oracle must agree at that lane
+    sc = {"dags": len(outs), "lanes": per_dag, "first_index": first,
+          "mismatches": bad_bits, "first_sat_mismatches": bad_first,
+          "what": "last timed step: root bits of %d sampled units x %d candidates and their "
+                  "first satisfying index vs oracle/evalref.c" % (len(outs), per_dag)}
+    return base, sc
 
 
 def main():
@@ -250,13 +328,8 @@ def main():
     t_compile = time.time() - t0
     image, t_jit, jit_cached = None, 0.0, False
     if args.jit:                      # code generation + assembly, still before the GPU
-        from mythril_amd import jit
         t0 = time.time()
-        ids = [d for d, _, _, _ in corpus]
-        image, jit_cached = jit.cached_image(
-            "%s_%d_%d_%d_%d_lds%d" % (args.workload, len(ids), ids[0], ids[-1], sum(ids), LDS_SLOTS),
-            lambda: jit.compile_batch([(p, None, d) for d, p, _, _ in corpus], workers=workers,
-                                      lds_slots=LDS_SLOTS))
+        image, jit_cached = node_image(args.workload, corpus, workers, world)
         t_jit = time.time() - t0
     if args.jit_build_only:
         print("jit image %.1f MB in %.1f s (cached: %s)" % (len(image or b"") / 1e6, t_jit,
@@ -272,6 +345,9 @@ def main():
 
     from mythril_amd import shard
     from mythril_amd.engine import Engine, default_leafgen
+    image_digest = None
+    if image is not None:                     # assignment axis: every rank runs the same code
+        image_digest = same_image(image, world if args.shard == "assign" else 1, "cuda")
     eng = Engine(local)
     loaded = [eng.load(p, default_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
     if image is not None:
@@ -368,14 +444,26 @@ def main():
                          "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kern_ms,
                          "int32_ops_per_launch": ops_launch},
             "kernel_key": key,
+            "runtime": dict(eng.runtime_info(), torch_hip=getattr(torch.version, "hip", None),
+                            note="the library's NEEDED libamdhip64.so.7 binds to the runtime "
+                                 "torch loaded first (tests/test_gpu_torch_runtime.py checks "
+                                 "parity in that configuration)"),
             "sat_dags": sat_dags,
             "compile_s": round(t_compile, 2),
             "path": "compiled programs (mythril_amd/jit.py)" if args.jit else "interpreter",
             "jit_s": round(t_jit, 2) if args.jit else None,
             "jit_cached": jit_cached if args.jit else None,
+            "jit_image_digest": image_digest,
         }
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(corpus, workload=args.workload)
+            last = step_first(args.shard, args.warmup + args.steps - 1, rank, world, n_assign)
+            pos = sample_indices(corpus)
+            idx = torch.tensor(pos, dtype=torch.long, device="cuda")
+            rows = d_bits.index_select(0, idx).cpu().numpy().view(np.uint64)
+            firsts = d_first.index_select(0, idx).cpu().numpy()
+            firsts = np.where(firsts == shard.NONE, -1, firsts)
+            out["cpu_baseline"], out["selfcheck"] = cpu_baseline(
+                corpus, workload=args.workload, check=(last, n_assign, rows, firsts))
             out["vs_cpu"] = out["value"] / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -166,6 +166,10 @@ void mg_jit_detach(mg_jit* jit);
 int mg_keccak256(mg_ctx* ctx, const uint8_t* data, const uint64_t* offsets,
                  const uint32_t* lens, uint32_t n, uint8_t* out);
 
+/* The HIP runtime this library runs on in this process: hipRuntimeGetVersion
+ * and the file of the libamdhip64 it resolved to (a process that loaded
+ * PyTorch first binds torch's bundled runtime; bench.py reports both). */
+int mg_runtime_info(int* hip_version, char* path, size_t path_len);
 /* Library/ABI version (no GPU needed). */
 int mg_version(void);
 /* Digest of the generated gfx950 assembly the library was built from (no

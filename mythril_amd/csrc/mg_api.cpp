@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <map>
 #include <elf.h>
+#include <dlfcn.h>
 
 #include "mythgpu.h"
 #include "mythgpu_ir.h"
@@ -375,6 +376,20 @@ void mg_free(mg_ctx* ctx) {
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int mg_runtime_info(int* hip_version, char* path, size_t path_len) {
+    if (hip_version) {
+        *hip_version = 0;
+        if (hipRuntimeGetVersion(hip_version) != hipSuccess) *hip_version = 0;
+    }
+    if (path && path_len) {
+        path[0] = 0;
+        Dl_info info;
+        if (dladdr((void*)&hipRuntimeGetVersion, &info) && info.dli_fname)
+            snprintf(path, path_len, "%s", info.dli_fname);
+    }
+    return MG_OK;
 }
 
 const char* mg_last_error(const mg_ctx* ctx) { return ctx ? ctx->err.c_str() : "no context"; }

@@ -25,7 +25,8 @@ _LIB_PATH = os.environ.get("MYTHGPU_LIB") or \
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
            "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_keccak256", "mg_version", "mg_config",
-           "mg_translate", "mg_asm_digest", "mg_last_kernel_ms", "mg_jit_attach", "mg_jit_detach")
+           "mg_translate", "mg_asm_digest", "mg_last_kernel_ms", "mg_jit_attach", "mg_jit_detach",
+           "mg_runtime_info")
 
 
 class EngineUnavailable(RuntimeError):
@@ -90,6 +91,7 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_jit_attach.argtypes = [p, C.POINTER(p), u32, p, C.c_size_t, C.POINTER(p)]
         lib.mg_jit_detach.argtypes = [p]
         lib.mg_jit_detach.restype = None
+        lib.mg_runtime_info.argtypes = [C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         pu32 = C.POINTER(u32)
         lib.mg_translate.argtypes = [p, u32, u32, u32, p, u32, p, u32, pu32, p, u32, pu32]
         for name in EXPORTS:
@@ -161,6 +163,14 @@ class Engine:
         if rc != 0:
             raise EngineError("%s failed (%d): %s" % (what, rc,
                               self.lib.mg_last_error(self._ctx).decode(errors="replace")))
+
+    def runtime_info(self) -> dict:
+        """The HIP runtime the library runs on in this process (version,
+        libamdhip64 file)."""
+        v = C.c_int()
+        path = C.create_string_buffer(1024)
+        self.lib.mg_runtime_info(C.byref(v), path, 1024)
+        return {"hip_runtime_version": v.value, "libamdhip64": path.value.decode()}
 
     def last_kernel_ms(self) -> float:
         """Device time of the last synchronous eval / search call."""

@@ -1214,27 +1214,36 @@ def code_digest() -> str:
     return h.hexdigest()[:16]
 
 
-def cached_image(key: str, build) -> Tuple[bytes, bool]:
+def cached_image(key: str, build, cache_dir: Optional[str] = None) -> Tuple[bytes, bool]:
     """(image, was_cached): ``build()``'s code object, memoised in
-    ``$MYTHGPU_JIT_CACHE/<key>.hsaco`` when that variable names a directory
-    (profiling runs: the image is assembled in a separate step, so a process
-    the profiler has already attached to the GPU never starts the assembler).
+    ``<dir>/<key>_<source digest>.hsaco`` when a directory is given
+    (``cache_dir``, else ``$MYTHGPU_JIT_CACHE``).  Profiling runs assemble the
+    image in a separate step, so a process the profiler has already attached
+    to the GPU never starts the assembler; the ranks of one node share one
+    build: the file is made under an exclusive ``flock`` of ``<path>.lock``,
+    so the first rank builds while the others wait and then read it.
     ``key`` must identify the programs (workload, ids); the source digest is
     added here."""
-    d = os.environ.get("MYTHGPU_JIT_CACHE")
+    d = cache_dir or os.environ.get("MYTHGPU_JIT_CACHE")
     if not d:
         return build(), False
+    import fcntl
     os.makedirs(d, exist_ok=True)
     path = os.path.join(d, "%s_%s.hsaco" % (re.sub(r"[^\w.-]", "_", key), source_digest()))
-    if os.path.exists(path):
-        with open(path, "rb") as fh:
-            return fh.read(), True
-    image = build()
-    tmp = path + ".tmp%d" % os.getpid()
-    with open(tmp, "wb") as fh:
-        fh.write(image)
-    os.replace(tmp, path)
-    return image, False
+    with open(path + ".lock", "a+") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            if os.path.exists(path):
+                with open(path, "rb") as fh:
+                    return fh.read(), True
+            image = build()
+            tmp = path + ".tmp%d" % os.getpid()
+            with open(tmp, "wb") as fh:
+                fh.write(image)
+            os.replace(tmp, path)
+            return image, False
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
 
 
 def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,

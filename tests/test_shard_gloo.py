@@ -183,3 +183,48 @@ def test_bench_timed_loop_world2_gloo():
         want = [_local_first(d, r, lo, world * N_ASSIGN) for d, r in enumerate(dags)]
         assert out[0][1][i] == out[1][1][i] == want
     assert out[0][2] == out[1][2] == 21.0 and out[0][3] == out[1][3] == 1.0
+
+
+def _image_worker(rank, world, port, q, cache_dir):
+    """bench.py's node-shared compiled-program image at world 2: both ranks
+    ask for the same corpus's image; one builds it under the file lock, the
+    other reads it, and the digest check across ranks passes — and fails on
+    both ranks when one holds a different image."""
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["MYTHGPU_JIT_CACHE"] = cache_dir
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        corpus = bench.build_corpus(3, 1)
+        image, cached = bench.node_image("c2", corpus, 1, world)
+        dg = bench.same_image(image, world)
+        refused = False
+        try:
+            bench.same_image(image + (b"x" if rank == 1 else b""), world)
+        except RuntimeError:
+            refused = True
+        q.put((rank, cached, dg, refused))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_shares_one_image_per_node_world2_gloo(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_image_worker, args=(r, world, port, q, str(tmp_path)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {r: (c, d, f) for r, c, d, f in (q.get(timeout=300) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(out[r][0] for r in out) == [False, True]      # built once, read once
+    assert out[0][1] == out[1][1]
+    assert out[0][2] and out[1][2]                              # a differing rank is refused
+    assert len([f for f in os.listdir(tmp_path) if f.endswith(".hsaco")]) == 1
