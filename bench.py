@@ -9,11 +9,15 @@ ranks with an RCCL all-reduce(MIN) — the search's one exchange step.
 Weak scaling: rank r evaluates candidate indices [r*2^20, (r+1)*2^20) of
 every DAG's stream.
 
-``--shard corpus`` (config C5) shards the corpus axis instead: the corpus is
-``dags x world`` DAGs, split across ranks by longest-processing-time first on
-their node counts (mythril_amd/shard.py), every rank evaluates its own DAGs'
-candidates [s*2^20, (s+1)*2^20) at step s, and nothing is exchanged on the
-data path (still weak scaling: per-rank work is one corpus).
+``--workload c5`` (config C5) batches every solidity_examples contract's
+stand-in query stream (mythril_amd/workloads.py c5_queries: the C1 / C3 / C4
+contracts and the other nine) and shards the assignment space like C2, with
+the RCCL all-reduce(MIN) of the first witnesses.  ``--shard corpus`` shards
+the corpus axis instead: the corpus is ``dags x world`` units, split across
+ranks by longest-processing-time first on their DAG sizes
+(mythril_amd/shard.py), every rank evaluates its own units' candidates
+[s*2^20, (s+1)*2^20) at step s, and nothing is exchanged on the data path
+(still weak scaling: per-rank work is one corpus).
 
 Prints ONE JSON line on rank 0 (contract in the task statement).  Extra
 fields: roofline (INT32 VALU bound, see mythril_amd/roofline.py) and
@@ -51,7 +55,7 @@ def workload_roots(workload, dag_id):
     if _STREAM is None or _STREAM[0] != workload:
         from mythril_amd import workloads as W
         seen, out = set(), []
-        for q in W.queries(workload, 8 * STREAM_QUERIES):
+        for q in W.queries(workload, 8 * default_units(workload)):
             key = tuple(c.id for c in q)
             if key not in seen:
                 seen.add(key)
@@ -59,6 +63,14 @@ def workload_roots(workload, dag_id):
         _STREAM = (workload, out)
     qs = _STREAM[1]
     return qs[dag_id % len(qs)]
+
+
+def default_units(workload):
+    """Units (DAGs / distinct queries) per step: 4096 corpus DAGs (C2), the
+    256 distinct queries of a stand-in stream (C3 / C4), 512 distinct queries
+    of the all-contracts stream (C5: the thirteen solidity_examples
+    contracts, mythril_amd/workloads.py c5_queries)."""
+    return {"c2": 4096, "c5": 2 * STREAM_QUERIES}.get(workload, STREAM_QUERIES)
 
 
 def compile_unit(item):
@@ -159,8 +171,9 @@ def my_dags(mode, n_dags, rank, world, workload="c2"):
     from mythril_amd.corpus import dag_target_nodes
     if workload == "c2":
         costs = [dag_target_nodes(d, SEED) for d in range(n_dags * world)]
-    else:
-        costs = [1] * (n_dags * world)
+    else:                             # stand-in queries: their DAG sizes
+        from mythril_amd.smt import node as N
+        costs = [len(N.topo_order(workload_roots(workload, d))) for d in range(n_dags * world)]
     return shard.corpus_shard(costs, rank, world)
 
 
@@ -292,12 +305,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", choices=("c2", "c3", "c4"), default="c2",
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2",
                     help="c2: synthetic corpus (default, BASELINE configs[1]); c3 / c4: the "
-                         "BECToken / token+WalletLibrary stand-in query streams")
+                         "BECToken / token+WalletLibrary stand-in query streams; c5: every "
+                         "solidity_examples contract's stream, batched (configs[4])")
     ap.add_argument("--dags", type=int, default=None,
-                    help="DAGs per step (default 4096 for c2, %d distinct queries for c3/c4)"
-                         % STREAM_QUERIES)
+                    help="DAGs per step (default 4096 for c2, %d distinct queries for c3/c4, "
+                         "%d for c5)" % (STREAM_QUERIES, 2 * STREAM_QUERIES))
     ap.add_argument("--assign-log2", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shard", choices=("assign", "corpus"), default="assign",
@@ -313,7 +327,7 @@ def main():
     args = ap.parse_args()
     args.jit = not args.interp
     if args.dags is None:
-        args.dags = 4096 if args.workload == "c2" else STREAM_QUERIES
+        args.dags = default_units(args.workload)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -402,15 +416,19 @@ def main():
             try:
                 with open(args.traffic_json) as fh:
                     tj = json.load(fh)
-                got = tj.get("kernel_key")
-                if got == key:
-                    traffic = tj.get("hbm_bytes_per_launch")
+                entries = tj.get("entries", [tj] if "kernel_key" in tj else [])
+                hit = next((e for e in entries if e.get("kernel_key") == key), None)
+                if hit is not None:
+                    traffic = hit.get("hbm_bytes_per_launch")
                     traffic_note = ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch of this "
-                                    "kernel (profiles/traffic.json, same kernel_key)")
+                                    "kernel (profiles/traffic.json entry with the same "
+                                    "kernel_key, %s)" % hit.get("evidence", "profiles/"))
                 else:
-                    diff = sorted(k for k in key if (got or {}).get(k) != key[k])
-                    traffic_note = "profiles/traffic.json is for another kernel (%s differ)" % \
-                        ", ".join(diff)
+                    same = [e["kernel_key"] for e in entries
+                            if e.get("kernel_key", {}).get("workload") == args.workload]
+                    diff = sorted(k for k in key if (same[0] if same else {}).get(k) != key[k])
+                    traffic_note = "profiles/traffic.json has no entry for this kernel (%s " \
+                        "differ)" % ", ".join(diff)
             except (OSError, ValueError) as e:
                 traffic_note = "profiles/traffic.json unreadable: %s" % e
         workload_txt = {
@@ -418,7 +436,10 @@ def main():
             "c3": "C3 stand-in stream: %d distinct BECToken-shaped integer-overflow queries "
                   "(mythril_amd/workloads.py)" % args.dags,
             "c4": "C4 stand-in stream: %d distinct token + WalletLibrary keccak/mapping queries "
-                  "(mythril_amd/workloads.py)" % args.dags}[args.workload]
+                  "(mythril_amd/workloads.py)" % args.dags,
+            "c5": "C5 all-contracts stream: %d distinct queries of the 13 solidity_examples "
+                  "contracts' stand-in streams, batched (mythril_amd/workloads.py c5_queries)"
+                  % args.dags}[args.workload]
         out = {
             "metric": "constraint-node evals/sec",
             "value": evals / elapsed,
@@ -434,8 +455,8 @@ def main():
             "data": "synthetic (corpus seed 0x6d797468, device-generated candidates)",
             "config": {"workload": ("%s x 2^%d assignments per GPU" % (workload_txt, args.assign_log2))
                        if args.shard == "assign" else
-                       ("C5 corpus axis: %d random 256-bit DAGs (64-512 nodes) per GPU, LPT-"
-                        "sharded, x 2^%d assignments each" % (args.dags, args.assign_log2)),
+                       ("corpus axis: %s per GPU, LPT-sharded by DAG size, x 2^%d assignments "
+                        "each" % (workload_txt, args.assign_log2)),
                        "dags": args.dags * (world if args.shard == "corpus" else 1),
                        "assignments_per_gpu": n_assign, "nodes_total": int(nodes_all),
                        "shard": args.shard, "parallelism": "dp%d" % world},

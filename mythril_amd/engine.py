@@ -366,24 +366,41 @@ def limbs_to_int(limbs) -> int:
     return v
 
 
-_engines: Dict[int, Engine] = {}
+_engines: Dict[Tuple[int, int], Engine] = {}
 _failed: Dict[int, str] = {}
+_engines_lock = threading.Lock()
 
 
-def get_engine(device: int = 0) -> Engine:
-    """The device's engine; an initialisation failure is remembered, so later
-    calls raise EngineUnavailable at once instead of retrying mg_init."""
-    e = _engines.get(device)
-    if e is None:
-        if device in _failed:
-            raise EngineUnavailable(_failed[device])
-        try:
-            e = Engine(device)
-        except EngineUnavailable as x:
-            _failed[device] = str(x)
-            raise
-        except Exception as x:  # noqa: BLE001 - any init failure means no engine
-            _failed[device] = "%s: %s" % (type(x).__name__, x)
-            raise EngineUnavailable(_failed[device]) from x
-        _engines[device] = e
-    return e
+def get_engine(device: int = 0, slot: int = 0) -> Engine:
+    """The engine (one HIP context) of ``device``; ``slot`` > 0 gives further
+    independent contexts on the same device (a device listed twice in
+    ``MYTHRIL_GPU_DEVICES`` is searched from two host threads, and a context
+    serves one thread at a time).  An initialisation failure is remembered,
+    so later calls raise EngineUnavailable at once instead of retrying
+    mg_init."""
+    with _engines_lock:
+        e = _engines.get((device, slot))
+        if e is None:
+            if device in _failed:
+                raise EngineUnavailable(_failed[device])
+            try:
+                e = Engine(device)
+            except EngineUnavailable as x:
+                _failed[device] = str(x)
+                raise
+            except Exception as x:  # noqa: BLE001 - any init failure means no engine
+                _failed[device] = "%s: %s" % (type(x).__name__, x)
+                raise EngineUnavailable(_failed[device]) from x
+            _engines[(device, slot)] = e
+        return e
+
+
+def device_slots(devices) -> List[Tuple[int, int]]:
+    """(device, slot) per entry of a device list: the k-th repeat of a device
+    gets slot k, its own context."""
+    seen: Dict[int, int] = {}
+    out = []
+    for d in devices:
+        out.append((d, seen.get(d, 0)))
+        seen[d] = seen.get(d, 0) + 1
+    return out

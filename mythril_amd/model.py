@@ -33,7 +33,7 @@ from typing import Dict, List, Optional, Sequence
 
 from . import z3bridge
 from .assign import Assignment, unpack
-from .engine import EngineError, EngineUnavailable, LeafGen, get_engine
+from .engine import EngineError, EngineUnavailable, LeafGen, device_slots, get_engine
 from .ir import Program, Unsupported, compile_constraints, harvest_hints  # noqa: F401
 from .smt import node as N
 
@@ -460,14 +460,14 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
     out: List = [None] * len(progs)
 
     def run(dev, idx):
-        eng = get_engine(dev)
+        eng = get_engine(*dev)
         loaded = [eng.load(progs[i], search_leafgen(progs[i]), prog_seed=0) for i in idx]
         hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
         _count_kernel(eng)
         for i, lp, h in zip(idx, loaded, hits):
             out[i] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
     with _Phase("search"):
-        _on_devices(run, [(d, idx) for d, idx in zip(devices, parts) if idx])
+        _on_devices(run, [(d, idx) for d, idx in zip(device_slots(devices), parts) if idx])
     return out
 
 
@@ -504,14 +504,14 @@ def search_assignment_axis(prog: Program, n_cand: int, devices: Sequence[int]):
     res: List = [None] * G
 
     def run(g, dev):
-        eng = get_engine(dev)
+        eng = get_engine(*dev)
         lp = eng.load(prog, search_leafgen(prog), prog_seed=0)
         n = bounds[g + 1] - bounds[g]
         h = eng.search(lp, SEARCH_SEED, n, first_index=bounds[g]) if n else (-1, None)
         _count_kernel(eng)
         res[g] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
     with _Phase("search"):
-        _on_devices(run, list(enumerate(devices)))
+        _on_devices(run, list(enumerate(device_slots(devices))))
     found = [r for r in res if r[0] >= 0]
     return min(found, key=lambda r: r[0]) if found else (-1, None)
 

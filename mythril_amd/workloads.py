@@ -580,7 +580,422 @@ def c4_queries(n: int = 256, seed: int = 0xC4) -> List[List[N.Node]]:
     return out[:n]
 
 
-WORKLOADS = {"c1": c1_queries, "c3": c3_queries, "c4": c4_queries}
+# ---------------------------------------------------------------------------
+# C5: every solidity_examples contract, batched.  Beyond the C1 / C3 / C4
+# contracts above, the other nine (solidity_examples/*.sol) are restated
+# here the same way: the dispatcher path of each function, its requires, and
+# the query each detection module appends at the instruction it watches
+# (analysis/module/modules/*.py).
+# ---------------------------------------------------------------------------
+
+def _env(t: Tx, name: str, w: int = 256) -> S.BitVec:
+    """``GlobalState.new_bitvec``: ``{tx}_{name}`` (global_state.py:125-135)."""
+    return S.symbol_factory.BitVecSym("{}_{}".format(t.id, name), w)
+
+
+def _call(t: Tx, to: S.BitVec, checks: List[S.Bool], pc: int, checked: bool,
+          value: Optional[S.BitVec] = None) -> S.BitVec:
+    """A CALL (``instructions.py:1920-2135``): ``retval_{pc}`` on the stack;
+    the external-call module asks ``UGT(gas, 2300) ∧ to == ATTACKER``
+    (``external_calls.py:79-84``), the unchecked-retval module
+    ``retval == 1`` / ``retval == 0`` (``unchecked_retval.py:85-89``) when the
+    result is not checked, the state-change module ``UGT(gas, 2300)`` with a
+    positive value (``state_change_external_calls.py:47-62,196``)."""
+    gas = _env(t, "gas")
+    ret = _env(t, "retval_%d" % pc)
+    checks.append(S.And(S.UGT(gas, bv(2300)), to == bv(ACTORS[1])))
+    if value is not None:
+        checks.append(S.And(S.UGT(gas, bv(2300)), S.UGT(value, bv(0))))
+    if checked:
+        t.require(S.Not(ret == bv(0)))
+    else:
+        checks.append(ret == bv(1))
+        checks.append(ret == bv(0))
+    return ret
+
+
+def _ether_thief(t: Tx, checks: List[S.Bool], amount: S.BitVec) -> None:
+    """``ether_thief.py:60-72``: the attacker's balance after the transfer
+    exceeds its starting balance, and the attacker sent the transaction."""
+    bal = t.world.balance
+    start = bal[bv(ACTORS[1])]
+    bal[t.caller] = bal[t.caller] + amount
+    checks.append(S.And(S.UGT(bal[bv(ACTORS[1])], start), t.caller == bv(ACTORS[1])))
+
+
+CALLS_FUNCS = sorted(selector(x) for x in (
+    "thisisfine()", "reentrancy()", "calluseraddress(address)", "callstoredaddress()",
+    "setstoredaddress(address)", "fixed_address()", "stored_address()"))
+
+
+def _calls_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``calls.sol``: fixed / stored / user-supplied call targets."""
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    c.sstore(bv(0), c.arg_address(0))                           # fixed_address = addr
+    for _ in range(1 + rng.randrange(2)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        name = rng.choice(["thisisfine()", "reentrancy()", "calluseraddress(address)",
+                           "callstoredaddress()", "setstoredaddress(address)"])
+        t.dispatch(CALLS_FUNCS, CALLS_FUNCS.index(selector(name)))
+        t.nonpayable()
+        if name == "setstoredaddress(address)":
+            t.sstore(bv(1), t.arg_address(0))
+        else:
+            if name == "calluseraddress(address)":
+                to = t.arg_address(0)
+            else:                                               # fixed / stored address
+                to = bv(ADDR_MASK) & t.sload(bv(1 if name == "callstoredaddress()" else 0))
+            _call(t, to, checks, 0x90 + len(name), checked=False)
+            if name == "reentrancy()":
+                t.sstore(bv(2), bv(0))                          # statevar = 0 after the call
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+ETHERSTORE_FUNCS = sorted(selector(x) for x in (
+    "depositFunds()", "withdrawFunds(uint256)", "withdrawalLimit()", "lastWithdrawTime(address)",
+    "balances(address)"))
+
+
+def _etherstore_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``etherstore.sol``: deposit (``+= msg.value``, integer module) and
+    withdraw (three requires, a call with value, then state changes)."""
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    c.sstore(bv(0), bv(10 ** 18))                               # withdrawalLimit = 1 ether
+    for _ in range(1 + rng.randrange(3)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        if rng.randrange(2):
+            t.dispatch(ETHERSTORE_FUNCS, ETHERSTORE_FUNCS.index(selector("depositFunds()")))
+            slot = t.mapping(t.sender(), 2)
+            cur = t.sload(slot)
+            checks.append(S.Not(S.BVAddNoOverflow(cur, t.callvalue, False)))
+            t.sstore(slot, cur + t.callvalue)
+        else:
+            t.dispatch(ETHERSTORE_FUNCS, ETHERSTORE_FUNCS.index(selector("withdrawFunds(uint256)")))
+            t.nonpayable()
+            amt = t.arg(0)
+            slot_b = t.mapping(t.sender(), 2)
+            t.require(S.UGE(t.sload(slot_b), amt))
+            t.require(S.ULE(amt, t.sload(bv(0))))
+            now = _env(t, "timestamp")
+            last = t.sload(t.mapping(t.sender(), 1))
+            checks.append(S.Not(S.BVAddNoOverflow(last, bv(604800), False)))
+            t.require(S.UGE(now, last + bv(604800)))
+            _call(t, t.sender(), checks, 0x1F3, checked=True, value=amt)
+            _ether_thief(t, checks, amt)
+            bal = t.sload(slot_b)
+            checks.append(S.Not(S.BVSubNoUnderflow(bal, amt, False)))
+            t.sstore(slot_b, bal - amt)
+            t.sstore(t.mapping(t.sender(), 1), now)
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+EXC_FUNCS = sorted(selector(x) for x in (
+    "assert1()", "assert2()", "assert3(uint256)", "requireisfine(uint256)", "divisionby0(uint256)",
+    "thisisfine(uint256)", "arrayaccess(uint256)", "thisisalsofind(uint256)"))
+
+
+def _exceptions_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``exceptions.sol``: the exceptions module asks whether each INVALID is
+    reachable — the path to it (``exceptions.py:45-60``): ``input == 23``,
+    a zero divisor (``ISZERO(input)`` before DIV), an index >= 8."""
+    w = World(concrete_storage=True)
+    w.tx(creation=True)
+    t = w.tx()
+    name = rng.choice(["assert3(uint256)", "requireisfine(uint256)", "divisionby0(uint256)",
+                       "thisisfine(uint256)", "arrayaccess(uint256)", "thisisalsofind(uint256)"])
+    t.dispatch(EXC_FUNCS, EXC_FUNCS.index(selector(name)))
+    t.nonpayable()
+    x = t.arg(0)
+    if name == "assert3(uint256)":
+        t.jumpi(S.Not(x == bv(23)), taken=False)                # to the INVALID
+    elif name == "requireisfine(uint256)":
+        t.require(S.Not(x == bv(23)))
+    elif name == "divisionby0(uint256)":
+        t.jumpi(t.iszero(x), taken=True)
+    elif name == "thisisfine(uint256)":
+        t.jumpi(S.UGT(x, bv(0)), taken=True)
+        t.jumpi(t.iszero(x), taken=rng.randrange(2) == 0)
+        t.sstore(bv(9), S.UDiv(bv(1), x))
+    elif name == "arrayaccess(uint256)":
+        t.jumpi(S.ULT(x, bv(8)), taken=False)                   # bounds check fails
+    else:
+        t.jumpi(S.ULT(x, bv(8)), taken=True)
+        t.jumpi(S.ULT(x, bv(8)), taken=rng.randrange(2) == 0)
+    out.append(w.query())
+
+
+def _hashforether_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``hashforether.sol``: ``require(uint32(msg.sender) == 0)`` then the
+    whole balance to the sender (ether thief)."""
+    funcs = sorted(selector(x) for x in ("withdrawWinnings()", "_sendWinnings()"))
+    w = World(concrete_storage=True)
+    w.tx(creation=True)
+    for _ in range(1 + rng.randrange(2)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        name = rng.choice(["withdrawWinnings()", "_sendWinnings()"])
+        t.dispatch(funcs, funcs.index(selector(name)))
+        t.nonpayable()
+        if name == "withdrawWinnings()":
+            t.require(S.Extract(31, 0, t.caller) == bv(0, 32))
+        amount = w.balance[bv(CONTRACT)]
+        _call(t, t.sender(), checks, 0x7A, checked=True, value=amount)
+        _ether_thief(t, checks, amount)
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+def _origin_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``origin.sol``: ``require(tx.origin != owner)`` (origin = the sender,
+    ``symbolic.py:98``), then ``if (newOwner != 0) owner = newOwner``."""
+    funcs = sorted(selector(x) for x in ("transferOwnership(address)", "owner()"))
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    c.sstore(bv(0), c.sender())
+    for _ in range(1 + rng.randrange(3)):
+        t = w.tx()
+        t.dispatch(funcs, funcs.index(selector("transferOwnership(address)")))
+        t.nonpayable()
+        owner = bv(ADDR_MASK) & t.sload(bv(0))
+        t.require(S.Not(t.sender() == owner))
+        out.append(w.query())
+        new = t.arg_address(0)
+        t.jumpi(S.Not(new == bv(0)), taken=rng.randrange(3) != 0)
+        t.sstore(bv(0), new)
+        out.append(w.query())
+
+
+def _returnvalue_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``returnvalue.sol``: the unchecked and the checked call."""
+    funcs = sorted(selector(x) for x in ("callnotchecked()", "callchecked()", "callee()"))
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    c.sstore(bv(0), bv(0xE0F7E56E62B4267062172495D7506087205A4229))
+    for _ in range(1 + rng.randrange(2)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        name = rng.choice(["callnotchecked()", "callchecked()"])
+        t.dispatch(funcs, funcs.index(selector(name)))
+        t.nonpayable()
+        _call(t, bv(ADDR_MASK) & t.sload(bv(0)), checks, 0x60 + len(name),
+              checked=name == "callchecked()")
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+RUBIXI_FUNCS = sorted(selector(x) for x in (
+    "dynamicPyramid()", "collectAllFees()", "collectFeesInEther(uint256)",
+    "collectPercentOfFees(uint256)", "changeOwner(address)", "changeMultiplier(uint256)",
+    "changeFeePercentage(uint256)", "currentMultiplier()", "totalParticipants()"))
+_R_BAL, _R_FEES, _R_FEEPCT, _R_MULT, _R_ORDER, _R_CREATOR, _R_PARTS = 0, 1, 2, 3, 4, 5, 6
+
+
+def _rubixi_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``rubixi.sol``: the fallback's fee / payout arithmetic (MUL / DIV by
+    100, ``+=`` checked by the integer module), the misnamed
+    ``dynamicPyramid`` constructor and the ``onlyowner`` fee withdrawals."""
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    c.sstore(bv(_R_FEEPCT), bv(10))
+    c.sstore(bv(_R_MULT), bv(300))
+    for _ in range(1 + rng.randrange(3)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        kind = rng.randrange(4)
+        if kind == 0:                                           # fallback -> init()
+            t.jumpi(S.ULT(t.calldata.size, bv(4)), taken=True)
+            v = t.callvalue
+            small = rng.randrange(2) == 0
+            t.jumpi(S.ULT(v, bv(10 ** 18)), taken=small)
+            fees = t.sload(bv(_R_FEES))
+            if small:
+                checks.append(S.Not(S.BVAddNoOverflow(fees, v, False)))
+                t.sstore(bv(_R_FEES), fees + v)
+            else:
+                fee = t.sload(bv(_R_FEEPCT))
+                big = rng.randrange(2) == 0
+                t.jumpi(S.Not(S.ULT(v, bv(50 * 10 ** 18))), taken=big)
+                if big:
+                    fee = S.UDiv(fee, bv(2))
+                mult = t.sload(bv(_R_MULT))
+                checks.append(S.Not(S.BVMulNoOverflow(v, mult, False)))
+                payout = S.UDiv(v * mult, bv(100))
+                n_parts = t.sload(bv(_R_PARTS))
+                checks.append(S.Not(S.BVAddNoOverflow(n_parts, bv(1), False)))
+                t.sstore(bv(_R_PARTS), n_parts + bv(1))
+                base = t.sha3(bv(_R_PARTS))
+                t.sstore(base + bv(2) * n_parts + bv(1), payout)
+                t.jumpi(n_parts + bv(1) == bv(10), taken=False)
+                share = S.UDiv(v * (bv(100) - fee), bv(100))
+                bal = t.sload(bv(_R_BAL))
+                checks.append(S.Not(S.BVAddNoOverflow(bal, share, False)))
+                t.sstore(bv(_R_BAL), bal + share)
+                checks.append(S.Not(S.BVAddNoOverflow(fees, S.UDiv(v * fee, bv(100)), False)))
+                first = t.sload(base + bv(2) * t.sload(bv(_R_ORDER)) + bv(1))
+                t.jumpi(S.UGT(bal + share, first), taken=rng.randrange(2) == 0)
+        elif kind == 1:
+            t.dispatch(RUBIXI_FUNCS, RUBIXI_FUNCS.index(selector("dynamicPyramid()")))
+            t.nonpayable()
+            t.sstore(bv(_R_CREATOR), t.sender())
+        else:
+            name = "collectFeesInEther(uint256)" if kind == 2 else "collectPercentOfFees(uint256)"
+            t.dispatch(RUBIXI_FUNCS, RUBIXI_FUNCS.index(selector(name)))
+            t.nonpayable()
+            t.jumpi(t.sender() == bv(ADDR_MASK) & t.sload(bv(_R_CREATOR)), taken=True)
+            fees = t.sload(bv(_R_FEES))
+            arg = t.arg(0)
+            if kind == 2:
+                checks.append(S.Not(S.BVMulNoOverflow(arg, bv(10 ** 18), False)))
+                amt = arg * bv(10 ** 18)
+                t.jumpi(S.UGT(amt, fees), taken=False)
+            else:
+                t.require(S.And(S.UGT(fees, bv(0)), S.ULE(arg, bv(100))))
+                amt = S.UDiv(fees, bv(100)) * arg
+            t.require(S.UGT(fees, bv(0)))
+            _call(t, bv(ADDR_MASK) & t.sload(bv(_R_CREATOR)), checks, 0x2C0 + kind, checked=True,
+                  value=amt)
+            _ether_thief(t, checks, amt)
+            checks.append(S.Not(S.BVSubNoUnderflow(fees, amt, False)))
+            t.sstore(bv(_R_FEES), fees - amt)
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+def _timelock_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``timelock.sol``: deposit (``now + 1 weeks``), increaseLockTime (the
+    overflow the integer module finds), withdraw (``now > lockTime``: the
+    predictable-variable module's ``timestamp`` dependence)."""
+    funcs = sorted(selector(x) for x in ("deposit()", "increaseLockTime(uint256)", "withdraw()",
+                                         "balances(address)", "lockTime(address)"))
+    w = World(concrete_storage=True)
+    w.tx(creation=True)
+    for _ in range(1 + rng.randrange(3)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        kind = rng.randrange(3)
+        now = _env(t, "timestamp")
+        slot_b, slot_l = t.mapping(t.sender(), 0), t.mapping(t.sender(), 1)
+        if kind == 0:
+            t.dispatch(funcs, funcs.index(selector("deposit()")))
+            b = t.sload(slot_b)
+            checks.append(S.Not(S.BVAddNoOverflow(b, t.callvalue, False)))
+            t.sstore(slot_b, b + t.callvalue)
+            checks.append(S.Not(S.BVAddNoOverflow(now, bv(604800), False)))
+            t.sstore(slot_l, now + bv(604800))
+        elif kind == 1:
+            t.dispatch(funcs, funcs.index(selector("increaseLockTime(uint256)")))
+            t.nonpayable()
+            cur = t.sload(slot_l)
+            checks.append(S.Not(S.BVAddNoOverflow(cur, t.arg(0), False)))
+            t.sstore(slot_l, cur + t.arg(0))
+        else:
+            t.dispatch(funcs, funcs.index(selector("withdraw()")))
+            t.nonpayable()
+            t.require(S.UGT(t.sload(slot_b), bv(0)))
+            t.require(S.UGT(now, t.sload(slot_l)))
+            checks.append(S.ULT(t.sload(slot_l), now))          # predictable-variable check
+            t.sstore(slot_b, bv(0))
+            _call(t, t.sender(), checks, 0x1B0, checked=True, value=t.sload(slot_b))
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+def _weakrandom_session(rng: random.Random, out: List[List[N.Node]]) -> None:
+    """``weak_random.sol``: the payable fallback's ticket loop (``moneySent
+    >= pricePerTicket && nextTicket < totalTickets``), and chooseWinner's
+    ``coinbase % 50`` / ``sender % 50`` / ``difficulty`` hash."""
+    w = World(concrete_storage=True)
+    c = w.tx(creation=True)
+    prize = 25 * 10 ** 17
+    c.sstore(bv(0), bv(prize))
+    c.sstore(bv(1), bv(50))
+    c.sstore(bv(2), bv(prize // 50))
+    c.sstore(bv(3), bv(1))
+    for _ in range(1 + rng.randrange(2)):
+        t = w.tx()
+        checks: List[S.Bool] = []
+        t.jumpi(S.ULT(t.calldata.size, bv(4)), taken=True)
+        money = t.callvalue
+        for k in range(1 + rng.randrange(3)):
+            price, nxt = t.sload(bv(2)), t.sload(bv(4))
+            t.jumpi(S.And(S.UGE(money, price), S.ULT(nxt, t.sload(bv(1)))), taken=True)
+            checks.append(S.Not(S.BVAddNoOverflow(nxt, bv(1), False)))
+            t.sstore(bv(4), nxt + bv(1))
+            slot = t.sha3(S.Concat(nxt, bv(5)))
+            t.sstore(slot, t.sender())
+            t.sstore(slot + bv(1), t.sload(bv(3)))
+            checks.append(S.Not(S.BVSubNoUnderflow(money, price, False)))
+            money = money - price
+        t.jumpi(S.And(S.UGE(money, t.sload(bv(2))), S.ULT(t.sload(bv(4)), t.sload(bv(1)))),
+                taken=False)
+        if rng.randrange(2):
+            t.jumpi(t.sload(bv(4)) == t.sload(bv(1)), taken=True)
+            cb = bv(ADDR_MASK) & _env(t, "coinbase")
+            s1 = t.sload(t.sha3(S.Concat(S.URem(cb, t.sload(bv(1))), bv(5))))
+            s2 = t.sload(t.sha3(S.Concat(S.URem(t.sender(), t.sload(bv(1))), bv(5))))
+            h = t.sha3(S.Concat(bv(ADDR_MASK) & s1, bv(ADDR_MASK) & s2,
+                                _env(t, "block_difficulty")))
+            checks.append(S.ULT(S.URem(h, t.sload(bv(1))), bv(50)))
+            t.sstore(bv(3), t.sload(bv(3)) + bv(1))
+            t.sstore(bv(4), bv(0))
+        t.jumpi(S.UGT(money, bv(0)), taken=rng.randrange(2) == 0)
+        out.append(w.query())
+        for chk in checks:
+            out.append(w.query([chk]))
+
+
+C5_EXTRA = {"calls": _calls_session, "etherstore": _etherstore_session,
+            "exceptions": _exceptions_session, "hashforether": _hashforether_session,
+            "origin": _origin_session, "returnvalue": _returnvalue_session,
+            "rubixi": _rubixi_session, "timelock": _timelock_session,
+            "weak_random": _weakrandom_session}
+
+
+def contract_queries(name: str, n: int, seed: int) -> List[List[N.Node]]:
+    """``n`` queries of one of the nine C5-only contracts (C5_EXTRA)."""
+    rng = random.Random(seed)
+    out: List[List[N.Node]] = []
+    while len(out) < n:
+        C5_EXTRA[name](rng, out)
+    return out[:n]
+
+
+# the thirteen solidity_examples contracts and their streams (C1 / C3 / C4
+# for the four contracts those configs analyse)
+C5_CONTRACTS = ("suicide", "BECToken", "token+WalletLibrary") + tuple(C5_EXTRA)
+
+
+def c5_queries(n: int = 1024, seed: int = 0xC5) -> List[List[N.Node]]:
+    """BASELINE config C5: every solidity_examples contract's query stream,
+    batched — the C1 (suicide), C3 (BECToken) and C4 (token + WalletLibrary)
+    stand-ins and the nine C5_EXTRA contracts, interleaved round-robin (one
+    query per contract in turn) so any prefix mixes all thirteen."""
+    per = -(-n // len(C5_CONTRACTS))
+    streams = [c1_queries(per, seed ^ 0xC1), c3_queries(per, seed ^ 0xC3),
+               c4_queries(per, seed ^ 0xC4)]
+    streams += [contract_queries(name, per, seed ^ (0x100 + k))
+                for k, name in enumerate(C5_EXTRA)]
+    out: List[List[N.Node]] = []
+    for i in range(per):
+        for st in streams:
+            if i < len(st):
+                out.append(st[i])
+    return out[:n]
+
+
+WORKLOADS = {"c1": c1_queries, "c3": c3_queries, "c4": c4_queries, "c5": c5_queries}
 
 
 def queries(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> List[List[N.Node]]:

@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or 8
 N_LANES, FIRST = 1 << 12, (3 << 20) + 192
 SEED = bench.SEED
-FULL = {"c2": 4096, "c3": bench.STREAM_QUERIES, "c4": bench.STREAM_QUERIES}
+FULL = {w: bench.default_units(w) for w in ("c2", "c3", "c4", "c5")}
 # (family, variant) handlers of the programs verified lane by lane below
 CHECKED = set()
 
@@ -96,7 +96,7 @@ def images(units):
 
 
 @pytest.mark.parametrize("path", ["interp", "jit"])
-@pytest.mark.parametrize("workload", ["c2", "c3", "c4"])
+@pytest.mark.parametrize("workload", ["c2", "c3", "c4", "c5"])
 def test_every_bench_unit_every_lane(engine, units, images, workload, path):
     us = units[workload]
     assert len(us) == FULL[workload]
@@ -120,7 +120,7 @@ def test_every_bench_unit_every_lane(engine, units, images, workload, path):
 
 def test_bench_handler_variants_all_checked(units):
     """Every (family, variant) executed by a bench configuration (what
-    bench.py compiles for C2, C3 and C4) belongs to a program the test above
+    bench.py compiles for C2, C3, C4 and C5) belongs to a program the test above
     verified lane by lane; the count is reported so a new variant shows up
     in the log."""
     assert CHECKED, "run with test_every_bench_unit_every_lane (same module)"

@@ -28,7 +28,7 @@ THREADS = int(os.environ.get("OMP_NUM_THREADS", "0")) or 8
 
 
 # C1 (suicide.sol -t 2) has only ~20 distinct paths; C3 / C4 have hundreds
-DISTINCT = {"c1": 16, "c3": 32, "c4": 32}
+DISTINCT = {"c1": 16, "c3": 32, "c4": 32, "c5": 48}
 
 
 def distinct_queries(name, k=None):
@@ -51,7 +51,7 @@ def _table(prog):
 
 
 @pytest.mark.parametrize("const_keys", [False, True], ids=["leafkeyed", "constkeyed"])
-@pytest.mark.parametrize("name", ["c1", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c1", "c3", "c4", "c5"])
 def test_workload_every_lane_every_constraint(engine, name, const_keys):
     n, seed, first = 4096, 0x5EED, 3 << 20
     checked = 0
@@ -81,7 +81,7 @@ def test_workload_every_lane_every_constraint(engine, name, const_keys):
     assert checked == DISTINCT[name]
 
 
-@pytest.mark.parametrize("name", ["c3", "c4"])
+@pytest.mark.parametrize("name", ["c3", "c4", "c5"])
 def test_workload_batch_entry_point(engine, name):
     """``mg_batch_eval_gen`` (the path ``bench.py --workload`` times) over 32
     queries against ``evalref.run_gen`` (same generator, same pools)."""
@@ -118,7 +118,7 @@ def test_workload_batch_entry_point(engine, name):
         assert firsts[k] == (first + int(hit[0]) if hit.size else shard.NONE), (name, k)
 
 
-@pytest.mark.parametrize("name", ["c1", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c1", "c3", "c4", "c5"])
 def test_workload_search_is_sound(engine, name):
     """Batched witness search over the shape's queries (the drop-in path of
     ``batch_is_possible``): every witness satisfies the query in the oracle."""

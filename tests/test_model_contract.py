@@ -124,7 +124,7 @@ class FakeEngine:
 @pytest.fixture
 def batch_env(monkeypatch, fresh):
     eng = FakeEngine()
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: eng)
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: eng)
     z3_calls = []
 
     def fake_z3(constraints, minimize, maximize, timeout):
@@ -222,7 +222,7 @@ def test_bucketed_witness_joins_group_assignments(monkeypatch, fresh):
             for k, v in enumerate(probes):
                 pr[k] = [(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)]
             return leaves, pr
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: Eng())
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: Eng())
     a, progs = REAL_GPU_SEARCH(nodes, 200)
     assert Eng.calls == 1 and len(progs) == 2
     assert a.vars == {"x": 9, "y": 4}
@@ -430,7 +430,7 @@ def test_batch_search_spreads_programs_over_devices(monkeypatch):
             return [(self.dev * 1000 + p.n_ins, np.zeros((len(p.leaves), 8), np.uint32))
                     for p in loaded]
     engines = {d: DevEngine(d) for d in (0, 1, 2)}
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: engines[dev])
     monkeypatch.setattr(M, "DEVICES", [0, 1, 2])
     x = N.bv_var("x", 256)
     progs = [compile_constraints([N.bv_cmp("bvult", N.bv_op("bvmul", *([x] * (k + 2))), x)])
@@ -491,7 +491,7 @@ def test_assignment_axis_equals_single_device_sweep(monkeypatch, sat, G):
     want = one.search(prog, 0, n)[0]
     log.clear()
     engines = {d: StreamEngine(d, sat, log) for d in range(G)}
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: engines[dev])
     idx, _ = M.search_assignment_axis(prog, n, list(range(G)))
     assert idx == want
     ranges = sorted((f, f + k) for _, f, k in log)
@@ -503,7 +503,7 @@ def test_assignment_axis_equals_single_device_sweep(monkeypatch, sat, G):
 def test_single_group_query_uses_every_device(monkeypatch, fresh, reset_engine_memo):
     log = []
     engines = {d: StreamEngine(d, [3 << 20], log) for d in range(4)}
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: engines[dev])
     monkeypatch.setattr(M, "DEVICES", [0, 1, 2, 3])
     M.clear_search_memos()
     x = symbol_factory.BitVecSym("ax", 256)
@@ -516,7 +516,7 @@ def test_single_group_query_uses_every_device(monkeypatch, fresh, reset_engine_m
 def miss_engine(monkeypatch):
     log = []
     eng = StreamEngine(0, [], log)                       # never satisfied
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: eng)
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: eng)
     monkeypatch.setattr(M, "DEVICES", [0])
     M.clear_search_memos()
     yield log
@@ -626,7 +626,7 @@ def test_shape_gate_skips_a_shape_that_keeps_missing(miss_engine, fresh, reset_e
 def test_shape_gate_keeps_searching_a_shape_that_hits(monkeypatch, fresh, reset_engine_memo):
     log = []
     engines = {0: StreamEngine(0, [5], log)}          # every program satisfied at index 5
-    monkeypatch.setattr(M, "get_engine", lambda dev=0: engines[dev])
+    monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: engines[dev])
     monkeypatch.setattr(M, "DEVICES", [0])
     M.clear_search_memos()
     for k in range(3 * M.SHAPE_MIN):
@@ -656,3 +656,31 @@ def test_query_shape_abstracts_leaves_not_structure():
     assert M.query_shape(ULT(a * b, a).raw) != s1
     assert M.query_shape((c == symbol_factory.BitVecVal(1, 8)).raw) != \
         M.query_shape((a == symbol_factory.BitVecVal(1, 256)).raw)
+
+
+def test_repeated_devices_get_their_own_contexts(monkeypatch):
+    """DEVICES=[0, 0]: two host threads must not share one context (its
+    workspace and stream serve one thread); the k-th repeat of a device is
+    slot k (engine.device_slots), and batch_search_devices asks for each."""
+    from mythril_amd.engine import device_slots
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.smt import node as N
+    assert device_slots([0, 0, 1, 0]) == [(0, 0), (0, 1), (1, 0), (0, 2)]
+    asked = []
+
+    class Eng:
+        def load(self, prog, leafgen, prog_seed=0):
+            return prog
+
+        def batch_search(self, loaded, seed, n_cand, first_index=0):
+            return [(-1, None) for _ in loaded]
+
+    def ge(dev=0, slot=0):
+        asked.append((dev, slot))
+        return Eng()
+    monkeypatch.setattr(M, "get_engine", ge)
+    monkeypatch.setattr(M, "DEVICES", [0, 0])
+    x = N.bv_var("x", 256)
+    progs = [compile_constraints([N.bv_cmp("bvult", x, N.bv_num(k + 3, 256))]) for k in range(4)]
+    M.batch_search_devices(progs, 1 << 16)
+    assert sorted(set(asked)) == [(0, 0), (0, 1)]

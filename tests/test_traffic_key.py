@@ -19,10 +19,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_traffic_json_keyed_to_this_tree():
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as fh:
         tj = json.load(fh)
+    entries = tj["entries"]
     corpus = bench.build_corpus(4096, min(8, os.cpu_count() or 1))
     key = bench.kernel_key(asmgen.digest(), "c2", 4096, 20, True, corpus)
-    diff = sorted(k for k in key if tj["kernel_key"].get(k) != key[k])
+    c2 = [e for e in entries if e["kernel_key"].get("workload") == "c2"]
+    assert c2, "profiles/traffic.json has no C2 entry"
+    diff = sorted(k for k in key if c2[0]["kernel_key"].get(k) != key[k])
     assert not diff, "profiles/traffic.json is for another kernel (%s differ): " \
         "re-run tools/profile.sh + tools/prof_summary.py" % ", ".join(diff)
-    # FETCH doubled (gfx950 correction) + WRITE, KiB -> bytes
-    assert tj["hbm_bytes_per_launch"] == (2 * tj["fetch_kib"] + tj["write_kib"]) * 1024
+    for e in entries:
+        # FETCH doubled (gfx950 correction) + WRITE, KiB -> bytes
+        assert e["hbm_bytes_per_launch"] == (2 * e["fetch_kib"] + e["write_kib"]) * 1024
+    # one entry per (workload, size, path)
+    slots = [(e["kernel_key"]["workload"], e["kernel_key"]["dags"], e["kernel_key"]["jit"])
+             for e in entries]
+    assert len(slots) == len(set(slots))

@@ -96,7 +96,7 @@ def test_c4_token_underflow_is_satisfied_by_planted_model():
     assert R.eval_constraints(q, off) == 0
 
 
-@pytest.mark.parametrize("name", ["c1", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c1", "c3", "c4", "c5"])
 def test_workload_shapes(name):
     qs = W.queries(name, 48)
     assert len(qs) == 48
@@ -110,6 +110,8 @@ def test_workload_shapes(name):
         assert {"bvumul_noovfl", "apply", "store", "K"} <= ops
     if name == "c4":
         assert {"apply", "store", "bvurem"} <= ops
+    if name == "c5":
+        assert {"apply", "store", "bvurem", "bvudiv", "bvumul_noovfl", "extract"} <= ops
     # deterministic
     assert [len(q) for q in W.queries(name, 48)] == [len(q) for q in qs]
 
@@ -124,7 +126,8 @@ def _to_oracle(prog, lv):
 
 
 @pytest.mark.parametrize("name,const_keys", [("c1", False), ("c1", True), ("c3", False),
-                                             ("c3", True), ("c4", False), ("c4", True)])
+                                             ("c3", True), ("c4", False), ("c4", True),
+                                             ("c5", False), ("c5", True)])
 def test_workload_programs_through_ir(name, const_keys):
     """Compiled IR (leaf-keyed or constant-keyed tables) executed by the
     reference executor equals direct oracle evaluation of the source DAG
@@ -190,7 +193,7 @@ def test_const_keys_skip_tables_read_at_many_symbolic_offsets():
     assert scan_const_keys(q, max_links=10 ** 6)["cd"] == list(range(40))
 
 
-@pytest.mark.parametrize("name", ["c1", "c3", "c4"])
+@pytest.mark.parametrize("name", ["c1", "c3", "c4", "c5"])
 def test_solve_mode_constructs_consistent_models(name):
     """Search-mode programs (argument-keyed tables + equality substitution)
     compute part of the model; under the model unpacked from leaves AND the
@@ -260,3 +263,22 @@ def test_reference_keccak_val8_sym256_case_is_satisfiable():
                        funcs={"keccak256_256": ([(100, h)], 0), "keccak256_256-1": ([(h, 100)], 0),
                               "keccak256_8": ([(100, h)], 0), "keccak256_8-1": ([(h, 100)], 0)})
     assert R.eval_constraints(q, asg) == 1
+
+
+def test_c5_interleaves_all_thirteen_contracts():
+    """C5 = every solidity_examples contract: twelve streams (token and
+    WalletLibrary share C4's), the first 12 queries are one from each stream
+    in C5_CONTRACTS order, and every one of the nine C5-only contracts builds
+    queries that compile."""
+    assert len(W.C5_CONTRACTS) == 12 and len(W.C5_EXTRA) == 9
+    per = 2
+    firsts = [W.c1_queries(per, 0xC5 ^ 0xC1)[0], W.c3_queries(per, 0xC5 ^ 0xC3)[0],
+              W.c4_queries(per, 0xC5 ^ 0xC4)[0]]
+    firsts += [W.contract_queries(n, per, 0xC5 ^ (0x100 + k))[0]
+               for k, n in enumerate(W.C5_EXTRA)]
+    got = W.c5_queries(12 * per)[:12]
+    assert [[c.id for c in q] for q in got] == [[c.id for c in q] for q in firsts]
+    for name in W.C5_EXTRA:
+        for q in W.contract_queries(name, 6, 3):
+            compile_constraints(q)
+            compile_constraints(q, const_keys=True, leaf_pools=True)

@@ -1,5 +1,11 @@
 #!/usr/bin/env python3
-"""Summarise gpurun_out/prof into profiles/<round>/ and profiles/traffic.json."""
+"""Summarise gpurun_out/prof[_<tag>] into profiles/<round>/[<tag>/] and
+profiles/traffic.json.
+
+usage: tools/prof_summary.py <round> [<tag>]   (tag: the workload profiled
+by ``PROF_TAG=<tag> tools/profile.sh --workload <tag>``; none = the default
+C2 bench).  traffic.json holds one entry per kernel_key: a new measurement
+replaces the entry of the same workload / size / code path."""
 import csv
 import glob
 import json
@@ -8,8 +14,9 @@ import shutil
 import sys
 
 ROUND = sys.argv[1] if len(sys.argv) > 1 else "r01"
-SRC = "gpurun_out/prof"
-DST = os.path.join("profiles", ROUND)
+TAG = sys.argv[2] if len(sys.argv) > 2 else ""
+SRC = "gpurun_out/prof" + ("_" + TAG if TAG else "")
+DST = os.path.join("profiles", ROUND, TAG) if TAG else os.path.join("profiles", ROUND)
 os.makedirs(DST, exist_ok=True)
 
 
@@ -61,11 +68,22 @@ if fetch_kb is not None and write_kb is not None:
     if keys[0] != keys[1] or keys[0] is None:
         sys.exit("FETCH and WRITE passes ran different kernels: %s" % keys)
     out = {"kernel_key": keys[0], "fetch_kib": fetch_kb, "write_kib": write_kb,
-           "hbm_bytes_per_launch": doubled, "hbm_bytes_raw": raw,
+           "hbm_bytes_per_launch": doubled, "hbm_bytes_raw": raw, "round": ROUND,
+           "evidence": DST,
            "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, per mg_interp "
-                   "dispatch of the default bench config; read side doubled per the gfx950 "
+                   "dispatch of this bench config; read side doubled per the gfx950 "
                    "FETCH_SIZE correction (upper bound)"}
-    json.dump(out, open("profiles/traffic.json", "w"), indent=1)
+    path = "profiles/traffic.json"
+    try:
+        tj = json.load(open(path))
+    except (OSError, ValueError):
+        tj = {}
+    entries = tj.get("entries", [tj] if "kernel_key" in tj else [])
+
+    def slot(k):
+        return (k.get("workload"), k.get("dags"), k.get("assign_log2"), k.get("jit"))
+    entries = [e for e in entries if slot(e["kernel_key"]) != slot(out["kernel_key"])] + [out]
+    json.dump({"entries": entries}, open(path, "w"), indent=1)
     print("traffic", out)
 sq = find("sq/**/*counter_collection.csv")
 if sq:
@@ -82,8 +100,8 @@ if sq:
     summ.update({"valu_per_wave": c.get("SQ_INSTS_VALU", 0) / w,
                  "salu_per_wave": c.get("SQ_INSTS_SALU", 0) / w,
                  "smem_per_wave": c.get("SQ_INSTS_SMEM", 0) / w,
-                 "note": "sums over the mg_interp dispatches of the --dags 512 pass; SQ cycle "
-                         "counters tick once per 4 shader cycles on CDNA"})
+                 "note": "sums over the mg_interp dispatches of the SQ pass (C2: --dags 512); "
+                         "SQ cycle counters tick once per 4 shader cycles on CDNA"})
     if c.get("SQ_WAVE_CYCLES"):
         summ["valu_active_frac_of_wave_time"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"]
         summ["salu_active_frac_of_wave_time"] = c.get("SQ_ACTIVE_INST_SALU", 0) / c["SQ_WAVE_CYCLES"]

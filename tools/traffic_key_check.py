@@ -16,5 +16,6 @@ from mythril_amd.engine import load_library  # noqa: E402
 corpus = bench.build_corpus(4096, min(8, os.cpu_count() or 1))
 key = bench.kernel_key(load_library().mg_asm_digest().decode(), "c2", 4096, 20, True, corpus)
 tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
-print(json.dumps({"tree": key, "traffic_json": tj["kernel_key"], "match": tj["kernel_key"] == key}))
-sys.exit(0 if tj["kernel_key"] == key else 1)
+keys = [e["kernel_key"] for e in tj.get("entries", [])]
+print(json.dumps({"tree": key, "traffic_json": keys, "match": key in keys}))
+sys.exit(0 if key in keys else 1)
