@@ -82,7 +82,20 @@ enum mg_op {
     MG_OUT = 31,     /* probe[imm0] = R[a]                                    */
     MG_ROOT = 32,    /* root &= R[a] & 1                                      */
     MG_MOV = 33,     /* dst = R[a]                                            */
-    MG_NUM_OPS = 34
+    /* The calldata word LASER builds for CALLDATALOAD (reference
+     * mythril/laser/ethereum/state/calldata.py:47-54,219-232):
+     *   Concat_{i<32} If(off + i <s size, select(cd, off + i), 0)
+     * over a free array read through its model table (entries (k_e, v_e) in
+     * first-match order, then `else`), evaluated as one short chain instead
+     * of 32 byte lookups (ir.py _calldata_word):
+     *   w = BCAST(else); for e = E-1 .. 0: w = CDWE(w, k_e - off, v_e);
+     *   word = CDWX(w, off, size)                                           */
+    MG_BCAST = 34,   /* dst = byte 0 of R[a] in all 32 bytes (width 256)      */
+    MG_CDWE = 35,    /* dst = R[a] with byte 31-d := R[c] & 0xff where        */
+                     /*   d = R[b] < 32 (else R[a]); width 256                */
+    MG_CDWX = 36,    /* dst = R[a] with byte 31-i := 0 for every i < 32 where */
+                     /*   !(R[b] + i <s R[c]) (256-bit wrapping add); width 256 */
+    MG_NUM_OPS = 37
 };
 
 #define MG_ROOT_FLAG (1u << 18)

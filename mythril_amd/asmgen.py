@@ -80,7 +80,10 @@ AOPS = ["NOP", "HALT", "CONST", "LEAF", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS", 
         "RELOADD",  # scratch reload straight into slot = variant, loads left in flight
         "EQSEL",    # fused EQ + ITE of a store-chain link (translator): see h_eqsel
         "EXTRACTN",  # EXTRACT to W > 32 bits: variant = result limbs - 1
-        "CONCATQ"]  # CONCAT: variant = limb shift q | 8 if a bit shift remains
+        "CONCATQ",  # CONCAT: variant = limb shift q | 8 if a bit shift remains
+        "BCAST",    # the calldata word (mythgpu_ir.h MG_BCAST / MG_CDWE / MG_CDWX)
+        "CDWE",
+        "CDWX"]
 AOP = {n: i for i, n in enumerate(AOPS)}
 V_ROOT, V_MASK, V_DC, V_W32, V_IP = 1, 2, 4, 8, 16
 # NW = a ROOT-fused result nobody reads: only the root is updated, the slot
@@ -102,6 +105,8 @@ SUPPORT.update({n: SUPPORT[n] | V_IP for n in ("ADD", "SUB", "AND", "OR", "XOR",
 for _n in ("EQ", "ULT", "ULE", "SLT", "SLE", "AND", "OR", "XOR"):
     SUPPORT[_n] |= V_NW
 SUPPORT["SUBR"] = _RM | V_IP
+SUPPORT["BCAST"] = 0
+SUPPORT["CDWE"] = SUPPORT["CDWX"] = V_IP        # 256-bit results, never ROOT
 SUPPORT["ITEN"] = V_ROOT | V_IP
 SUPPORT["WAITVM"] = 0
 V_NEG, V_GEN = 1, 2          # EQSEL: copy where not equal / three-address form
@@ -1330,6 +1335,176 @@ def h_eqsel(a: Asm, bank: int, var: int):
     dispatch(a, 1 - bank)
 
 
+# ---- the calldata word (ir.py _calldata_word) ---------------------------------
+
+def h_bcast(a, bank, root, mask, dc=False, w32=False, ip=False):
+    """F[D] = byte 0 of F[A] in all 32 bytes (the table's else byte, an
+    8-bit value): one multiply by 0x01010101, four pair moves."""
+    prologue(a, bank)
+    a("s_mov_b32 %s, 0x1010101" % s(S_T))
+    a.idx_on(fld(bank, F_A), "SRC0")
+    a("v_mul_lo_u32 %s, %s, %s" % (v(R[0]), v(F[0]), s(S_T)))
+    a.idx_off()
+    a("v_mov_b32 %s, %s" % (v(R[1]), v(R[0])))
+    a.idx_on(fld(bank, F_D), "DST")
+    for j in range(0, 8, 2):
+        a("v_mov_b64 %s, %s" % (vp(F[j]), vp(R[0])))
+    a.idx_off()
+    dispatch(a, 1 - bank)
+
+
+def h_cdwe(a, bank, root, mask, dc=False, w32=False, ip=False):
+    """One table entry of a calldata word: F[D] = F[A] with byte 31 - d set to
+    F[C] & 0xff in the lanes where d = F[B] (= key - off) is below 32.  A
+    wave with no such lane only copies (in place: nothing at all).  The
+    byte's limb q = (31 - d) >> 2 is selected per limb by a compare (X[j]:
+    the byte mask where q == j, else 0), then one v_bfi per limb."""
+    prologue(a, bank)
+    a.idx_on(fld(bank, F_B), "SRC0,SRC1,SRC2")
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(F[1]), v(F[2]), v(F[3])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[2]), v(F[4]), v(F[5]), v(F[6])))
+    a("s_set_gpr_idx_mode gpr_idx(SRC0)")
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(F[7]), v(T[1]), v(T[2])))
+    a("v_mov_b32 %s, %s" % (v(T[0]), v(F[0])))
+    a.idx_off()
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(S_T), v(T[1])))
+    a("v_cmp_gt_u32 vcc, 32, %s" % v(T[0]))
+    a("s_and_b64 vcc, vcc, %s" % sp(S_T))            # lanes whose key is a byte of the word
+    if not ip:
+        a.read_slot(R, fld(bank, F_A))
+    done = a.uniq("cdwe")
+    a("s_cbranch_vccz %s" % done)
+    a("v_sub_u32 %s, 31, %s" % (v(T[2]), v(T[0])))               # byte position p
+    a("v_lshrrev_b32 %s, 2, %s" % (v(T[3]), v(T[2])))            # its limb
+    a("v_lshlrev_b32 %s, 3, %s" % (v(T[4]), v(T[2])))
+    a("v_and_b32 %s, 24, %s" % (v(T[4]), v(T[4])))               # its shift in the limb
+    a.idx_on(fld(bank, F_C), "SRC1")
+    a("v_lshlrev_b32 %s, %s, %s" % (v(T[5]), v(T[4]), v(F[0])))  # value byte in place
+    a.idx_off()
+    a("v_mov_b32 %s, 0xff" % v(T[6]))
+    a("v_lshlrev_b32 %s, %s, %s" % (v(T[6]), v(T[4]), v(T[6])))  # byte mask
+    a("v_cndmask_b32_e64 %s, 0, %s, vcc" % (v(T[6]), v(T[6])))    # no hit: no byte
+    for j in range(8):
+        a("v_cmp_eq_u32_e64 %s, %d, %s" % (sp(S_T), j, v(T[3])))
+        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(X[j]), v(T[6]), sp(S_T)))
+    if ip:
+        a.idx_on(fld(bank, F_D), "SRC2,DST")
+        for j in range(8):
+            a("v_bfi_b32 %s, %s, %s, %s" % (v(F[j]), v(X[j]), v(T[5]), v(F[j])))
+        a.idx_off()
+    else:
+        for j in range(8):
+            a("v_bfi_b32 %s, %s, %s, %s" % (v(R[j]), v(X[j]), v(T[5]), v(R[j])))
+    a.label(done)
+    if not ip:
+        a.write_slot(R, fld(bank, F_D))
+    dispatch(a, 1 - bank)
+
+
+def _prefix(a: Asm, out: int, n: int, pair: int):
+    """v[out] = the low n bits set, n in 0..32 (32: all ones): the low half
+    of (1 << n) - 1 from a 64-bit shift (a 32-bit shift by 32 is a shift by
+    0); v[pair:pair+1] is scratch (even-aligned)."""
+    a("v_lshlrev_b64 %s, %s, 1" % (vp(pair), v(n)))
+    a("v_add_u32 %s, -1, %s" % (v(out), v(pair)))
+
+
+def h_cdwx(a, bank, root, mask, dc=False, w32=False, ip=False):
+    """The calldata word's size test: F[D] = F[A] with byte 31 - i cleared for
+    every i < 32 where not (F[B] + i <s F[C]) (off, size; the add wraps at
+    2^256).  With u = off ^ 2^255 and s' = size ^ 2^255 the test is the
+    unsigned u + i < s'.  Without wrap (u <= 2^256 - 32) the valid bytes are
+    the first n = (s' < u) ? 0 : min(s' - u, 32); lanes whose u + i wraps
+    (off's top limb 0x7fffffff, then the exact test out of line) add the
+    interval [K, min(32, K + s')) past the wrap point K = 2^256 - u.  The
+    32-bit byte set is bit-reversed so nibble j covers limb j, and each
+    nibble is spread to a byte mask (a 24-bit multiply puts bit k at bit
+    8k, then t * 255)."""
+    prologue(a, bank)
+    a.read_slot(Y, fld(bank, F_B))                                 # off
+    a.idx_on(fld(bank, F_C), "SRC0")                              # size - off, signed borrow
+    a("v_sub_co_u32 %s, vcc, %s, %s" % (v(T[0]), v(F[0]), v(Y[0])))
+    for j in range(1, 7):
+        a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(T[j]), v(F[j]), v(Y[j])))
+    a("s_set_gpr_idx_mode gpr_idx(SRC1)")
+    a("v_xor_b32 %s, 0x80000000, %s" % (v(T[7]), v(F[7])))
+    a.idx_off()
+    a("v_xor_b32 %s, 0x80000000, %s" % (v(T[8]), v(Y[7])))
+    a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(T[7]), v(T[7]), v(T[8])))
+    a("s_mov_b64 %s, vcc" % sp(S_X))                             # size <s off
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(T[1]), v(T[2]), v(T[3])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(T[1]), v(T[4]), v(T[5])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(T[1]), v(T[6]), v(T[7])))
+    a("v_min_u32 %s, 32, %s" % (v(T[0]), v(T[0])))
+    a("v_cmp_ne_u32 vcc, 0, %s" % v(T[1]))
+    a("v_cndmask_b32_e64 %s, %s, 32, vcc" % (v(T[0]), v(T[0])))
+    a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(T[0]), v(T[0]), sp(S_X)))   # n
+    wrap, back, done = a.uniq("cdxw"), a.uniq("cdxb"), a.uniq("cdxd")
+    a("v_cmp_eq_u32 vcc, 0x7fffffff, %s" % v(Y[7]))
+    a("s_cbranch_vccnz %s" % wrap)
+    _prefix(a, T[2], T[0], T[2])                                   # valid bytes
+    a.label(back)
+    a("v_cmp_ne_u32 vcc, -1, %s" % v(T[2]))
+    if not ip:
+        a.read_slot(R, fld(bank, F_A))
+    a("s_cbranch_vccz %s" % done)                                  # every byte valid
+    a("v_bfrev_b32 %s, %s" % (v(T[2]), v(T[2])))                   # bit 4j + k: limb j, byte k
+    a("s_mov_b32 %s, 0x1010101" % s(S_T))
+    for j in range(8):
+        a("v_bfe_u32 %s, %s, %d, 4" % (v(T[3]), v(T[2]), 4 * j))
+        a("v_mul_u32_u24 %s, 0x204081, %s" % (v(T[3]), v(T[3])))    # bit k -> bit 8k
+        a("v_and_b32 %s, %s, %s" % (v(T[3]), s(S_T), v(T[3])))
+        # x 255 (a 24-bit multiply would drop byte 3's bit): (t << 8) - t
+        a("v_lshlrev_b32 %s, 8, %s" % (v(X[j]), v(T[3])))
+        a("v_sub_u32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[3])))
+    if ip:
+        a.idx_on(fld(bank, F_D), "SRC1,DST")
+        for j in range(8):
+            a("v_and_b32 %s, %s, %s" % (v(F[j]), v(X[j]), v(F[j])))
+        a.idx_off()
+    else:
+        for j in range(8):
+            a("v_and_b32 %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j])))
+    a.label(done)
+    if not ip:
+        a.write_slot(R, fld(bank, F_D))
+    dispatch(a, 1 - bank)
+    a.cold()
+    # some lane's off has the top limb 0x7fffffff: u + i may wrap at 2^256
+    a.label(wrap)
+    a("v_and_b32 %s, %s, %s" % (v(T[3]), v(Y[1]), v(Y[2])))
+    for j in range(3, 7):
+        a("v_and_b32 %s, %s, %s" % (v(T[3]), v(T[3]), v(Y[j])))
+    a("v_cmp_eq_u32_e64 %s, -1, %s" % (sp(S_T), v(T[3])))
+    a("s_and_b64 %s, %s, vcc" % (sp(S_T), sp(S_T)))                # u's upper limbs all ones
+    a("v_sub_u32 %s, 0, %s" % (v(T[4]), v(Y[0])))                 # K = 2^32 - u_lo
+    a("v_add_u32 %s, -1, %s" % (v(T[5]), v(T[4])))
+    a("v_cmp_gt_u32 vcc, 31, %s" % v(T[5]))                        # K in 1..31
+    a("s_and_b64 %s, %s, vcc" % (sp(S_T), sp(S_T)))
+    a("v_cndmask_b32_e64 %s, 32, %s, %s" % (v(T[4]), v(T[4]), sp(S_T)))   # K (32: no wrap)
+    a.idx_on(fld(bank, F_C), "SRC0,SRC1,SRC2")                    # min(s', 32)
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[5]), v(F[1]), v(F[2]), v(F[3])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[6]), v(F[4]), v(F[5]), v(F[6])))
+    a("s_set_gpr_idx_mode gpr_idx(SRC1)")
+    a("v_xor_b32 %s, 0x80000000, %s" % (v(T[7]), v(F[7])))
+    a("v_min_u32 %s, 32, %s" % (v(T[8]), v(F[0])))
+    a.idx_off()
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[5]), v(T[5]), v(T[6]), v(T[7])))
+    a("v_cmp_ne_u32 vcc, 0, %s" % v(T[5]))
+    a("v_cndmask_b32_e64 %s, %s, 32, vcc" % (v(T[8]), v(T[8])))
+    a("v_add_u32 %s, %s, %s" % (v(T[8]), v(T[4]), v(T[8])))
+    a("v_min_u32 %s, 32, %s" % (v(T[8]), v(T[8])))                # end of the wrapped run
+    a("v_min_u32 %s, %s, %s" % (v(T[0]), v(T[4]), v(T[0])))       # min(K, n)
+    _prefix(a, T[2], T[0], T[2])
+    _prefix(a, T[6], T[8], T[6])
+    _prefix(a, T[8], T[4], T[8])
+    a("v_bfi_b32 %s, %s, 0, %s" % (v(T[6]), v(T[8]), v(T[6])))    # [K, end)
+    a("v_or_b32 %s, %s, %s" % (v(T[2]), v(T[2]), v(T[6])))
+    a("s_branch %s" % back)
+    a.hot()
+    a.flush_cold()
+
+
 def h_waitvm(a, bank, root, mask, dc=False, w32=False, ip=False):
     prologue(a, bank)
     a("s_waitcnt vmcnt(0)")
@@ -2032,7 +2207,7 @@ CHEAP = {
     "XOR": h_xor, "NOT": h_not, "EQ": h_eq, "ULT": h_ult, "ULE": h_ule, "SLT": h_slt,
     "SLE": h_sle, "ITE": h_ite, "CONCAT": h_concat, "EXTRACT": h_extract, "SEXT": h_sext,
     "NEG": h_neg, "OUT": h_out, "ROOT": h_root, "MOV": h_mov, "SUBR": h_subr, "ITEN": h_iten,
-    "WAITVM": h_waitvm, "MUL": h_mul,
+    "WAITVM": h_waitvm, "MUL": h_mul, "BCAST": h_bcast, "CDWE": h_cdwe, "CDWX": h_cdwx,
     "SHL": h_shift("SHL"), "LSHR": h_shift("LSHR"), "ASHR": h_shift("ASHR"),
 }
 SLOT_HANDLERS = {"SPILL_LDS": h_spill_lds, "SPILL_SCR": h_spill_scr, "RELOAD_LDS": h_reload_lds}

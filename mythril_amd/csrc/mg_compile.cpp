@@ -688,6 +688,8 @@ struct Lowerer {
             return {mk(MG_ITE, w, {c, a, b})};
         }
         if (op == S_CONCAT) {
+            int word = calldata_word(n);
+            if (word >= 0) return {word};
             std::vector<std::pair<Chunks, int>> pieces;
             for (int a : s.args) pieces.push_back({M(a), S[a].width});
             return assemble(pieces);
@@ -810,6 +812,66 @@ struct Lowerer {
             return table_lookup(s.str, key, (int)s.p0, w, "func");
         }
         throw Unsupported(opname(n) + " on a " + std::to_string(w) + "-bit value");
+    }
+
+    // -- the calldata word (ir._Lowerer._calldata_word) --------------------------
+    // x = base + c (mod 2^256): base -1 for a numeral
+    void index_parts(int x, int& base, U& c) const {
+        const Src& s = S[x];
+        if (s.op == S_BVNUM) { base = -1; c = s.val.chunk(0); return; }
+        if (s.op == S_BVADD && s.args.size() == 2) {
+            int a = s.args[0], b = s.args[1];
+            if (S[b].op == S_BVNUM && S[a].op != S_BVNUM) { base = a; c = S[b].val.chunk(0); return; }
+            if (S[a].op == S_BVNUM && S[b].op != S_BVNUM) { base = b; c = S[a].val.chunk(0); return; }
+        }
+        base = x;
+        c = U();
+    }
+
+    int calldata_word(int n) {
+        const Src& s = S[n];
+        if (s.width != 256 || s.args.size() != 32) return -1;
+        int size = -1, arr = -1, base = -1, off = -1;
+        U c0;
+        for (int i = 0; i < 32; i++) {
+            const Src& x = S[s.args[i]];
+            if (x.op != S_ITE || x.width != 8) return -1;
+            const Src& cond = S[x.args[0]];
+            const Src& sel = S[x.args[1]];
+            const Src& zero = S[x.args[2]];
+            if (zero.op != S_BVNUM || !zero.val.l.empty() || cond.op != S_BVSLT || sel.op != S_SELECT)
+                return -1;
+            int idx = sel.args[1];
+            if (cond.args[0] != idx || S[idx].width != 256) return -1;
+            if (i == 0) {
+                size = cond.args[1];
+                arr = sel.args[0];
+                if (S[arr].op != S_ARRAY) return -1;
+                index_parts(idx, base, c0);
+                off = idx;
+            } else if (cond.args[1] != size || sel.args[0] != arr) {
+                return -1;
+            } else {
+                int b;
+                U c;
+                index_parts(idx, b, c);
+                if (b != base || !(c == ((c0 + U::of((uint64_t)i)) & mask(256)))) return -1;
+            }
+        }
+        const std::string& name = S[arr].str;
+        const std::vector<Big>* ck = table_ckeys.find(name);
+        if ((ck && !ck->empty()) || (solve && solve_tables.count(name))) return -1;
+        table_kinds.put(name, "array");
+        int entries = table_sizes.setdefault(name, default_entries);
+        int o = narrow(off), sz = narrow(size);
+        int acc = mk(MG_BCAST, 256, {cell(name, K_ELSE, 0, 8)[0]});
+        for (int e = entries - 1; e >= 0; e--) {
+            int key = cell(name, K_KEY, e, 256)[0];
+            int delta = mk(MG_SUB, 256, {key, o});
+            int val = cell(name, K_VAL, e, 8)[0];
+            acc = mk(MG_CDWE, 256, {acc, delta, val});
+        }
+        return mk(MG_CDWX, 256, {acc, o, sz});
     }
 
     // -- arrays and uninterpreted functions ----------------------------------------
@@ -2246,9 +2308,11 @@ struct Alloc {
                 if (!nw) reg_clean[d] = N.width <= 32;
             } else {
                 if ((N.op == MG_ADD || N.op == MG_SUB || N.op == MG_AND || N.op == MG_OR || N.op == MG_XOR ||
-                     N.op == MG_NOT || N.op == MG_NEG || N.op == MG_ITE) && N.width > 32) {
+                     N.op == MG_NOT || N.op == MG_NEG || N.op == MG_ITE || N.op == MG_CDWE ||
+                     N.op == MG_CDWX) && N.width > 32) {
                     std::vector<int> cand;
                     if (N.op == MG_ITE) { for (size_t k = 1; k < 3 && k < slots.size(); k++) cand.push_back(slots[k]); }
+                    else if (N.op == MG_CDWE || N.op == MG_CDWX) cand.push_back(slots[0]);
                     else { for (size_t k = 0; k < 2 && k < slots.size(); k++) cand.push_back(slots[k]); }
                     for (int r : cand)
                         if (in(free_regs, r)) { remove(free_regs, r); d = r; break; }
@@ -2273,6 +2337,7 @@ struct Alloc {
             else if (N.op == MG_EXTRACT || N.op == MG_CONCAT || N.op == MG_SEXT) imm = (uint32_t)N.imm.w[0];
             else if (is_pred(N.op)) width = (uint32_t)N.imm.w[0];
             else if (N.op == MG_ITE) { c = slots[0]; a = slots[1]; b = slots[2]; }
+            else if (N.op == MG_CDWE || N.op == MG_CDWX) c = slots[2];
             ins.push_back({(uint32_t)N.op, width, (uint32_t)d, a, b, c, imm, flags});
         }
     }

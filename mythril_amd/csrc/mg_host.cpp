@@ -80,7 +80,8 @@ static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, u
     // for CONCAT's high part
     case MG_EXTRACT: return ((1u << d) | (3u << a)) & ((1u << MG_NREG) - 1);
     case MG_CONCAT: return (1u << d) | (1u << a) | (a ? 1u << (a - 1) : 0u) | (1u << b);
-    case MG_ITE: return (1u << d) | (1u << a) | (1u << b) | (1u << c);
+    case MG_ITE: case MG_CDWE: case MG_CDWX: return (1u << d) | (1u << a) | (1u << b) | (1u << c);
+    case MG_BCAST: return (1u << d) | (1u << a);
     default: return (1u << d) | (1u << a) | (1u << b);
     }
 }
@@ -94,8 +95,9 @@ static uint32_t slots_read(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint
     default: break;
     }
     const bool d_operand = d == a || (op != MG_NOT && op != MG_NEG && op != MG_MOV &&
-                                      op != MG_EXTRACT && op != MG_SEXT && d == b) ||
-                           (op == MG_ITE && d == c) || (op == MG_EXTRACT && d == a + 1) ||
+                                      op != MG_EXTRACT && op != MG_SEXT && op != MG_BCAST && d == b) ||
+                           ((op == MG_ITE || op == MG_CDWE || op == MG_CDWX) && d == c) ||
+                           (op == MG_EXTRACT && d == a + 1) ||
                            (op == MG_CONCAT && a && d == a - 1);
     return d_operand ? m : m & ~(1u << d);
 }
@@ -291,6 +293,9 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         case MG_OUT: aop = MGA_OUT; r[4] = imm; break;
         case MG_ROOT: aop = MGA_ROOT; break;
         case MG_MOV: aop = MGA_MOV; break;
+        case MG_BCAST: aop = MGA_BCAST; var = 0; break;
+        case MG_CDWE: aop = MGA_CDWE; var = d == a ? MGA_V_IP : 0; break;
+        case MG_CDWX: aop = MGA_CDWX; var = d == a ? MGA_V_IP : 0; break;
         default: aop = MGA_NOP; break;
         }
         // in place: the destination is operand a's slot (swap operands of
@@ -384,6 +389,12 @@ int mg_validate(std::string* err, const uint32_t* code, uint32_t n_ins, uint32_t
             break;
         case MG_SEXT:
             if (imm0 < 1 || imm0 > w) return fail(err, MG_E_ARG, "ins %u: sext width", pc);
+            break;
+        case MG_BCAST:
+        case MG_CDWE:
+        case MG_CDWX:          // their handlers write all eight limbs
+            if (w != MG_MAX_WIDTH) return fail(err, MG_E_ARG, "ins %u: calldata word width %u", pc, w);
+            if (in[0] & MG_ROOT_FLAG) return fail(err, MG_E_ARG, "ins %u: ROOT on a word", pc);
             break;
         default:
             break;

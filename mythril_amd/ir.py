@@ -363,6 +363,9 @@ class _Lowerer:
                 raise Unsupported("array-valued ite outside select")
             return [self.mk(I.ITE, w, (A(0), A(1), A(2)))]     # node width (>= both arms)
         if op == "concat":
+            word = self._calldata_word(n)
+            if word is not None:
+                return [word]
             return self.assemble([(self.memo[a.id], a.width) for a in n.args])
         if op == "extract":
             hi, lo = n.params
@@ -452,6 +455,80 @@ class _Lowerer:
             return self._table(fname, self.memo[n.args[0].id], dom, w, "func")
         raise Unsupported("%s on a %d-bit value" % (op, w))
 
+    # -- the calldata word --------------------------------------------------------
+    @staticmethod
+    def _index_parts(x: Node) -> Tuple[Optional[Node], int]:
+        """(base, constant) with x = base + constant (mod 2^256): a numeral
+        has no base; ``bvadd`` of a term and a numeral (either order, as LASER
+        builds it and as z3's simplify orders it) splits; anything else is
+        its own base."""
+        if x.op == "bvnum":
+            return None, x.params[0]
+        if x.op == "bvadd" and len(x.args) == 2:
+            a, b = x.args
+            if b.op == "bvnum" and a.op != "bvnum":
+                return a, b.params[0]
+            if a.op == "bvnum" and b.op != "bvnum":
+                return b, a.params[0]
+        return x, 0
+
+    def _calldata_word(self, n: Node) -> Optional[LNode]:
+        """LASER's calldata word (``calldata.py:47-54,219-232``)
+        ``Concat_{i<32} If(off + i <s size, select(cd, off + i), 0)`` over a
+        free array read through its model table (eval form: leaf-keyed
+        entries, no constant keys, not argument-keyed) as one chain — the
+        ``else`` byte broadcast, one ``CDWE`` per table entry (last entry
+        first, so the first match wins) on ``key - off``, then ``CDWX``
+        zeroing the bytes past ``size`` — instead of 32 byte lookups, 32
+        signed compares, 32 ITEs and 31 CONCATs.  Returns None when ``n`` is
+        not that shape.  The byte terms were lowered already (post-order);
+        nothing reads them unless another term does."""
+        if n.width != 256 or len(n.args) != 32:
+            return None
+        size = arr = base = None
+        c0 = 0
+        for i, x in enumerate(n.args):
+            if x.op != "ite" or x.width != 8:
+                return None
+            cond, sel, zero = x.args
+            if zero.op != "bvnum" or zero.params[0] != 0 or cond.op != "bvslt" or \
+                    sel.op != "select":
+                return None
+            idx = sel.args[1]
+            if cond.args[0] is not idx or idx.width != 256:
+                return None
+            if i == 0:
+                size, arr = cond.args[1], sel.args[0]
+                if arr.op != "array":
+                    return None
+                base, c0 = self._index_parts(idx)
+                off = idx
+            elif cond.args[1] is not size or sel.args[0] is not arr:
+                return None
+            else:
+                b, c = self._index_parts(idx)
+                if b is not base or c != (c0 + i) % (1 << 256):
+                    return None
+        name = arr.params[0]
+        if self.table_ckeys.get(name) or (self.solve and name in self.solve_tables):
+            return None
+        self.table_kinds[name] = "array"
+        entries = self.table_sizes.setdefault(name, self.default_entries)
+        o, sz = self._narrow(off), self._narrow(size)
+        acc = self.mk(I.BCAST, 256, (self._cell(name, "else", 0, 8)[0],))
+        for e in reversed(range(entries)):
+            delta = self.mk(I.SUB, 256, (self._cell(name, "key", e, 256)[0], o))
+            acc = self.mk(I.CDWE, 256, (acc, delta, self._cell(name, "val", e, 8)[0]))
+        return self.mk(I.CDWX, 256, (acc, o, sz))
+
+    def _cell(self, name: str, kind: str, e: int, width: int) -> List[LNode]:
+        """The leaves of one model-table cell (key / value / else / constant-
+        keyed value), one per 256-bit chunk."""
+        tag = {"key": "k%d" % e, "val": "v%d" % e, "else": "else", "cval": "c%d" % e}[kind]
+        return [self.leaf("%s#%s#%d" % (name, tag, k), self.chunk_width(width, k), kind,
+                          name, chunk=k, entry=e)
+                for k in range(self.nchunks(width))]
+
     # -- arrays and uninterpreted functions ------------------------------------
     def _chunk_eq(self, x: List[LNode], y: List[LNode], w: int) -> LNode:
         parts = [self.mk(I.EQ, self.chunk_width(w, k), (x[k], y[k])) for k in range(len(x))]
@@ -483,10 +560,7 @@ class _Lowerer:
         ckeys = self.table_ckeys.get(name, [])
 
         def cell(kind: str, e: int, width: int) -> List[LNode]:
-            tag = {"key": "k%d" % e, "val": "v%d" % e, "else": "else", "cval": "c%d" % e}[kind]
-            return [self.leaf("%s#%s#%d" % (name, tag, k), self.chunk_width(width, k), kind,
-                              name, chunk=k, entry=e)
-                    for k in range(self.nchunks(width))]
+            return self._cell(name, kind, e, width)
         kval = None
         if all(k.op == I.CONST for k in key):
             kval = 0
@@ -619,7 +693,7 @@ def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
     return out, fused
 
 
-_INPLACE = {I.ADD, I.SUB, I.AND, I.OR, I.XOR, I.NOT, I.NEG, I.ITE}
+_INPLACE = {I.ADD, I.SUB, I.AND, I.OR, I.XOR, I.NOT, I.NEG, I.ITE, I.CDWE, I.CDWX}
 
 
 def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = frozenset(),
@@ -765,7 +839,8 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
             # in place: reuse a dying operand's register (the engine then
             # writes the result through the file directly)
             if n.op in _INPLACE and n.width > 32:
-                cand = slots[1:3] if n.op == I.ITE else slots[:2]
+                cand = slots[1:3] if n.op == I.ITE else \
+                    slots[:1] if n.op in (I.CDWE, I.CDWX) else slots[:2]
                 for r in cand:
                     if r in free_regs:
                         free_regs.remove(r)
@@ -808,6 +883,8 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
             width = n.imm
         elif op == I.ITE:
             c, a, b = slots[0], slots[1], slots[2]
+        elif op in (I.CDWE, I.CDWX):
+            c = slots[2]
         ins.append((op, width, d, a, b, c, imm, flags))
     return ins, n_lds, n_spill, n_reload
 

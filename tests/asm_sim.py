@@ -439,6 +439,9 @@ class Wave:
     def i_s_cbranch_vccz(self, a, pc):
         return self._target(a[0]) if self.vcc == 0 else None
 
+    def i_s_cbranch_vccnz(self, a, pc):
+        return self._target(a[0]) if self.vcc != 0 else None
+
     def i_s_cbranch_execz(self, a, pc):
         return self._target(a[0]) if self.exec == 0 else None
 
@@ -599,6 +602,22 @@ class Wave:
 
     def i_v_alignbit_b32(self, a, pc):
         self._vop3(a, lambda hi, lo, s: (((hi << np.uint64(32)) | lo) >> (s & np.uint64(31))), 3)
+
+    def i_v_lshlrev_b64(self, a, pc):
+        s = self.vread(a[1], "SRC0")
+        x = self.vread(a[2], "SRC1", 64)
+        self.vwrite(a[0], (x << (s & np.uint64(63))) & np.uint64(M64))
+
+    def i_v_bfrev_b32(self, a, pc):
+        x = self.vread(a[1], "SRC0").astype(np.uint32)
+        r = np.zeros_like(x)
+        for k in range(32):
+            r |= ((x >> np.uint32(k)) & np.uint32(1)) << np.uint32(31 - k)
+        self.vwrite(a[0], r.astype(np.uint64))
+
+    def i_v_mul_u32_u24(self, a, pc):
+        m24 = np.uint64(0xFFFFFF)
+        self._vop2(a, lambda x, y: (x & m24) * (y & m24))
 
     def i_v_lshrrev_b64(self, a, pc):
         s = self.vread(a[1], "SRC0")

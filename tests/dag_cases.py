@@ -122,6 +122,71 @@ def array_case(entries=3):
     return constraints, probes, gen, {"A": entries, "cd": entries}
 
 
+def _cd_word(cd, size, off, numerals_first=False, const_base=None):
+    """LASER's calldata word (calldata.py:47-54,219-232): 32 bytes
+    If(off + i <s size, cd[off + i], 0), high byte first."""
+    parts = []
+    for i in range(32):
+        if const_base is not None:
+            idx = N.bv_num((const_base + i) % (1 << 256), 256)
+        elif i == 0:
+            idx = off
+        elif numerals_first:
+            idx = N.bv_op("bvadd", N.bv_num(i, 256), off)
+        else:
+            idx = N.bv_op("bvadd", off, N.bv_num(i, 256))
+        parts.append(N.ite(N.bv_cmp("bvslt", idx, size), N.select(cd, idx), N.bv_num(0, 8)))
+    return N.concat(*parts)
+
+
+# offsets around every edge of the word: the signed wrap of off + i at
+# 2^255 (u = off ^ 2^255 wraps at 2^256), the unsigned wrap of the index at
+# 2^256, zero, and ordinary ABI offsets
+CD_OFFSETS = (0, 4, 36, 68, (1 << 255) - 32, (1 << 255) - 31, (1 << 255) - 17, (1 << 255) - 1,
+              1 << 255, (1 << 256) - 32, (1 << 256) - 16, (1 << 256) - 1, (1 << 32) - 5,
+              ((1 << 32) - 5) | (0x7FFFFFFF << 224) | (((1 << 192) - 1) << 32))
+
+
+def calldata_word_case(entries=4):
+    """Calldata words over a free array read through its model table (the
+    fused BCAST / CDWE / CDWX chain, ir.py _calldata_word): symbolic
+    offsets (both bvadd operand orders), a constant offset, sizes that
+    straddle the word, sizes with the sign bit set, offsets at the signed
+    and unsigned wrap points, and table keys that hit the word at random
+    bytes, past its ends and more than once (first match wins)."""
+    cd = N.array_var("cdw", 256, 8)
+    size = N.bv_var("cdw_size", 256)
+    o1, o2 = N.bv_var("cdw_o1", 256), N.bv_var("cdw_o2", 256)
+    w1 = _cd_word(cd, size, o1)
+    w2 = _cd_word(cd, size, o2, numerals_first=True)
+    w3 = _cd_word(cd, size, None, const_base=4)
+    w4 = _cd_word(cd, size, N.bv_op("bvadd", o1, N.bv_num(4, 256)))
+    probes = [w1, w2, w3, w4, N.bv_op("bvxor", w1, w3)]
+    constraints = [N.bv_cmp("bvult", w3, w1)]
+
+    def gen(rng):
+        offs = [rng.choice(CD_OFFSETS) if rng.randrange(3) else edge_value(rng, 256)
+                for _ in range(2)]
+        ents = []
+        for _ in range(rng.randrange(entries + 1)):
+            base = rng.choice(offs + [4, 8])
+            key = (base + rng.choice((rng.randrange(-2, 36), rng.randrange(32)))) % (1 << 256)
+            ents.append((key, rng.randrange(256)))
+        sizes = [0, 1, 4, 35, 36, 40, 67, 68, 100, 1 << 255, (1 << 255) - 1, (1 << 256) - 1]
+        k = rng.randrange(4)
+        if k == 0:
+            sz = rng.choice(sizes)
+        elif k == 1:
+            sz = (rng.choice(offs) + rng.randrange(-3, 36)) % (1 << 256)
+        elif k == 2:
+            sz = edge_value(rng, 256)
+        else:
+            sz = ((1 << 255) - rng.randrange(40)) % (1 << 256)
+        return Assignment(vars={"cdw_o1": offs[0], "cdw_o2": offs[1], "cdw_size": sz},
+                          arrays={"cdw": (ents, rng.randrange(256))})
+    return constraints, probes, gen, {"cdw": entries}
+
+
 def keccak_uf_case():
     """The UF-pair shape of keccak_function_manager.py:121-149 on a 512-bit
     (mapping-slot) input: keccak256_512(concat(key, slot)) with the interval /
@@ -227,6 +292,7 @@ def named_cases():
     out["bool"] = (c, p, g, {})
     out["array"] = array_case()
     out["keccak_uf"] = keccak_uf_case()
+    out["calldata_word"] = calldata_word_case()
     c, p, g = overflow_case()
     out["overflow"] = (c, p, g, {})
     c, p, g = division_case()

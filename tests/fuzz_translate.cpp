@@ -63,9 +63,12 @@ static Prog valid_program(std::mt19937_64& rng) {
             break;
         case MG_EXTRACT: imm = rng() % (MG_MAX_WIDTH - w + 1); break;
         case MG_SEXT: imm = 1 + rng() % w; break;
+        case MG_BCAST: case MG_CDWE: case MG_CDWX: w = MG_MAX_WIDTH; break;   // words only
         default: break;
         }
-        if (rng() % 8 == 0 && op != MG_OUT && op != MG_ROOT) op |= MG_ROOT_FLAG;
+        if (rng() % 8 == 0 && op != MG_OUT && op != MG_ROOT && op != MG_BCAST && op != MG_CDWE &&
+            op != MG_CDWX)
+            op |= MG_ROOT_FLAG;
         p.code.push_back(ins_w0(op & 0xFF, w) | (op & MG_ROOT_FLAG));
         p.code.push_back(MG_INS_W1(d, a, b, c));
         p.code.push_back(imm);

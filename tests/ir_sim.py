@@ -97,6 +97,18 @@ def run(program, leaf_vals):
             pass
         elif op == I.MOV:
             r = x
+        elif op == I.BCAST:
+            r = (x & 0xFF) * int("01" * 32, 16)
+        elif op == I.CDWE:
+            r = x
+            if y < 32:
+                sh = 8 * (31 - y)
+                r = (x & ~(0xFF << sh)) | ((regs[c] & 0xFF) << sh)
+        elif op == I.CDWX:
+            r = x
+            for i in range(32):
+                if not _signed((y + i) % (1 << 256), 256) < _signed(regs[c], 256):
+                    r &= ~(0xFF << (8 * (31 - i)))
         else:
             raise AssertionError("op %d" % op)
         if w0 & I.ROOT_FLAG:

@@ -38,4 +38,4 @@ def test_version_without_gpu():
 
 def test_ir_header_matches_python_table():
     from mythril_amd import irdefs
-    assert irdefs.NUM_OPS == 34 and irdefs.ROOT == 32 and irdefs.TRASH == irdefs.NREG - 1
+    assert irdefs.NUM_OPS == 37 and irdefs.ROOT == 32 and irdefs.CDWX == 36 and irdefs.TRASH == irdefs.NREG - 1
