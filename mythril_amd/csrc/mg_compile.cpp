@@ -815,17 +815,19 @@ struct Lowerer {
     }
 
     // -- the calldata word (ir._Lowerer._calldata_word) --------------------------
-    // x = base + c (mod 2^256): base -1 for a numeral
+    // x = base + c (mod 2^256), nested adds of numerals folded: base -1 for
+    // a numeral
     void index_parts(int x, int& base, U& c) const {
-        const Src& s = S[x];
-        if (s.op == S_BVNUM) { base = -1; c = s.val.chunk(0); return; }
-        if (s.op == S_BVADD && s.args.size() == 2) {
-            int a = s.args[0], b = s.args[1];
-            if (S[b].op == S_BVNUM && S[a].op != S_BVNUM) { base = a; c = S[b].val.chunk(0); return; }
-            if (S[a].op == S_BVNUM && S[b].op != S_BVNUM) { base = b; c = S[a].val.chunk(0); return; }
-        }
-        base = x;
         c = U();
+        while (true) {
+            const Src& s = S[x];
+            if (s.op == S_BVNUM) { base = -1; c = (c + s.val.chunk(0)) & mask(256); return; }
+            if (s.op != S_BVADD || s.args.size() != 2) { base = x; return; }
+            int a = s.args[0], b = s.args[1];
+            if (S[b].op == S_BVNUM && S[a].op != S_BVNUM) { c = (c + S[b].val.chunk(0)) & mask(256); x = a; }
+            else if (S[a].op == S_BVNUM && S[b].op != S_BVNUM) { c = (c + S[a].val.chunk(0)) & mask(256); x = b; }
+            else { base = x; return; }
+        }
     }
 
     int calldata_word(int n) {

@@ -460,17 +460,22 @@ class _Lowerer:
     def _index_parts(x: Node) -> Tuple[Optional[Node], int]:
         """(base, constant) with x = base + constant (mod 2^256): a numeral
         has no base; ``bvadd`` of a term and a numeral (either order, as LASER
-        builds it and as z3's simplify orders it) splits; anything else is
-        its own base."""
-        if x.op == "bvnum":
-            return None, x.params[0]
-        if x.op == "bvadd" and len(x.args) == 2:
+        builds it and as z3's simplify orders it) splits, nested ones too
+        (``word(off + 4)`` reads ``(off + 4) + i``); anything else is its own
+        base."""
+        c = 0
+        while True:
+            if x.op == "bvnum":
+                return None, (c + x.params[0]) % (1 << 256)
+            if x.op != "bvadd" or len(x.args) != 2:
+                return x, c
             a, b = x.args
             if b.op == "bvnum" and a.op != "bvnum":
-                return a, b.params[0]
-            if a.op == "bvnum" and b.op != "bvnum":
-                return b, a.params[0]
-        return x, 0
+                x, c = a, (c + b.params[0]) % (1 << 256)
+            elif a.op == "bvnum" and b.op != "bvnum":
+                x, c = b, (c + a.params[0]) % (1 << 256)
+            else:
+                return x, c
 
     def _calldata_word(self, n: Node) -> Optional[LNode]:
         """LASER's calldata word (``calldata.py:47-54,219-232``)
