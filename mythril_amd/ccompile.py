@@ -274,6 +274,9 @@ def _program(code, raw: bytes, ncv: int, meta):
                       {k: [int(h, 16) for h in v] for k, v in meta["table_ckeys"]}, stats,
                       [tuple(r) for r in meta["pool_ranges"]], dict(meta["derived"]),
                       {k: v for k, v in meta["entry_keys"]}, meta["n_user_probes"])
+    # native compile phases (us): decode, lower, solve, sinks, schedule,
+    # allocate, pools, metadata — diagnostics only (tools/compile_profile.py)
+    prog.compile_us = meta.get("t_us")
     pre = meta.get("presets")
     if pre is not None:
         from .abi import Plan

@@ -20,6 +20,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -2696,7 +2697,17 @@ struct mgc_result {
 
 namespace {
 
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(
+        std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static void compile(const mgc_input* in, mgc_result* res) {
+    // phase boundaries (meta "t_us": decode, lower, solve, sinks, schedule,
+    // allocate, pools + tables, metadata) — diagnostics for the get_model
+    // compile latency, never part of the program
+    double tp[9];
+    tp[0] = now_us();
     // -- decode and check the source DAG ----------------------------------------
     // (the C ABI takes arrays from any caller: every index, count and width
     // is checked before use, so a malformed DAG is an error, never a wild
@@ -2801,6 +2812,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
         }
     }
 
+    tp[1] = now_us();
     Lowerer lw(S, in->default_entries);
     for (int t = 0; t < in->n_tables; t++) {
         if (in->table_name[t] < 0 || in->table_name[t] >= in->n_strings || in->table_size[t] < 0 ||
@@ -2829,6 +2841,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
         roots.push_back(lw.lower(c)[0]);
         births.push_back(S[c].id);
     }
+    tp[2] = now_us();
     std::vector<std::pair<int, int>> derived_nodes;
     Solver* solver = nullptr;
     std::unique_ptr<Solver> solver_own;
@@ -2837,6 +2850,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
         solver = solver_own.get();
         solver->run(roots, derived_nodes);
     }
+    tp[3] = now_us();
     Memo probe_memo;
     Chunks sinks;
     for (size_t i = 0; i < roots.size(); i++) {
@@ -2884,8 +2898,10 @@ static void compile(const mgc_input* in, mgc_result* res) {
     }
     for (auto& n : lw.ln)
         if (is_pred(n.op)) { n.imm = U::of((uint64_t)n.width); n.has_imm = true; n.width = 1; }
+    tp[4] = now_us();
     std::unordered_set<int> fused;
     std::vector<int> order = fuse_roots(lw.ln, schedule(lw.ln, sinks), fused);
+    tp[5] = now_us();
     U M256 = mask(256);
     std::vector<U> const_values;
     for (int n : order) if (lw.ln[n].op == MG_CONST) const_values.push_back(lw.ln[n].imm & M256);
@@ -2901,6 +2917,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
     for (size_t i = 0; i < const_values.size(); i++) const_index[const_values[i]] = (int)i;
     Alloc al(lw.ln, order, const_index, fused, in->nreg, in->remat_mode, in->remat_k, in->keep_clean != 0);
     al.run();
+    tp[6] = now_us();
     res->code.resize(4 * al.ins.size());
     for (size_t k = 0; k < al.ins.size(); k++) {
         const Ins& x = al.ins[k];
@@ -2937,6 +2954,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
     for (const auto& pl : pools)
         for (const U& u : pl) put(u);
 
+    tp[7] = now_us();
     // -- metadata ---------------------------------------------------------------
     std::string& o = res->meta;
     o = "{\"leaves\":[";
@@ -3053,6 +3071,14 @@ static void compile(const mgc_input* in, mgc_result* res) {
         o += "]]";
     }
     o += "],\"n_user_probes\":" + std::to_string(n_user_probes);
+    tp[8] = now_us();
+    o += ",\"t_us\":[";
+    for (int k = 0; k < 8; k++) {
+        char b[32];
+        std::snprintf(b, sizeof b, "%s%.1f", k ? "," : "", tp[k + 1] - tp[k]);
+        o += b;
+    }
+    o += "]";
     if (have_presets) {
         o += ",\"presets\":{\"vars\":[";
         for (size_t i = 0; i < presets.vars.size(); i++) {
