@@ -6,8 +6,10 @@
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 TAG=${1:-r4m}
 for W in c3 c4; do
-  timeout -k 10 400 python -u bench.py --workload $W --no-cpu-baseline > gpurun_out/${TAG}_bench_$W.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_$W.log; exit 1; }
-  tail -c 300 gpurun_out/${TAG}_bench_$W.log
+  for P in ${REMAT_POLICIES:-scratch2}; do
+    MYTHRIL_GPU_LEAF_REMAT=$P timeout -k 10 400 python -u bench.py --workload $W --no-cpu-baseline > gpurun_out/${TAG}_bench_${W}_$P.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench_${W}_$P.log; exit 1; }
+    tail -c 300 gpurun_out/${TAG}_bench_${W}_$P.log
+  done
 done
 timeout -k 10 300 python -u tools/search_jit_probe.py > gpurun_out/${TAG}_search_jit.log 2>&1 || { tail -20 gpurun_out/${TAG}_search_jit.log; exit 1; }
 timeout -k 10 400 python -u tools/superset_census.py > gpurun_out/${TAG}_superset.log 2>&1 || { tail -20 gpurun_out/${TAG}_superset.log; exit 1; }

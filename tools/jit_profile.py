@@ -3,7 +3,8 @@
 instruction-level simulator (tests/asm_sim.py) running corpus DAGs in
 generator mode: VALU / SALU / other per record of each family, so the JIT's
 remaining overhead can be located without a GPU.
-usage: tools/jit_profile.py [dag ids...]"""
+usage: tools/jit_profile.py [dag ids...]   (C2 corpus DAGs)
+       tools/jit_profile.py c3 [unit ids...]   (bench units of c3 / c4 / c5)"""
 import bisect
 import collections
 import functools
@@ -61,10 +62,17 @@ def step(self, op, a, pc):
 
 
 asm_sim.Wave.step = step
-dags = [int(x) for x in sys.argv[1:]] or [0, 1, 2, 3, 5, 8]
+args = sys.argv[1:]
+workload = args.pop(0) if args and args[0].startswith("c") else "c2"
+dags = [int(x) for x in args] or ([0, 1, 2, 3, 5, 8] if workload == "c2" else
+                                  list(range(0, 64, 8)))
 for d in dags:
-    roots, _ = make_dag(d, SEED)
-    prog = compile_constraints(roots)
+    if workload == "c2":
+        roots, _ = make_dag(d, SEED)
+        prog = compile_constraints(roots)
+    else:
+        import bench
+        prog = bench.compile_unit((workload, d))[1]
     for name, n in prog.stats["hist"].items():
         NREC[name] += n
     asm_sim.simulate(prog, gen=(SEED, d, 4096, default_leafgen(prog)), jit=True)
