@@ -69,7 +69,7 @@ def shape_lines(eng, n_queries, n_sample=48):
     from mythril_amd.smt.node import topo_order
     out = {}
     M.time_handler.start_execution(3600)
-    for name in ("c1", "c3", "c4"):
+    for name in ("c1", "c3", "c4", "c5"):
         qs = W.queries(name, n_queries)
         M._SEARCH_CACHE = None
         t0 = time.perf_counter()
@@ -137,7 +137,12 @@ def shape_lines(eng, n_queries, n_sample=48):
             "batch": {"candidates_per_program": n_cand, "wall_s": dt,
                       "queries_with_witness": sum(solved), "hit_rate": sum(solved) / len(qs),
                       "candidates_needed": needed, "candidates_per_s": needed / dt,
-                      "ir_ins_candidates_per_s": ins_cand / dt},
+                      "ir_ins_candidates_per_s": ins_cand / dt,
+                      # where the witnesses are: how far a search must go
+                      "hit_groups": sum(i >= 0 for i, _ in hits),
+                      "first_index_max": max([i for i, _ in hits if i >= 0], default=-1),
+                      "first_index_over": {str(1 << b): sum(i >= (1 << b) for i, _ in hits)
+                                           for b in (8, 12, 16, 18, 20)}},
             "get_model": cold,
             "get_model_stream": stream,
         }
