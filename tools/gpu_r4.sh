@@ -4,6 +4,11 @@
 # workloads in $PROFILE_TAGS ("c2" = the default bench, else --workload <w>).
 # Each GPU step has its own time limit; the chain stops at the first failure.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+# long fixtures (oracle runs over every bench unit, image assembly) print
+# nothing for minutes: keep a heartbeat file moving for gpurun's watchdog
+( while true; do date >> gpurun_out/heartbeat.txt; sleep 45; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 TAG=${1:-r4}
 if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; echo "gpu tests failed"; exit 1; }

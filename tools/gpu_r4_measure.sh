@@ -4,6 +4,11 @@
 # superset-memo census, the search bench.  Each GPU step has its own limit;
 # the chain stops at the first failure.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+# long fixtures (oracle runs over every bench unit, image assembly) print
+# nothing for minutes: keep a heartbeat file moving for gpurun's watchdog
+( while true; do date >> gpurun_out/heartbeat.txt; sleep 45; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 TAG=${1:-r4m}
 for W in c3 c4; do
   for P in ${REMAT_POLICIES:-scratch2}; do
