@@ -41,11 +41,16 @@ typedef struct mg_batch mg_batch;
 typedef struct mg_jit mg_jit;
 
 /* Device candidate generator for one leaf (free variable / table cell),
- * generator v7 (restated bit-exactly by oracle/gen_ref.py):
+ * generator v8 (restated bit-exactly by oracle/gen_ref.py):
  *   salt = prog_seed * 0xD1B54A32D192ED03 ^ (leaf + 1) * 0x8CB92BA72F3D8DD7
- *   r0   = SplitMix64(seed ^ salt ^ index)          (one step, state += golden)
+ *   ss   = seed ^ salt
+ *   r0   = SplitMix64(ss ^ index)                   (one step, state += golden)
  *   x    = lo(r0) ^ hi(r0)                          (32 bits)
- *   cls  = mulhi(x * 0x2545F491 mod 2^32, 100)      (not from emitted value bits)
+ *   cls  = mulhi(((lo32(index >> 6) ^ lo32(ss)) * 0x2545F491 mod 2^32)
+ *                ^ hi32(ss), 100)                   (one class per leaf per
+ *                                                    group of 64 indices: a
+ *                                                    wave from a multiple of
+ *                                                    64 runs one class's code)
  * and by class (thresholds are cumulative percentages):
  *   pct_uniform <= cls < pct_small   r0 (< 2^64)
  *   pct_small <= cls < pct_boundary  {0, 1, 2^(w-1), 2^256-1, 2^k+1, 2^k-1},

@@ -1055,7 +1055,7 @@ def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
 GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
 PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
-CLS_MUL = 0x2545F491                              # class remix (generator v7)
+CLS_MUL = 0x2545F491                              # class remix (generator v7/v8)
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
 S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
@@ -1097,26 +1097,71 @@ def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
     a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
 
 
-def _class_mask(a: Asm, out: int, lo_sgpr: Optional[int], hi_sgpr: Optional[int], cls: int):
-    """s[out:out+1] = lanes with lo <= cls < hi (all lanes active)."""
-    if lo_sgpr is not None and hi_sgpr is not None:
-        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(out), s(lo_sgpr), v(cls)))
-        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(S_T), s(hi_sgpr), v(cls)))
-        a("s_and_b64 %s, %s, %s" % (sp(out), sp(out), sp(S_T)))
-    elif lo_sgpr is not None:
-        a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(out), s(lo_sgpr), v(cls)))
-    else:
-        a("v_cmp_gt_u32_e64 %s, %s, %s" % (sp(out), s(hi_sgpr), v(cls)))
+def _uniform_limbs(a: Asm, dst: List[int], z: List[int], x: int):
+    """The uniform class's value: r0 in limbs 0-1, limb pair k = 1..3 is
+    x * C_k + r0 (mod 2^64) with x = lo ^ hi of r0 — one v_mad_u64_u32 per
+    two limbs (v6; v4 spent a 4-VALU multiply-xorshift per limb).  Uses
+    s[S_PAIR..S_PAIR+2] and v[x]."""
+    a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(x), v(z[0]), v(z[1])))
+    for k, c in enumerate(PAIR_MUL):
+        a("s_mov_b32 %s, 0x%x" % (s(S_PAIR + k), c))
+    for k in range(3):
+        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(x), s(S_PAIR + k),
+                                                 vp(z[0])))
+
+
+def _boundary_loads(a: Asm, dst: List[int], lo: int, f, tt: List[int]):
+    """Boundary values {0, 1, 2^(w-1), 2^256-1, 2^k+1, 2^k-1}: one load pair
+    from the context's boundary table (mg_api.cpp mg_boundary_table): entry
+    kind * 256 + p, p = w - 1 for kind 2 and k otherwise, kind = mulhi(lo,
+    6), k = mulhi(lo * 0x9E3779B1, w); masked to the width by the handler.
+    The table pointer is loaded here, into s[S_T+6:S_T+7] (only waves of
+    this class pay for it; that pair is the dispatch's jump target, so the
+    load is settled before the block ends)."""
+    a("s_load_dwordx2 %s, %s, 0x38" % (sp(S_T + 6), IN["desc"]))   # boundary table
+    kind, k, bit = tt[0], tt[1], tt[2]
+    a("v_mul_hi_u32 %s, %s, 6" % (v(kind), v(lo)))
+    a("s_mov_b32 %s, 0x9e3779b1" % s(S_T))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(k), v(lo), s(S_T)))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(k), v(k), s(f["w"])))
+    a("s_sub_u32 %s, %s, 1" % (s(S_T + 1), s(f["w"])))
+    a("v_mov_b32 %s, %s" % (v(bit), s(S_T + 1)))
+    a("v_cmp_eq_u32 vcc, 2, %s" % v(kind))
+    a("v_cndmask_b32 %s, %s, %s, vcc" % (v(k), v(k), v(bit)))
+    a("v_lshl_add_u32 %s, %s, 8, %s" % (v(k), v(kind), v(k)))
+    a("v_lshlrev_b32 %s, 5, %s" % (v(k), v(k)))
+    a("s_waitcnt lgkmcnt(0)")
+    a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(k), sp(S_T + 6)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(k), sp(S_T + 6)))
+
+
+def _pool_loads(a: Asm, dst: List[int], lo: int, f, tt: List[int]):
+    """Pool values consts[pool_off + e] + delta - 1, stored as (v-1, v, v+1)
+    triples (entry e * 3 + delta): e = mulhi(lo, pool_n), delta =
+    mulhi(lo * 0x85EBCA6B, 3); one load pair."""
+    e, delta = tt[0], tt[1]
+    a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(f["pn"])))
+    a("s_mov_b32 %s, 0x85ebca6b" % s(S_T))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(delta), v(lo), s(S_T)))
+    a("v_mul_hi_u32 %s, %s, 3" % (v(delta), v(delta)))
+    a("v_mad_u32_u24 %s, %s, 3, %s" % (v(e), v(e), v(delta)))
+    a("v_lshl_add_u32 %s, %s, 5, %s" % (v(e), v(e), s(f["poff"])))
+    a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(e), sp(S_CONST)))
+    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(e), sp(S_CONST)))
 
 
 def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = True):
     """dst[0..7] (default X) <- generator value of leaf C for candidate
     first + lane; the boundary / pool lanes arrive by loads into dst, waited
     for unless wait=False (LEAFD: the translator places the WAITVM).
-    Mirrors oracle/gen_ref.py gen_leaf.  The uniform class's value (the
-    class word r0 in limbs 0-1, limbs 2-7 mixed from it) is computed for
-    every lane (the small class is r0);
-    the boundary and pool classes then overwrite their lanes under exec.
+    Mirrors oracle/gen_ref.py gen_leaf (generator v8).  r0 = SplitMix64 of
+    the candidate index is computed per lane; the class (v8) is drawn once
+    per group of 64 consecutive indices, so when every active lane of the
+    wave is in one group — every wave of a launch that starts at a multiple
+    of 64: all search and bench launches — the class is wave-uniform and
+    only its own code runs (branch on the scalar class).  A wave across
+    two groups (an unaligned eval) runs the two classes in turn.
     Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
     pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi.  A
     LEAFD (``in_record``: 256 bits) finds them in its own record instead
@@ -1126,7 +1171,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     cls, lo = T[8], z[0]
     g = S_CUR
     in_record = dst is not None and dst != X
-    a("s_load_dwordx2 %s, %s, 0x38" % (sp(S_T + 6), IN["desc"]))   # boundary table
     if in_record:
         f = {"w": g + 0, "poff": fld(bank, LEAFD_POFF), "pn": fld(bank, LEAFD_PN),
              "pu": g + 3, "ps": g + 4, "pb": g + 5, "salt": fld(bank, LEAFD_SALT)}
@@ -1147,80 +1191,66 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
     if not in_record:
         a("s_waitcnt lgkmcnt(0)")
-    a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(f["salt"])))
+    a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(f["salt"])))     # ss = seed ^ salt
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), OP_IDX_LO))
     a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), OP_IDX_HI))
+    # v8 class: cls = mulhi(((lo32(idx >> 6) ^ lo32(ss)) * CLS_MUL) ^ hi32(ss), 100)
+    a("v_alignbit_b32 %s, %s, %s, 6" % (v(cls), OP_IDX_HI, OP_IDX_LO))
+    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T), v(cls)))
+    a("s_mov_b32 %s, 0x%x" % (s(S_T + 2), CLS_MUL))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(cls), s(S_T + 2)))
+    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T + 1), v(cls)))
+    a("s_movk_i32 %s, 100" % s(S_T + 2))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(S_T + 2)))
     sm64(a, st, z, tt)
-    # ---- uniform values for every lane: r0 in limbs 0-1 (small lanes keep
-    # only those), limb pair k = 1..3 is x * C_k + r0 (mod 2^64) with
-    # x = lo ^ hi of r0: one v_mad_u64_u32 per two limbs (v6; v4 spent a
-    # 4-VALU multiply-xorshift per limb)
-    # (built straight in dst: a LEAFD's slot)
     dst = X if dst is None else dst
+    # waterfall over the wave's distinct class draws: exec = the lanes whose
+    # draw equals the first active lane's, run that class's code, repeat
+    # with the rest.  A wave of consecutive indices spans at most two
+    # groups; a launch from a multiple of 64 is one pass (the common path:
+    # ~8 SALU + 2 VALU over the class's own code).
+    sc, rest, save = S_T + 2, S_T + 4, S_X          # (division's lane masks: free here)
+    lab_loop, lab_again = a.uniq("gcls"), a.uniq("gagain")
+    lab_uni, lab_small, lab_bnd, lab_done = (a.uniq("guni"), a.uniq("gsml"), a.uniq("gbnd"),
+                                             a.uniq("gdone"))
+    a("s_mov_b64 %s, exec" % sp(save))
+    a.label(lab_loop)
+    a("v_readfirstlane_b32 %s, %s" % (s(sc), v(cls)))
+    a("v_cmp_eq_u32 vcc, %s, %s" % (s(sc), v(cls)))
+    a("s_and_saveexec_b64 %s, vcc" % sp(rest))
+    a("s_andn2_b64 %s, %s, exec" % (sp(rest), sp(rest)))   # lanes still to do
+    a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["pu"])))
+    a("s_cbranch_scc1 %s" % lab_uni)                 # cls < pct_uniform
+    a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["ps"])))
+    a("s_cbranch_scc1 %s" % lab_small)
+    a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["pb"])))
+    a("s_cbranch_scc1 %s" % lab_bnd)
+    a("s_cmp_eq_u32 %s, 0" % s(f["pn"]))
+    a("s_cbranch_scc1 %s" % lab_uni)                 # pool class, empty pool
+    _pool_loads(a, dst, lo, f, tt)                   # pool
+    a("s_branch %s" % lab_done)
+    a.label(lab_bnd)
+    _boundary_loads(a, dst, lo, f, tt)
+    a("s_branch %s" % lab_done)
+    a.label(lab_small)                               # small: r0 (< 2^64)
     a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(tt[0]), v(z[0]), v(z[1])))
-    # v7: class = mulhi(x * CLS_MUL, 100) — from a remix of x, not from bits
-    # that are emitted as value bits (oracle/gen_ref.py gen_class)
-    a("s_mov_b32 %s, 0x%x" % (s(S_T), CLS_MUL))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(tt[0]), s(S_T)))
-    a("s_movk_i32 %s, 100" % s(S_T + 1))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(S_T + 1)))
-    for k, c in enumerate(PAIR_MUL):
-        a("s_mov_b32 %s, 0x%x" % (s(S_PAIR + k), c))
-    for k in range(3):
-        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(tt[0]), s(S_PAIR + k),
-                                                 vp(z[0])))
-    # class masks from three compares (cls >= each threshold), ranges by
-    # SALU: small = ge_u & ~ge_s, boundary = ge_s & ~ge_b, pool = ge_b
-    ge_s, ge_b = S_X, S_X + 2                   # (division's lane masks: free here)
-    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(S_T + 2), s(f["pu"]), v(cls)))
-    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(ge_s), s(f["ps"]), v(cls)))
-    a("v_cmp_le_u32_e64 %s, %s, %s" % (sp(ge_b), s(f["pb"]), v(cls)))
-    a("s_andn2_b64 %s, %s, %s" % (sp(S_T + 2), sp(S_T + 2), sp(ge_s)))   # small
-    lab = exec_begin(a, S_T + 2, S_T + 4)
     moves(a, dst[2:], [None] * 6)
-    exec_end(a, lab, S_T + 4)
-    # ---- boundary: pct_small <= cls < pct_boundary -------------------------
-    a("s_andn2_b64 %s, %s, %s" % (sp(S_T + 2), sp(ge_s), sp(ge_b)))     # boundary
-    # (no skip branch: with 64 lanes some lane nearly always is in the class;
-    # with exec = 0 the loads access nothing)
-    a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
-    if in_record:
-        a("s_waitcnt lgkmcnt(0)")                  # the boundary table pointer
-    # one load from the context's boundary table (mg_api.cpp
-    # mg_boundary_table): entry kind * 256 + p, p = width - 1 for kind 2
-    # (1 << (w-1)) and k otherwise; masked to the width by the handler
-    kind, k, bit = tt[0], tt[1], tt[2]
-    a("v_mul_hi_u32 %s, %s, 6" % (v(kind), v(lo)))
-    a("s_mov_b32 %s, 0x9e3779b1" % s(S_T))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(k), v(lo), s(S_T)))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(k), v(k), s(f["w"])))
-    a("s_sub_u32 %s, %s, 1" % (s(S_T + 1), s(f["w"])))
-    a("v_mov_b32 %s, %s" % (v(bit), s(S_T + 1)))
-    a("v_cmp_eq_u32 vcc, 2, %s" % v(kind))
-    a("v_cndmask_b32 %s, %s, %s, vcc" % (v(k), v(k), v(bit)))
-    a("v_lshl_add_u32 %s, %s, 8, %s" % (v(k), v(kind), v(k)))
-    a("v_lshlrev_b32 %s, 5, %s" % (v(k), v(k)))
-    a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(k), sp(S_T + 6)))
-    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(k), sp(S_T + 6)))
-    # ---- pool: cls >= pct_boundary and pool_n > 0 --------------------------
-    # the pool is stored as (v-1, v, v+1) triples: entry e * 3 + delta
-    a("s_mov_b64 exec, %s" % sp(S_T + 4))
-    a("s_cmp_lg_u32 %s, 0" % s(f["pn"]))
-    a("s_cselect_b64 %s, %s, 0" % (sp(S_T + 2), sp(ge_b)))             # pool
-    a("s_and_b64 exec, %s, %s" % (sp(S_T + 2), sp(S_T + 4)))
-    e, delta = tt[0], tt[1]
-    a("v_mul_hi_u32 %s, %s, %s" % (v(e), v(lo), s(f["pn"])))
-    a("s_mov_b32 %s, 0x85ebca6b" % s(S_T))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(delta), v(lo), s(S_T)))
-    a("v_mul_hi_u32 %s, %s, 3" % (v(delta), v(delta)))
-    a("v_mad_u32_u24 %s, %s, 3, %s" % (v(e), v(e), v(delta)))
-    a("v_lshl_add_u32 %s, %s, 5, %s" % (v(e), v(e), s(f["poff"])))
-    a("global_load_dwordx4 v[%d:%d], %s, %s" % (dst[0], dst[3], v(e), sp(S_CONST)))
-    a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(e), sp(S_CONST)))
-    a("s_mov_b64 exec, %s" % sp(S_T + 4))
+    a("s_branch %s" % lab_done)
+    a.label(lab_uni)
+    _uniform_limbs(a, dst, z, tt[0])
+    a.label(lab_done)
+    a("s_mov_b64 exec, %s" % sp(rest))
+    a("s_cbranch_execnz %s" % lab_again)
+    a("s_mov_b64 exec, %s" % sp(save))
     if wait:
-        a("s_waitcnt vmcnt(0)")                   # boundary and pool loads
+        a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
+    a.cold()
+    # another group in this wave: its loads are in flight into other lanes
+    # of dst; settle them before the next class writes dst
+    a.label(lab_again)
+    a("s_waitcnt vmcnt(0)")
+    a("s_branch %s" % lab_loop)
+    a.hot()
 
 
 def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):

@@ -359,6 +359,8 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
     idx_at: Dict[str, object] = {}       # label -> index state where it was placed
     call = None
     fallthrough = True
+    dead = False                         # after a branch folded taken: skip to a reached label
+    dead_labels = set()                  # labels skipped in such code (no branch may go there)
 
     def emit(text):
         out.append(text)
@@ -384,6 +386,8 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
         return list(range(r[0], r[0] + r[1])) if r else []
 
     def branch_to(label):
+        if label in dead_labels:
+            raise JitUnsupported("branch to %s in code a folded branch skipped" % label)
         if label in idx_at:
             if idx_at[label] != st.idx:
                 raise JitUnsupported("index state differs on a branch back to %s" % label)
@@ -431,9 +435,15 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
         if t.endswith(":"):
             lab = t[:-1]
             if lab not in targets:
+                if dead:
+                    continue
                 if not fallthrough:
                     raise JitUnsupported("label %s is never reached" % lab)
                 continue                     # no branch comes here: not a join
+            if dead and lab not in idx_in:
+                dead_labels.add(lab)         # only branches from skipped code come here
+                continue
+            dead = False
             incoming = idx_in.pop(lab, "none")
             if fallthrough:
                 settle(i)
@@ -474,6 +484,8 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
             st.idx = None
             continue
         if not fallthrough:
+            if dead:
+                continue                     # the folded branch's skipped code
             raise JitUnsupported("unreachable code after a jump: %s" % t)
         # ---- control flow ------------------------------------------------
         if m in ("s_cbranch_scc0", "s_cbranch_scc1") and st.scc is not None:
@@ -481,7 +493,7 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
                 settle(i)
                 branch_to(ops[0])
                 emit(render("s_branch", ops))
-                fallthrough = False
+                fallthrough, dead = False, True
             continue
         if m.startswith("s_cbranch") or m == "s_branch":
             settle(i)

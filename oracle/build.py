@@ -6,16 +6,18 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "lib", "libevalref.so")
+LIB_WIDE = os.path.join(HERE, "lib", "libevalref_wide.so")    # 1024-bit values (-DL=16)
 
 
 def build(force: bool = False) -> str:
     src = os.path.join(HERE, "evalref.c")
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= os.path.getmtime(src):
-        return LIB
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.run(["gcc", "-O3", "-fopenmp", "-fPIC", "-shared", "-Wall", "-o", LIB + ".tmp", src],
-                   check=True)
-    os.replace(LIB + ".tmp", LIB)
+    for lib, defs in ((LIB, []), (LIB_WIDE, ["-DL=16"])):
+        if not force and os.path.exists(lib) and os.path.getmtime(lib) >= os.path.getmtime(src):
+            continue
+        os.makedirs(os.path.dirname(lib), exist_ok=True)
+        subprocess.run(["gcc", "-O3", "-fopenmp", "-fPIC", "-shared", "-Wall"] + defs +
+                       ["-o", lib + ".tmp", src], check=True)
+        os.replace(lib + ".tmp", lib)
     return LIB
 
 

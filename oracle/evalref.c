@@ -7,7 +7,8 @@
  * z3.Optimize.check / Model.eval; SMT-LIB 2.6 FixedSizeBitVectors with
  * hi_div0, as restated in oracle/smtlib_ref.py, which pins this file in
  * tests/test_evalref.py).  It evaluates the SOURCE DAG (not the GPU IR):
- * values are 512-bit (8 x u64 limbs), division is Knuth D on 64-bit digits
+ * values are 512-bit (8 x u64 limbs; the _wide build, -DL=16, 1024-bit for
+ * DAGs with wider nodes: keccak inputs of three words), division is Knuth D on 64-bit digits
  * with __int128 estimates, arrays are resolved by walking store chains,
  * free arrays / UFs by first-match table lookup.  Assignments are either
  * given (SoA leaf values) or rebuilt with the same SplitMix64 candidate
@@ -22,7 +23,9 @@
 #include <omp.h>
 #endif
 
-#define L 8                      /* 8 x 64 = 512 bits */
+#ifndef L
+#define L 8                      /* 8 x 64 = 512 bits (-DL=16: the wide build) */
+#endif
 typedef struct { uint64_t w[L]; } V;
 
 enum {
@@ -96,7 +99,7 @@ static void vneg(const V* a, V* r) {
     vsub(&z, a, r);
 }
 
-static void vmul(const V* a, const V* b, V* r) {   /* low 512 bits */
+static void vmul(const V* a, const V* b, V* r) {   /* low L * 64 bits */
     uint64_t t[L] = {0};
     for (int i = 0; i < L; ++i) {
         unsigned __int128 c = 0;
@@ -414,7 +417,7 @@ static void eval_dag(const dag_t* g, const V* leaves, V* vals) {
         case E_SLT: r.w[0] = vslt(a, b, n[5]); break;
         case E_SLE: r.w[0] = !vslt(b, a, n[5]); break;
         case E_UMULNO: {
-            /* a, b < 2^w with w <= 256, so the full product fits 512 bits */
+            /* a, b < 2^w with w <= 256, so the full product fits L * 64 bits */
             V p;
             vmul(a, b, &p);
             V m = p;
@@ -446,13 +449,14 @@ static uint64_t sm64(uint64_t* s) {
 
 static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t idx, uint32_t w,
                      const uint64_t* pool, uint32_t pool_n, const uint32_t pct[3], V* out) {
-    uint64_t s = seed ^ (prog_seed * 0xD1B54A32D192ED03ull) ^
-                 ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull) ^ idx;   /* v5 */
+    const uint64_t ss = seed ^ (prog_seed * 0xD1B54A32D192ED03ull) ^
+                        ((uint64_t)(leaf + 1) * 0x8CB92BA72F3D8DD7ull);
+    uint64_t s = ss ^ idx;                                                /* v5 */
     uint64_t r0 = sm64(&s);
-    /* v2 range reduction: multiply-high (Lemire) instead of modulo; v7: the
-     * class from a remix of lo ^ hi, not from emitted value bits */
-    const uint32_t xr = (uint32_t)r0 ^ (uint32_t)(r0 >> 32);
-    uint32_t cls = mulhi32(xr * 0x2545F491u, 100u), lo = (uint32_t)r0;
+    /* v2 range reduction: multiply-high (Lemire) instead of modulo; v8: the
+     * class once per group of 64 candidate indices (idx >> 6) */
+    const uint32_t y = (((uint32_t)(idx >> 6) ^ (uint32_t)ss) * 0x2545F491u) ^ (uint32_t)(ss >> 32);
+    uint32_t cls = mulhi32(y, 100u), lo = (uint32_t)r0;
     vzero(out);
     if (cls >= pct[0] && cls < pct[1]) {
         out->w[0] = r0;                       /* v3: the class word itself */
@@ -476,7 +480,7 @@ static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t 
         vzero(&one);
         one.w[0] = 1;
         vzero(&p);
-        memcpy(p.w, pool + (size_t)e * L, 4 * sizeof(uint64_t));
+        memcpy(p.w, pool + (size_t)e * L, 4 * sizeof(uint64_t));   /* entries are L words */
         if (delta == 0) vsub(&p, &one, out);
         else if (delta == 2) vadd(&p, &one, out);
         else *out = p;
@@ -513,6 +517,19 @@ static void make_tables(const table_desc* td, uint32_t n, const uint32_t* leafid
     }
 }
 
+/* Limbs per value of this build (consts, pool and vals_out use this stride). */
+int ev_limbs(void) { return L; }
+
+/* -2 when a node or table is wider than this build's values (the caller
+ * picks the wide build; nothing is evaluated). */
+static int too_wide(const uint32_t* nodes, uint32_t n_nodes, const table_desc* td, uint32_t n_tables) {
+    for (uint32_t i = 0; i < n_nodes; ++i)
+        if (nodes[(size_t)i * NW + 1] > L * 64) return 1;
+    for (uint32_t t = 0; t < n_tables; ++t)
+        if (td[t].key_w > L * 64 || td[t].val_w > L * 64) return 1;
+    return 0;
+}
+
 /* Evaluate under generated candidates [first, first + n): root bits. */
 int ev_run_gen(const uint32_t* nodes, uint32_t n_nodes, const uint64_t* consts,
                const table_desc* td, uint32_t n_tables, const uint32_t* leafidx,
@@ -522,6 +539,7 @@ int ev_run_gen(const uint32_t* nodes, uint32_t n_nodes, const uint64_t* consts,
                uint8_t* root_out, int threads) {
     table_t tabs[64];
     if (n_tables > 64) return -1;
+    if (too_wide(nodes, n_nodes, td, n_tables)) return -2;
     make_tables(td, n_tables, leafidx, tabs);
     dag_t g = {nodes, n_nodes, consts, tabs, n_tables};
 #ifdef _OPENMP
@@ -554,6 +572,7 @@ int ev_run_leaves_roots(const uint32_t* nodes, uint32_t n_nodes, const uint64_t*
                         const uint64_t* leaves_in, uint64_t n, uint8_t* root_out, int threads) {
     table_t tabs[64];
     if (n_tables > 64) return -1;
+    if (too_wide(nodes, n_nodes, td, n_tables)) return -2;
     make_tables(td, n_tables, leafidx, tabs);
     dag_t g = {nodes, n_nodes, consts, tabs, n_tables};
 #ifdef _OPENMP
@@ -588,6 +607,7 @@ int ev_run_leaves(const uint32_t* nodes, uint32_t n_nodes, const uint64_t* const
                   const uint64_t* leaves_in, uint64_t n, uint64_t* vals_out, uint8_t* root_out) {
     table_t tabs[64];
     if (n_tables > 64) return -1;
+    if (too_wide(nodes, n_nodes, td, n_tables)) return -2;
     make_tables(td, n_tables, leafidx, tabs);
     dag_t g = {nodes, n_nodes, consts, tabs, n_tables};
     V* vals = (V*)malloc(sizeof(V) * (n_nodes ? n_nodes : 1));

@@ -158,13 +158,14 @@ def serialize(constraints: Sequence[Node], program, probes: Sequence[Node] = ())
     return S
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        path = _build.LIB
+def lib(wide: bool = False):
+    """The C oracle: 512-bit values, or ``wide`` 1024-bit (a DAG with a node
+    or table wider than 512 bits; the 512-bit build refuses one, rc -2)."""
+    if wide not in _libs:
+        path = _build.LIB_WIDE if wide else _build.LIB
         if not os.path.exists(path):
             _build.build()
         L = C.CDLL(path)
@@ -176,20 +177,30 @@ def lib():
                                     p, C.c_uint64, p, p]
         L.ev_run_leaves_roots.argtypes = [p, C.c_uint32, p, p, C.c_uint32, p, p, C.c_uint32,
                                           C.c_uint32, p, C.c_uint64, p, C.c_int]
-        _lib = L
-    return _lib
+        L.ev_limbs.restype = C.c_int
+        _libs[wide] = L
+    return _libs[wide]
+
+
+def _wide(S: Serialized) -> bool:
+    w = max([r[1] for r in S.recs] + [t.key_w for t in S.tables] + [t.val_w for t in S.tables] +
+            [0])
+    return w > 512 or any(v >> 512 for v in S.consts)
 
 
 def _arrays(S: Serialized):
+    """(library, limbs, nodes, consts, tables, leafidx, roots)."""
+    L = lib(_wide(S))
+    nl = L.ev_limbs()
     nodes = np.ascontiguousarray(np.array(S.recs, dtype=np.uint32).reshape(-1, 8))
-    consts = np.zeros((max(1, len(S.consts)), 8), dtype=np.uint64)
+    consts = np.zeros((max(1, len(S.consts)), nl), dtype=np.uint64)
     for i, v in enumerate(S.consts):
-        for k in range(8):
+        for k in range(nl):
             consts[i, k] = (v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
     tabs = (TableDesc * max(1, len(S.tables)))(*S.tables)
     leafidx = np.array(S.leafidx or [0], dtype=np.uint32)
     roots = np.array(S.roots or [0], dtype=np.uint32)
-    return nodes, consts, tabs, leafidx, roots
+    return L, nl, nodes, consts, tabs, leafidx, roots
 
 
 def _p(a):
@@ -198,25 +209,25 @@ def _p(a):
 
 def run_gen(S: Serialized, program, seed: int, prog_seed: int, first: int, n: int,
             threads: int = 0, pct=(50, 70, 85)) -> np.ndarray:
-    nodes, consts, tabs, leafidx, roots = _arrays(S)
+    L, nl, nodes, consts, tabs, leafidx, roots = _arrays(S)
     widths = np.array([l.width for l in program.leaves] or [1], dtype=np.uint32)
-    pool = np.zeros((max(1, len(program.const_values)), 8), dtype=np.uint64)
+    pool = np.zeros((max(1, len(program.const_values)), nl), dtype=np.uint64)
     for i, v in enumerate(program.const_values):
         for k in range(4):
             pool[i, k] = (v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
     pctv = np.array(pct, dtype=np.uint32)
     out = np.zeros(n, dtype=np.uint8)
-    rc = lib().ev_run_gen(_p(nodes), nodes.shape[0], _p(consts), C.cast(tabs, C.c_void_p),
+    rc = L.ev_run_gen(_p(nodes), nodes.shape[0], _p(consts), C.cast(tabs, C.c_void_p),
                           len(S.tables), _p(leafidx), _p(roots), len(S.roots), _p(widths),
                           len(program.leaves), _p(pool), len(program.const_values), _p(pctv),
                           seed & (2**64 - 1), prog_seed & (2**64 - 1), first, n, _p(out), threads)
-    assert rc == 0
+    assert rc == 0, rc
     return out.astype(bool)
 
 
 def run_leaves(S: Serialized, program, leaf_vals: Sequence[Sequence[int]], want_nodes=False):
     """leaf_vals: per assignment, the program's leaf values (<= 256 bits)."""
-    nodes, consts, tabs, leafidx, roots = _arrays(S)
+    L, nl_, nodes, consts, tabs, leafidx, roots = _arrays(S)
     n = len(leaf_vals)
     nl = len(program.leaves)
     lv = np.zeros((max(1, n), max(1, nl), 4), dtype=np.uint64)
@@ -224,9 +235,9 @@ def run_leaves(S: Serialized, program, leaf_vals: Sequence[Sequence[int]], want_
         for i, v in enumerate(vals):
             for k in range(4):
                 lv[a, i, k] = (v >> (64 * k)) & 0xFFFFFFFFFFFFFFFF
-    vals_out = np.zeros((n, nodes.shape[0], 8), dtype=np.uint64) if want_nodes else None
+    vals_out = np.zeros((n, nodes.shape[0], nl_), dtype=np.uint64) if want_nodes else None
     out = np.zeros(max(1, n), dtype=np.uint8)
-    rc = lib().ev_run_leaves(_p(nodes), nodes.shape[0], _p(consts), C.cast(tabs, C.c_void_p),
+    rc = L.ev_run_leaves(_p(nodes), nodes.shape[0], _p(consts), C.cast(tabs, C.c_void_p),
                              len(S.tables), _p(leafidx), _p(roots), len(S.roots), nl, _p(lv), n,
                              None if vals_out is None else _p(vals_out), _p(out))
     assert rc == 0
@@ -238,7 +249,7 @@ def run_leaves_soa(S: Serialized, program, leaves_soa: np.ndarray, per_root: boo
     """Root bits (``per_root``: (n, n_constraints) bits of every constraint)
     under the engine's own leaf buffer ((n_leaves, 8, n) u32 limbs, e.g.
     ``Engine.eval_gen(..., want_leaves=True)``)."""
-    nodes, consts, tabs, leafidx, roots = _arrays(S)
+    L, _, nodes, consts, tabs, leafidx, roots = _arrays(S)
     nl, _, n = leaves_soa.shape
     x = np.ascontiguousarray(leaves_soa.transpose(2, 0, 1)).astype(np.uint64)   # (n, nl, 8)
     lv = np.ascontiguousarray(x[:, :, 0::2] | (x[:, :, 1::2] << np.uint64(32)))  # (n, nl, 4)
@@ -246,7 +257,7 @@ def run_leaves_soa(S: Serialized, program, leaves_soa: np.ndarray, per_root: boo
         lv = np.zeros((max(1, n), 1, 4), dtype=np.uint64)
     nr = max(1, len(S.roots))
     out = np.zeros((max(1, n), nr), dtype=np.uint8)
-    rc = lib().ev_run_leaves_roots(_p(nodes), nodes.shape[0], _p(consts),
+    rc = L.ev_run_leaves_roots(_p(nodes), nodes.shape[0], _p(consts),
                                    C.cast(tabs, C.c_void_p), len(S.tables), _p(leafidx), _p(roots),
                                    len(S.roots), max(nl, 1), _p(lv), n, _p(out), threads)
     assert rc == 0
@@ -256,6 +267,6 @@ def run_leaves_soa(S: Serialized, program, leaves_soa: np.ndarray, per_root: boo
 
 def node_value(vals_out, a: int, rec_index: int) -> int:
     v = 0
-    for k in reversed(range(8)):
+    for k in reversed(range(vals_out.shape[2])):
         v = (v << 64) | int(vals_out[a, rec_index, k])
     return v

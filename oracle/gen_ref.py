@@ -24,22 +24,34 @@ def _sm64(s):
 CLS_MUL = 0x2545F491
 
 
-def gen_class(r0: int) -> int:
-    """v7: the class comes from a multiplicative remix of x = lo ^ hi of r0,
-    not from bits that are emitted as value bits (v3-v6 used r0 >> 32, which
-    confined bits 32-63 of the uniform / small values to their class's
-    percentage band: bit 63 was never set by a random class)."""
-    x = (r0 ^ (r0 >> 32)) & 0xFFFFFFFF
-    return _mulhi((x * CLS_MUL) & 0xFFFFFFFF, 100)
+def gen_class(seed: int, prog_seed: int, leaf: int, idx: int) -> int:
+    """v8: the class is drawn once per leaf per GROUP of 64 consecutive
+    candidate indices (idx >> 6: the candidates of one wave when a launch
+    starts at a multiple of 64, which every search / bench launch does), so
+    a wave evaluates one class's code instead of all four under exec:
+      ss  = seed ^ salt
+      y   = ((lo32(idx >> 6) ^ lo32(ss)) * CLS_MUL) ^ hi32(ss)   (mod 2^32)
+      cls = mulhi(y, 100)
+    v7 drew it per lane from a remix of r0 (and v3-v6 from r0 >> 32, which
+    confined value bits 32-63 to the class's band); the value bits still
+    come from r0 alone."""
+    ss = (seed ^ _salt(prog_seed, leaf)) & M64
+    w = (idx >> 6) & 0xFFFFFFFF
+    y = ((((w ^ ss) & 0xFFFFFFFF) * CLS_MUL) & 0xFFFFFFFF) ^ (ss >> 32)
+    return _mulhi(y, 100)
+
+
+def _salt(prog_seed: int, leaf: int) -> int:
+    return ((prog_seed * 0xD1B54A32D192ED03) & M64) ^ (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64)
 
 
 def gen_leaf(seed: int, prog_seed: int, leaf: int, idx: int, width: int, pool,
              pct=(50, 70, 85)) -> int:
-    s = (seed ^ ((prog_seed * 0xD1B54A32D192ED03) & M64) ^
-         (((leaf + 1) * 0x8CB92BA72F3D8DD7) & M64) ^ idx) & M64    # v5: idx itself
+    s = (seed ^ _salt(prog_seed, leaf) ^ idx) & M64    # v5: idx itself
     s, r0 = _sm64(s)
-    # v2 range reduction: multiply-high (Lemire), no modulo
-    cls = gen_class(r0)
+    # v2 range reduction: multiply-high (Lemire), no modulo; v8: the class
+    # per 64-candidate group
+    cls = gen_class(seed, prog_seed, leaf, idx)
     lo = r0 & 0xFFFFFFFF
     mask = (1 << width) - 1
     if pct[0] <= cls < pct[1]:

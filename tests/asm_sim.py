@@ -445,6 +445,9 @@ class Wave:
     def i_s_cbranch_execz(self, a, pc):
         return self._target(a[0]) if self.exec == 0 else None
 
+    def i_s_cbranch_execnz(self, a, pc):
+        return self._target(a[0]) if self.exec != 0 else None
+
     def i_s_getpc_b64(self, a, pc):
         self.swrite(a[0], CODE_BASE + 8 * (pc + 1))
 
@@ -503,6 +506,12 @@ class Wave:
 
     def i_v_mov_b64(self, a, pc):
         self.vwrite(a[0], self.vread(a[1], "SRC0", 64))
+
+    def i_v_readfirstlane_b32(self, a, pc):
+        # the lowest active lane (lane 0 with exec = 0)
+        x = self.vread(a[1], "SRC0")
+        lane = (self.exec & -self.exec).bit_length() - 1 if self.exec else 0
+        self.swrite(a[0], int(x[lane]) & M32)
 
     def _vop2(self, a, f):
         x = self.vread(a[1], "SRC0")

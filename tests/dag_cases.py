@@ -187,14 +187,18 @@ def calldata_word_case(entries=4):
     return constraints, probes, gen, {"cdw": entries}
 
 
-def keccak_uf_case():
+def keccak_uf_case(words: int = 2):
     """The UF-pair shape of keccak_function_manager.py:121-149 on a 512-bit
     (mapping-slot) input: keccak256_512(concat(key, slot)) with the interval /
-    mod-64 conditions and the inverse function."""
+    mod-64 conditions and the inverse function.  ``words=3``: a 768-bit input
+    (concat(key, key2, slot): wider than the 512-bit C oracle build, so it
+    runs on the wide one)."""
+    bits = 256 * words
     key, slot = N.bv_var("kkey", 256), N.bv_var("kslot", 256)
-    data = N.concat(key, slot)
-    f = lambda t: N.apply_uf("keccak256_512", 512, 256, t)        # noqa: E731
-    inv = lambda t: N.apply_uf("keccak256_512-1", 256, 512, t)    # noqa: E731
+    data = N.concat(key, slot) if words == 2 else N.concat(N.concat(key, N.bv_var("kkey2", 256)), slot)
+    fn = "keccak256_%d" % bits
+    f = lambda t: N.apply_uf(fn, bits, 256, t)                   # noqa: E731
+    inv = lambda t: N.apply_uf(fn + "-1", 256, bits, t)          # noqa: E731
     h = f(data)
     TOTAL_PARTS = 10 ** 40
     PART = (2 ** 256 - 1) // TOTAL_PARTS
@@ -203,20 +207,24 @@ def keccak_uf_case():
                      N.bool_op("or", N.bv_cmp("bvult", N.bv_num(lo, 256), h), N.eq(N.bv_num(lo, 256), h)),
                      N.bv_cmp("bvult", h, N.bv_num(lo + PART, 256)),
                      N.eq(N.bv_op("bvurem", h, N.bv_num(64, 256)), N.bv_num(0, 256)))
-    probes = [h, inv(h), N.extract(300, 100, data), N.extract(511, 256, inv(h)),
+    probes = [h, inv(h), N.extract(300, 100, data), N.extract(bits - 1, bits - 256, inv(h)),
               N.zero_extend(256, key)]
     constraints = [cond]
 
     def gen(rng):
         kv, sv = edge_value(rng, 256), rng.randrange(8)
+        vars_ = {"kkey": kv, "kslot": sv}
         d = (kv << 256) | sv
+        if words == 3:
+            vars_["kkey2"] = edge_value(rng, 256)
+            d = (kv << 512) | (vars_["kkey2"] << 256) | sv
         hv = lo + 64 * rng.randrange(1 << 20) if rng.randrange(3) else edge_value(rng, 256)
         fent = [(d, hv)] if rng.randrange(4) else []
         ient = [(hv, d)] if rng.randrange(4) else [(hv, edge_value(rng, 256))]
-        return Assignment(vars={"kkey": kv, "kslot": sv},
-                          funcs={"keccak256_512": (fent, edge_value(rng, 256)),
-                                 "keccak256_512-1": (ient, rng.getrandbits(512))})
-    return constraints, probes, gen, {"keccak256_512": 2, "keccak256_512-1": 2}
+        return Assignment(vars=vars_,
+                          funcs={fn: (fent, edge_value(rng, 256)),
+                                 fn + "-1": (ient, rng.getrandbits(bits))})
+    return constraints, probes, gen, {fn: 2, fn + "-1": 2}
 
 
 def overflow_case():
@@ -292,6 +300,7 @@ def named_cases():
     out["bool"] = (c, p, g, {})
     out["array"] = array_case()
     out["keccak_uf"] = keccak_uf_case()
+    out["keccak_uf_768"] = keccak_uf_case(3)
     out["calldata_word"] = calldata_word_case()
     c, p, g = overflow_case()
     out["overflow"] = (c, p, g, {})
