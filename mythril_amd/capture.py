@@ -149,16 +149,16 @@ def replay_gpu(records: List[dict]) -> Dict[str, object]:
                 continue
             sets.append(cs)
             idx.append(r["id"])
-    progs, owner = [], []
+    per_set, owner = [], []
     for k, cs in enumerate(sets):
-        try:
-            for b in M.dependence_buckets(cs):
-                progs.append(M._compile_search(b))
-                owner.append(k)
+        try:            # all of a set's groups or none (a partial set is no witness)
+            per_set.append([M._compile_search(b) for b in M.dependence_buckets(cs)])
         except Unsupported:
             continue
+        owner += [k] * len(per_set[-1])
     t0 = time.perf_counter()
-    hits = M.batch_search_devices(progs, M.SEARCH_CANDIDATES)   # (index, model) per group
+    # (index, model) per group, one batched search; constant groups on the host
+    hits = M._search_sets(per_set, M.SEARCH_CANDIDATES)
     secs = time.perf_counter() - t0
     found = collections.defaultdict(list)
     for k, (i, a) in zip(owner, hits):

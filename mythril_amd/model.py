@@ -34,6 +34,7 @@ from typing import Dict, List, Optional, Sequence
 from . import z3bridge
 from .assign import Assignment, unpack
 from .engine import EngineError, EngineUnavailable, LeafGen, device_slots, get_engine
+from . import irdefs as I
 from .ir import Program, Unsupported, compile_constraints, harvest_hints  # noqa: F401
 from .smt import node as N
 
@@ -110,6 +111,8 @@ class SolverStatistics:
         self.unsupported = 0
         self.errors = 0
         self.rejected = 0
+        self.ground_true = 0            # groups folded to true: answered without a launch
+        self.ground_false = 0           # queries with a group folded to false: not searched
         self.phase = {k: 0.0 for k in PHASES}
 
     def gpu_report(self) -> str:
@@ -434,6 +437,49 @@ def _n_cand(progs: Sequence[Program], budget_ms: float) -> int:
     return 1 << (n.bit_length() - 1)
 
 
+GROUND_MISS = 1 << 62     # group-miss depth of a group that folds to false
+
+
+def _ground_value(p: Program) -> Optional[bool]:
+    """The truth value of a group the compiler folded to a constant root (its
+    one instruction is a CONST carrying the ROOT flag, no leaf and no ABI
+    preset left: nothing for a candidate to choose), else None.  Such a
+    group needs no launch: true joins every witness as is, false means no
+    candidate satisfies the query (z3 decides it)."""
+    if p.n_ins != 1 or p.leaves or p.presets:
+        return None
+    w0 = int(p.code[0, 0])
+    if (w0 & 0xFF) != I.CONST or not (w0 & I.ROOT_FLAG):
+        return None
+    return bool(int(p.consts[int(p.code[0, 2]), 0]) & 1)
+
+
+def search_groups(progs: Sequence[Program], n_cand: int):
+    """``batch_search_devices`` over the groups that need a search: a group
+    folded to a constant (:func:`_ground_value`) is answered on the host —
+    true: (0, empty model); false: (-1, None) — and nothing is launched for
+    any group of a query with a false one (round 4: 2 of 3 C3 stand-in groups
+    fold to true; every one was a load + launch + witness read)."""
+    return _search_sets([progs], n_cand)
+
+
+def _search_sets(sets: Sequence[Sequence[Program]], n_cand: int):
+    """:func:`search_groups` over several queries' groups in ONE batched
+    search: a query with a group folded to false contributes no launch."""
+    ground = [[_ground_value(p) for p in progs] for progs in sets]
+    dead = [any(g is False for g in gs) for gs in ground]
+    stats.ground_false += sum(dead)
+    live = [p for progs, gs, d in zip(sets, ground, dead) if not d
+            for p, g in zip(progs, gs) if g is None]
+    stats.ground_true += sum(g is True for gs, d in zip(ground, dead) if not d for g in gs)
+    found = iter(batch_search_devices(live, n_cand) if live else ())
+    out = []
+    for gs, d in zip(ground, dead):
+        for g in gs:
+            out.append((-1, None) if d else next(found) if g is None else (0, Assignment()))
+    return out
+
+
 def batch_search_devices(progs: Sequence[Program], n_cand: int):
     """``Engine.batch_search`` over ``DEVICES``: programs are spread over the
     devices by longest-processing-time first on their instruction counts
@@ -665,8 +711,15 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
         stats.memo_misses += 1
         return None
     devices = list(DEVICES) or [0]
-    if len(progs) > 1 or len(devices) > 1:
-        hits = batch_search_devices(progs, n_cand)
+    ground = [_ground_value(p) for p in progs]
+    if any(g is False for g in ground):
+        stats.ground_false += 1
+        for k, g in zip(keys, ground):
+            if g is False:
+                _note_miss(k, GROUND_MISS)
+        return None
+    if len(progs) > 1 or len(devices) > 1 or ground[0] is not None:
+        hits = search_groups(progs, n_cand)
     else:
         eng = get_engine(devices[0])
         with _Phase("load"):
@@ -915,7 +968,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
             t0 = time.perf_counter()
             flat = [p for _, progs in pending for p in progs]
             n_cand = _n_cand(flat, min(timeout, SEARCH_BUDGET_MS))
-            hits = iter(batch_search_devices(flat, n_cand))
+            hits = iter(_search_sets([progs for _, progs in pending], n_cand))
             stats.gpu_time += time.perf_counter() - t0
             for cs, progs in pending:
                 found = [next(hits) for _ in progs]
@@ -923,7 +976,8 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
                 stats.gpu_candidates += sum(n_cand if k < 0 else k + 1 for k, _ in found)
                 for p, (k, _) in zip(progs, found):
                     if k < 0 and p.group_key is not None:
-                        _note_miss(p.group_key, n_cand)
+                        _note_miss(p.group_key, GROUND_MISS if _ground_value(p) is False
+                                   else n_cand)
                 if any(k < 0 for k, _ in found):
                     # the set goes straight to z3 only when the batch searched
                     # it as far as get_model alone would have; otherwise

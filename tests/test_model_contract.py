@@ -140,7 +140,9 @@ def test_batch_is_possible_matches_the_per_state_loop(batch_env, monkeypatch):
     unsat_like = symbol_factory.Bool(False).__class__(symbol_factory.Bool(False).raw)
     sets = [(c_sat(),), (c_sat(), False), (unsat_like,), (True, c_sat()), (ULT(x, x),)]
     got = M.batch_is_possible(sets)
-    assert eng.batches == [4]                        # one batched search, no per-set launches
+    # one batched search, no per-set launches; the constant-false set folds
+    # on the host (no launch: model.search_groups)
+    assert eng.batches == [3]
     want = []
     for cs in sets:
         try:
@@ -684,3 +686,33 @@ def test_repeated_devices_get_their_own_contexts(monkeypatch):
     progs = [compile_constraints([N.bv_cmp("bvult", x, N.bv_num(k + 3, 256))]) for k in range(4)]
     M.batch_search_devices(progs, 1 << 16)
     assert sorted(set(asked)) == [(0, 0), (0, 1)]
+
+
+_REAL_GPU_SEARCH = M.gpu_search
+
+
+def test_constant_groups_are_answered_on_the_host(batch_env, monkeypatch):
+    """A group the compiler folds to a constant root needs no launch
+    (model._ground_value): true joins the witness as is, false sends the
+    query to z3 without searching its other groups, and the false group is
+    remembered as a miss at any depth."""
+    eng, z3_calls = batch_env
+    monkeypatch.setattr(M, "gpu_search", _REAL_GPU_SEARCH)
+    M.clear_search_memos()
+    x = symbol_factory.BitVecSym("gx", 256)
+    y = symbol_factory.BitVecSym("gy", 256)
+    t = symbol_factory.BitVecVal(3, 8) == symbol_factory.BitVecVal(3, 8)
+    f = symbol_factory.BitVecVal(3, 8) == symbol_factory.BitVecVal(4, 8)
+    live = ULT(x, symbol_factory.BitVecVal(5, 256))
+    raws = M._raw_nodes([t, live])
+    progs = [M._compile_search(b) for b in M.dependence_buckets(raws)]
+    assert sorted(M._ground_value(p) is True for p in progs) == [False, True]
+    M.stats.reset_gpu()
+    M.get_model((t, live), enforce_execution_time=False)
+    assert eng.batches == [1] and M.stats.ground_true == 1       # only the live group
+    eng.batches.clear()
+    with pytest.raises(M.UnsatError):
+        M.get_model((f, ULT(y, symbol_factory.BitVecVal(9, 256))), enforce_execution_time=False)
+    assert eng.batches == [] and M.stats.ground_false == 1 and len(z3_calls) == 1
+    fkey = M._group_key(M.dependence_buckets(M._raw_nodes([f]))[0])
+    assert M._group_miss[fkey] == M.GROUND_MISS
