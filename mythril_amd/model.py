@@ -28,6 +28,8 @@ from __future__ import annotations
 
 import logging
 import time
+
+import numpy as np
 from functools import lru_cache
 from typing import Dict, List, Optional, Sequence
 
@@ -441,17 +443,19 @@ GROUND_MISS = 1 << 62     # group-miss depth of a group that folds to false
 
 
 def _ground_value(p: Program) -> Optional[bool]:
-    """The truth value of a group the compiler folded to a constant root (its
-    one instruction is a CONST carrying the ROOT flag, no leaf and no ABI
-    preset left: nothing for a candidate to choose), else None.  Such a
-    group needs no launch: true joins every witness as is, false means no
-    candidate satisfies the query (z3 decides it)."""
-    if p.n_ins != 1 or p.leaves or p.presets:
-        return None
-    w0 = int(p.code[0, 0])
-    if (w0 & 0xFF) != I.CONST or not (w0 & I.ROOT_FLAG):
-        return None
-    return bool(int(p.consts[int(p.code[0, 2]), 0]) & 1)
+    """False when a root of the group folded to the constant false (a CONST
+    instruction carrying the ROOT flag: no candidate can satisfy it, whatever
+    the other roots); True when the whole group folded to the constant true
+    (its one instruction, no leaf and no ABI preset left: nothing for a
+    candidate to choose); else None.  Such a group needs no launch: true
+    joins every witness as is, false sends the query to z3."""
+    w0 = p.code[:, 0]
+    for k in np.flatnonzero(((w0 & 0xFF) == I.CONST) & ((w0 & I.ROOT_FLAG) != 0)):
+        if not int(p.consts[int(p.code[k, 2]), 0]) & 1:
+            return False
+    if p.n_ins == 1 and not p.leaves and not p.presets and (int(w0[0]) & 0xFF) == I.CONST:
+        return True
+    return None
 
 
 def search_groups(progs: Sequence[Program], n_cand: int):

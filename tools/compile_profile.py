@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--queries", type=int, default=24)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--graph", default="", help="write gprof's call graph here")
     args = ap.parse_args()
     import numpy as np
     import mythril_amd.model as M
@@ -67,6 +68,11 @@ def main():
         out = subprocess.run(["gprof", "-b", "-p", exe, os.path.join(d, "gmon.out")],
                              capture_output=True, text=True, check=True).stdout
         print("\n".join(out.splitlines()[:args.top + 5]))
+        if args.graph:
+            g = subprocess.run(["gprof", "-b", "-q", exe, os.path.join(d, "gmon.out")],
+                               capture_output=True, text=True, check=True).stdout
+            with open(args.graph, "w") as fh:
+                fh.write(g)
 
 
 if __name__ == "__main__":
