@@ -504,9 +504,32 @@ struct Lowerer {
     }
 
     // -- main lowering (ir._Lowerer.lower) -------------------------------------
+    // post-order of the nodes under n not lowered yet (ir._Lowerer._pending:
+    // a lowered node's operands are not walked again)
+    std::vector<char> pend_seen_;
+    std::vector<int> pending(int n) {
+        if (pend_seen_.size() < S.size()) pend_seen_.assign(S.size(), 0);
+        std::vector<int> out, touched;
+        std::vector<std::pair<int, bool>> stack{{n, false}};
+        while (!stack.empty()) {
+            auto [m, done] = stack.back();
+            stack.pop_back();
+            if (done) { out.push_back(m); continue; }
+            if (pend_seen_[m] || has_memo[m]) continue;
+            pend_seen_[m] = 1;
+            touched.push_back(m);
+            stack.push_back({m, true});
+            const auto& a = S[m].args;
+            for (size_t i = a.size(); i-- > 0;)
+                if (!pend_seen_[a[i]] && !has_memo[a[i]]) stack.push_back({a[i], false});
+        }
+        for (int m : touched) pend_seen_[m] = 0;
+        return out;
+    }
+
     const Chunks& lower(int n) {
         if (has_memo[n]) return memo[n];
-        std::vector<int> nodes = topo(S, {n});
+        std::vector<int> nodes = pending(n);
         std::unordered_set<int> skip;
         for (int m : nodes)
             if (S[m].op == S_EXTRACT && is_carry(m)) {

@@ -251,7 +251,7 @@ class _Lowerer:
         if r is not None:
             return r
         # iterative post-order so deep DAGs do not hit the recursion limit
-        nodes = topo_order([n])
+        nodes = self._pending(n)
         skip = set()
         for m in nodes:            # operands consumed only through the carry pattern
             if m.op == "extract" and self._is_carry(m):
@@ -270,6 +270,29 @@ class _Lowerer:
                 self.birth = m.id
         self.birth = max(saved, self.birth) if saved else self.birth
         return self.memo[n.id]
+
+    def _pending(self, n: Node) -> List[Node]:
+        """Post-order of the nodes under ``n`` not lowered yet: a lowered
+        node's operands are not walked again (every constraint's lower()
+        call walked the whole DAG below it; a carry pattern's skipped
+        operands under a node lowered by an earlier call are then no longer
+        in this call's skip set, so a later use elsewhere is lowered instead
+        of being refused)."""
+        memo, seen, out = self.memo, set(), []
+        stack = [(n, False)]
+        while stack:
+            m, done = stack.pop()
+            if done:
+                out.append(m)
+                continue
+            if m.id in seen or m.id in memo:
+                continue
+            seen.add(m.id)
+            stack.append((m, True))
+            for a in reversed(m.args):
+                if a.id not in seen and a.id not in memo:
+                    stack.append((a, False))
+        return out
 
     def _narrow(self, n: Node) -> LNode:
         ch = self.memo[n.id]
