@@ -504,7 +504,7 @@ def test_assignment_axis_equals_single_device_sweep(monkeypatch, sat, G):
 
 def test_single_group_query_uses_every_device(monkeypatch, fresh, reset_engine_memo):
     log = []
-    engines = {d: StreamEngine(d, [3 << 20], log) for d in range(4)}
+    engines = {d: StreamEngine(d, [3 << 17], log) for d in range(4)}
     monkeypatch.setattr(M, "get_engine", lambda dev=0, slot=0: engines[dev])
     monkeypatch.setattr(M, "DEVICES", [0, 1, 2, 3])
     M.clear_search_memos()
