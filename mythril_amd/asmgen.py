@@ -1935,6 +1935,20 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     vn = Y
     b, c, dinv = T[2], T[3], T[10]
     bz = S_T + 4
+    # every active lane's divisor fits one limb: short division, out of line
+    lab_short, lab_done = a.uniq("dsh"), a.uniq("dsd")
+    t = T[4]
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[1]), v(Y[2]), v(Y[3])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[4]), v(Y[5])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[6]), v(Y[7])))
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
+    a("s_cmp_eq_u64 vcc, exec")
+    a("s_cbranch_scc1 %s" % lab_short)
+    a.cold()
+    a.label(lab_short)
+    _udivrem_short(a, want_rem, z)
+    a("s_branch %s" % lab_done)
+    a.hot()
     for j in range(0, 8, 2):
         a("v_mov_b64 %s, 0" % vp(R[j]))
     a("v_mov_b32 %s, 0" % v(T[0]))                                       # un[16]
@@ -1981,9 +1995,79 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(vn[4]), v(vn[5])))
     a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(DIV_Z6), v(t)))
     d = vn[7]
-    # dinv = floor((2^64-1)/d) - 2^32 (d >= 2^31): f64 reciprocal, one
-    # Newton step (the estimate is then within one of the exact value), then
-    # one exact integer correction in each direction
+    _reciprocal(a, d, dinv)
+    a("v_mov_b32 %s, 0" % v(T[9]))                                  # RH of the digit loop
+    for j in reversed(range(8)):
+        u2, u1 = un[j + 8], un[j + 7]
+        skip = a.uniq("dvs")
+        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(u2)))
+        a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(u1), v(d)))
+        a("s_or_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 2)))
+        a("s_cbranch_vccz %s" % skip)
+        _div_digit(a, un, vn, j, d, dinv)
+        a.label(skip)
+    if want_rem:
+        # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
+        a("v_mov_b32 %s, 0" % v(T[0]))
+        t = X + [T[0]]
+        for st in (1, 2, 4):
+            _stage(a, t, st, 9, False, DIV_M[st])
+        bitshift_right(a, t, b, 8)
+    a.label(lab_done)
+
+
+def _udivrem_short(a: Asm, want_rem: bool, z: int):
+    """udivrem when every active lane's divisor Y fits 32 bits (wave-uniform:
+    no limb barrel, no multiply-subtract): d = Y[0] << b normalised, u =
+    X << b over 9 limbs, then eight 2-by-1 steps with the reciprocal
+    (r:u[j]) / d -> quotient digit R[j], remainder r (r < d throughout),
+    remainder = r >> b.  Same contract as udivrem: lanes with Y == 0 divide
+    0 by 1 (s[z:z+1] marks them).  Registers: d = Y0, b = T2, c / r = T3,
+    A = T4:T5, P = T6:T7, CR = T8, dinv = T10, QH = T11."""
+    d, b, c, r, dinv = Y[0], T[2], T[3], T[3], T[10]
+    A0, A1, P0, CR, QH = T[4], T[5], T[6], T[8], T[11]
+    bz = S_T + 4
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(d)))                   # Y == 0
+    a("v_cndmask_b32_e64 %s, %s, 1, %s" % (v(d), v(d), sp(z)))
+    lab = exec_begin(a, z, S_T)
+    moves(a, X, [None] * 8)
+    exec_end(a, lab, S_T)
+    a("v_ffbh_u32 %s, %s" % (v(b), v(d)))                              # d >= 1: 0..31
+    a("v_lshlrev_b32 %s, %s, %s" % (v(d), v(b), v(d)))
+    a("v_sub_u32 %s, 32, %s" % (v(c), v(b)))
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(bz), v(b)))
+    a("v_mov_b32 %s, 0" % v(R[0]))
+    bitshift_left(a, X + [R[0]], c, bz, 9, S_T)                       # u = X << b
+    _reciprocal(a, d, dinv)
+    a("v_mov_b32 %s, %s" % (v(r), v(R[0])))                           # r = u[8] < d
+    lt = sp(S_T + 2)
+    for j in reversed(range(8)):
+        # (A1:A0) = dinv * r + (r:u[j]); q = A1 + 1; r' = u[j] - q * d
+        a("v_mov_b32 %s, %s" % (v(A0), v(X[j])))
+        a("v_mov_b32 %s, %s" % (v(A1), v(r)))
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (A0, A1, sp(S_T + 6), v(dinv), v(r),
+                                                           A0, A1))
+        a("v_add_u32 %s, 1, %s" % (v(QH), v(A1)))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(P0), v(QH), v(d)))
+        a("v_sub_u32 %s, %s, %s" % (v(CR), v(X[j]), v(P0)))
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (lt, v(CR), v(A0)))           # r' > q0: q--, r' += d
+        a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(QH), sp(S_T + 4), v(QH), lt))
+        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), lt))
+        a("v_add_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
+        a("v_cmp_ge_u32_e64 %s, %s, %s" % (lt, v(CR), v(d)))            # r' >= d: q++, r' -= d
+        a("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (v(R[j]), sp(S_T + 4), v(QH), lt))
+        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), lt))
+        a("v_sub_u32 %s, %s, %s" % (v(r), v(CR), v(P0)))
+    if want_rem:
+        a("v_lshrrev_b32 %s, %s, %s" % (v(X[0]), v(b), v(r)))
+        moves(a, X[1:], [None] * 7)
+
+
+def _reciprocal(a: Asm, d: int, dinv: int):
+    """v[dinv] = floor((2^64-1)/d) - 2^32 for a normalised divisor v[d]
+    (d >= 2^31) in every lane: f64 reciprocal, one Newton step (the estimate
+    is then within one of the exact value), then one exact integer
+    correction in each direction.  Clobbers T4..T9, s[S_T..S_T+7], vcc."""
     f0, f1, fe = T[4], T[6], T[8]
     a("v_cvt_f64_u32_e32 %s, %s" % (vp(f0), v(d)))
     a("v_rcp_f64_e32 %s, %s" % (vp(f1), vp(f0)))
@@ -2010,23 +2094,6 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 2)))
     a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(S_T + 6)))
     a("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), sp(S_T)))
-    a("v_mov_b32 %s, 0" % v(T[9]))                                  # RH of the digit loop
-    for j in reversed(range(8)):
-        u2, u1 = un[j + 8], un[j + 7]
-        skip = a.uniq("dvs")
-        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(u2)))
-        a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(u1), v(d)))
-        a("s_or_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 2)))
-        a("s_cbranch_vccz %s" % skip)
-        _div_digit(a, un, vn, j, d, dinv)
-        a.label(skip)
-    if want_rem:
-        # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
-        a("v_mov_b32 %s, 0" % v(T[0]))
-        t = X + [T[0]]
-        for st in (1, 2, 4):
-            _stage(a, t, st, 9, False, DIV_M[st])
-        bitshift_right(a, t, b, 8)
 
 
 def _div_digit(a: Asm, un, vn, j, d, dinv):

@@ -270,6 +270,26 @@ def division_case():
     return constraints, probes, gen
 
 
+def division_one_limb_case():
+    """All five division operators with divisors that fit 32 bits in every
+    lane (y & 0xffffffff and its negation): every wave takes the short
+    division (asmgen._udivrem_short; the negated divisor only for the signed
+    operators)."""
+    x, y = N.bv_var("sx", 256), N.bv_var("sy", 256)
+    d = N.bv_op("bvand", y, N.bv_num(0xFFFFFFFF, 256))
+    nd = N.bv_op("bvsub", N.bv_num(0, 256), d)
+    probes = [N.bv_op(op, x, dv) for dv in (d, nd)
+              for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    constraints = [N.bv_cmp("bvult", probes[1], N.bv_op("bvadd", d, N.bv_num(1, 256)))]
+
+    def gen(rng):
+        dv = rng.choice([0, 1, 3, 1 << 31, (1 << 32) - 1, rng.getrandbits(rng.choice((8, 31, 32)))])
+        xv = rng.choice([0, (1 << 256) - 1, 1 << 255, rng.getrandbits(256),
+                         rng.getrandbits(rng.randrange(1, 256))])
+        return Assignment(vars={"sx": xv, "sy": dv | (rng.getrandbits(224) << 32)})
+    return constraints, probes, gen
+
+
 def const_shift_case(w: int):
     """Shifts by constants and unsigned division / remainder by powers of
     two (the forms EVM SHR/SHL/SAR/DIV/MOD by 2^k take), lowered to
@@ -306,6 +326,8 @@ def named_cases():
     out["overflow"] = (c, p, g, {})
     c, p, g = division_case()
     out["division_hard"] = (c, p, g, {})
+    c, p, g = division_one_limb_case()
+    out["division_one_limb"] = (c, p, g, {})
     for w in (8, 160, 256):
         c, p, g = const_shift_case(w)
         out["const_shift_w%d" % w] = (c, p, g, {})
