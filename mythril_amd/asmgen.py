@@ -1900,6 +1900,9 @@ def shift_core(a: Asm, kind: str, fa: int, fb: int, fw: int, masked: bool):
 DIV_BITS_FIRST = os.environ.get("MYTHGPU_DIV_BITS_FIRST", "1") != "0"
 DIV_M = {4: 48, 2: 50, 1: 52}   # limb-shift stage masks (bank B: free in heavy bodies)
 DIV_Z6 = 54                     # lanes with vn[0..5] == 0 (bank B)
+# limb-barrel stages this long get a branch over an empty lane mask (A/B
+# knob: MYTHGPU_DIV_STAGE_SKIP=99 never branches, the round-3 code)
+DIV_STAGE_SKIP = int(os.environ.get("MYTHGPU_DIV_STAGE_SKIP", "6"))
 DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm:
                                 # unused by division)
 
@@ -1907,8 +1910,12 @@ DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
            live: Optional[int] = None) -> int:
     """One limb-barrel stage: shift t by st limbs in the lanes of s[mask]
-    (under exec; zero fill).  Returns the new number of live low limbs."""
-    lab = exec_begin(a, mask, S_T + 2)
+    (under exec; zero fill).  Returns the new number of live low limbs.
+    Stages of at least DIV_STAGE_SKIP limbs branch over an empty mask (a
+    wave of full-width divisors — every uniform-class divisor leaf under
+    generator v8 — needs none of them)."""
+    n = min(nl, (nl if live is None else live) + st) if left else nl
+    lab = exec_begin(a, mask, S_T + 2, skip=n >= DIV_STAGE_SKIP)
     if left:
         hi = nl if live is None else live
         top = min(nl, hi + st)

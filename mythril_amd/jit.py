@@ -1201,7 +1201,8 @@ def source_digest() -> str:
                     h.update(f.encode() + fh.read())
     from . import ir
     knobs = {"coalesce": COALESCE, "flush": COLD_FLUSH, "asm": G.digest(),
-             "div_bits_first": G.DIV_BITS_FIRST, "probe": G._PROBE,
+             "div_bits_first": G.DIV_BITS_FIRST, "div_stage_skip": G.DIV_STAGE_SKIP,
+             "probe": G._PROBE,
              "leaf_remat": ir.LEAF_REMAT, "keep_clean": ir.KEEP_CLEAN}
     h.update(repr(sorted(knobs.items())).encode())
     return h.hexdigest()[:16]
