@@ -1160,8 +1160,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     per group of 64 consecutive indices, so when every active lane of the
     wave is in one group — every wave of a launch that starts at a multiple
     of 64: all search and bench launches — the class is wave-uniform and
-    only its own code runs (branch on the scalar class).  A wave across
-    two groups (an unaligned eval) runs the two classes in turn.
+    only its own code runs (branch on the scalar class, computed in SALU
+    from the first active lane's index).  A wave across two groups (an
+    unaligned eval) draws per lane and runs the two classes in turn.
     Device descriptor (8 words at gen + 32*leaf): width, pool_off (bytes),
     pool_n, pct_uniform, pct_small, pct_boundary, salt_lo, salt_hi.  A
     LEAFD (``in_record``: 256 bits) finds them in its own record instead
@@ -1195,30 +1196,36 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), OP_IDX_LO))
     a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), OP_IDX_HI))
     # v8 class: cls = mulhi(((lo32(idx >> 6) ^ lo32(ss)) * CLS_MUL) ^ hi32(ss), 100)
-    a("v_alignbit_b32 %s, %s, %s, 6" % (v(cls), OP_IDX_HI, OP_IDX_LO))
-    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T), v(cls)))
-    a("s_mov_b32 %s, 0x%x" % (s(S_T + 2), CLS_MUL))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(cls), s(S_T + 2)))
-    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T + 1), v(cls)))
-    a("s_movk_i32 %s, 100" % s(S_T + 2))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(S_T + 2)))
-    sm64(a, st, z, tt)
-    dst = X if dst is None else dst
-    # waterfall over the wave's distinct class draws: exec = the lanes whose
-    # draw equals the first active lane's, run that class's code, repeat
-    # with the rest.  A wave of consecutive indices spans at most two
-    # groups; a launch from a multiple of 64 is one pass (the common path:
-    # ~8 SALU + 2 VALU over the class's own code).
+    # When the first active lane's index is a multiple of 64 every active
+    # lane is in its group (a wave's indices are consecutive): the class is
+    # computed once, in SALU, from that index.  Otherwise (out of line) per
+    # lane, and a waterfall runs each distinct class of the wave in turn:
+    # exec = the lanes whose draw equals the first active lane's, that
+    # class's code, repeat with the rest (a wave of consecutive indices spans
+    # at most two groups).
     sc, rest, save = S_T + 2, S_T + 4, S_X          # (division's lane masks: free here)
-    lab_loop, lab_again = a.uniq("gcls"), a.uniq("gagain")
+    lab_slow, lab_join, lab_loop, lab_again = (a.uniq("gslow"), a.uniq("gjoin"), a.uniq("gcls"),
+                                               a.uniq("gagain"))
+    lab_disp = a.uniq("gdisp")
     lab_uni, lab_small, lab_bnd, lab_done = (a.uniq("guni"), a.uniq("gsml"), a.uniq("gbnd"),
                                              a.uniq("gdone"))
+    a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
+    a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
+    a("s_and_b32 %s, %s, 63" % (s(rest), s(sc)))
+    a("s_cbranch_scc1 %s" % lab_slow)
+    a("s_lshr_b64 %s, %s, 6" % (sp(sc), sp(sc)))
+    a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T)))
+    a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
+    a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
+    a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
+    a("s_mov_b64 %s, 0" % sp(rest))                 # one pass: no lanes left after it
+    a.label(lab_join)
+    sm64(a, st, z, tt)
+    dst = X if dst is None else dst
     a("s_mov_b64 %s, exec" % sp(save))
-    a.label(lab_loop)
-    a("v_readfirstlane_b32 %s, %s" % (s(sc), v(cls)))
-    a("v_cmp_eq_u32 vcc, %s, %s" % (s(sc), v(cls)))
-    a("s_and_saveexec_b64 %s, vcc" % sp(rest))
-    a("s_andn2_b64 %s, %s, exec" % (sp(rest), sp(rest)))   # lanes still to do
+    a("s_cmp_lg_u64 %s, 0" % sp(rest))
+    a("s_cbranch_scc1 %s" % lab_loop)                # per-lane classes: the waterfall
+    a.label(lab_disp)
     a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["pu"])))
     a("s_cbranch_scc1 %s" % lab_uni)                 # cls < pct_uniform
     a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["ps"])))
@@ -1245,6 +1252,24 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     if wait:
         a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
     a.cold()
+    # per-lane class draws (ss still in s[S_T:S_T+1]); rest != 0 sends the
+    # join to the waterfall
+    a.label(lab_slow)
+    a("v_alignbit_b32 %s, %s, %s, 6" % (v(cls), OP_IDX_HI, OP_IDX_LO))
+    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T), v(cls)))
+    a("s_mov_b32 %s, 0x%x" % (s(sc), CLS_MUL))
+    a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
+    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T + 1), v(cls)))
+    a("s_movk_i32 %s, 100" % s(sc))
+    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
+    a("s_mov_b64 %s, -1" % sp(rest))
+    a("s_branch %s" % lab_join)
+    a.label(lab_loop)
+    a("v_readfirstlane_b32 %s, %s" % (s(sc), v(cls)))
+    a("v_cmp_eq_u32 vcc, %s, %s" % (s(sc), v(cls)))
+    a("s_and_saveexec_b64 %s, vcc" % sp(rest))
+    a("s_andn2_b64 %s, %s, exec" % (sp(rest), sp(rest)))   # lanes still to do
+    a("s_branch %s" % lab_disp)
     # another group in this wave: its loads are in flight into other lanes
     # of dst; settle them before the next class writes dst
     a.label(lab_again)
@@ -2396,8 +2421,14 @@ def generate() -> List[str]:
             for bank in (0, 1):
                 a.label(".Lh%d_%%=" % hid(aop, var, bank))
                 emit_handler(a, name, var, bank)
-    body_umulno(a)
-    body_div(a)
+        # a shared body right after the stubs that branch to it (s_branch
+        # reaches +-128 KB; at the end of the handlers the division body was
+        # within 3 % of that from its first stub); handlers end in a
+        # dispatch, so nothing falls into a body
+        if name == "SMOD":
+            body_div(a)
+        elif name == "UMULNO":
+            body_umulno(a)
     a.label(".Lexit_%=")
     a("s_set_gpr_idx_off")
     a("s_mov_b32 m0, %s" % s(S_M0))

@@ -364,6 +364,9 @@ class Wave:
         # S1[4:0] = offset, S1[22:16] = width
         self._sop2(a, lambda x, y: (x >> (y & 31)) & ((1 << ((y >> 16) & 0x7F)) - 1))
 
+    def i_s_xor_b32(self, a, pc):
+        self._sop2(a, lambda x, y: x ^ y)
+
     def i_s_and_b64(self, a, pc):
         self._sop2(a, lambda x, y: x & y, 64)
 
@@ -393,6 +396,12 @@ class Wave:
 
     def i_s_lshr_b32(self, a, pc):
         self._sop2(a, lambda x, y: x >> (y & 31))
+
+    def i_s_lshr_b64(self, a, pc):
+        x, y = self.sread(a[1], 64), self.sread(a[2])
+        r = x >> (y & 63)
+        self.swrite(a[0], r)
+        self.scc = int(r != 0)
 
     def i_s_lshl_b64(self, a, pc):
         x, y = self.sread(a[1], 64), self.sread(a[2])
