@@ -1056,6 +1056,9 @@ GOLD = 0x9E3779B97F4A7C15
 MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
 PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
 CLS_MUL = 0x2545F491                              # class remix (generator v7/v8)
+# the wave's class in SALU when its first active index starts a 64-group
+# (A/B knob: MYTHGPU_GEN_SALU_CLASS=0 draws per lane in every wave)
+GEN_SALU_CLASS = os.environ.get("MYTHGPU_GEN_SALU_CLASS", "1") != "0"
 # SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
 S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
@@ -1209,16 +1212,31 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     lab_disp = a.uniq("gdisp")
     lab_uni, lab_small, lab_bnd, lab_done = (a.uniq("guni"), a.uniq("gsml"), a.uniq("gbnd"),
                                              a.uniq("gdone"))
-    a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
-    a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
-    a("s_and_b32 %s, %s, 63" % (s(rest), s(sc)))
-    a("s_cbranch_scc1 %s" % lab_slow)
-    a("s_lshr_b64 %s, %s, 6" % (sp(sc), sp(sc)))
-    a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T)))
-    a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
-    a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
-    a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
-    a("s_mov_b64 %s, 0" % sp(rest))                 # one pass: no lanes left after it
+    def lane_class():
+        # per-lane class draws (ss still in s[S_T:S_T+1]); rest != 0 sends
+        # the join to the waterfall
+        a("v_alignbit_b32 %s, %s, %s, 6" % (v(cls), OP_IDX_HI, OP_IDX_LO))
+        a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T), v(cls)))
+        a("s_mov_b32 %s, 0x%x" % (s(sc), CLS_MUL))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
+        a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T + 1), v(cls)))
+        a("s_movk_i32 %s, 100" % s(sc))
+        a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
+        a("s_mov_b64 %s, -1" % sp(rest))
+
+    if GEN_SALU_CLASS:
+        a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
+        a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
+        a("s_and_b32 %s, %s, 63" % (s(rest), s(sc)))
+        a("s_cbranch_scc1 %s" % lab_slow)
+        a("s_lshr_b64 %s, %s, 6" % (sp(sc), sp(sc)))
+        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T)))
+        a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
+        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
+        a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
+        a("s_mov_b64 %s, 0" % sp(rest))             # one pass: no lanes left after it
+    else:
+        lane_class()
     a.label(lab_join)
     sm64(a, st, z, tt)
     dst = X if dst is None else dst
@@ -1252,18 +1270,10 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     if wait:
         a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
     a.cold()
-    # per-lane class draws (ss still in s[S_T:S_T+1]); rest != 0 sends the
-    # join to the waterfall
-    a.label(lab_slow)
-    a("v_alignbit_b32 %s, %s, %s, 6" % (v(cls), OP_IDX_HI, OP_IDX_LO))
-    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T), v(cls)))
-    a("s_mov_b32 %s, 0x%x" % (s(sc), CLS_MUL))
-    a("v_mul_lo_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
-    a("v_xor_b32 %s, %s, %s" % (v(cls), s(S_T + 1), v(cls)))
-    a("s_movk_i32 %s, 100" % s(sc))
-    a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
-    a("s_mov_b64 %s, -1" % sp(rest))
-    a("s_branch %s" % lab_join)
+    if GEN_SALU_CLASS:
+        a.label(lab_slow)
+        lane_class()
+        a("s_branch %s" % lab_join)
     a.label(lab_loop)
     a("v_readfirstlane_b32 %s, %s" % (s(sc), v(cls)))
     a("v_cmp_eq_u32 vcc, %s, %s" % (s(sc), v(cls)))
