@@ -111,6 +111,36 @@ def test_division_one_limb_waves(rep):
         assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
 
 
+@pytest.mark.parametrize("small", ["y", "x", "both", "none"])
+def test_mul_short_operand_waves(small):
+    """MUL where one operand is below 2^64 in every lane takes the two-row
+    product (asmgen.h_mul): either side, both, and a wave where the check
+    fails (one lane wide), against the oracle at several widths."""
+    rng = random.Random(len(small))
+    for w in (256, 160, 64):
+        x, y = N.bv_var("x", w), N.bv_var("y", w)
+        probes = [N.bv_op("bvmul", x, y), N.bv_op("bvmul", y, x)]
+        prog = compile_constraints([], probes)
+        M = (1 << w) - 1
+        asgs = []
+        for lane in range(64):
+            xv, yv = rng.getrandbits(w), rng.getrandbits(w)
+            if small in ("x", "both"):
+                xv = rng.choice([0, 1, (1 << 64) - 1, rng.getrandbits(64), rng.getrandbits(33)])
+            if small in ("y", "both"):
+                yv = rng.choice([0, 1, (1 << 64) - 1, rng.getrandbits(64), rng.getrandbits(32)])
+            if small == "none" and lane == 17:
+                xv, yv = M, M
+            elif small == "none":
+                yv = rng.getrandbits(60)
+            asgs.append(PA(vars={"x": xv & M, "y": yv & M}))
+        root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+        for a, asg in enumerate(asgs):
+            want = R.evaluate(probes, R.Assignment(asg.vars))
+            got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+            assert got == want, (small, w, a)
+
+
 @pytest.mark.parametrize("spans", [(1, 33, 64), (65, 100, 128), (1, 64, 128), (1, 64, 256)])
 def test_division_short_divisor_chains(spans):
     """Waves whose divisors span few digits (any position, after
