@@ -1668,20 +1668,18 @@ def col_product(a: Asm, x: List[int], y: List[int], ncols: int, out: Optional[Li
             a("v_pk_mov_b32 v[%d:%d], v[%d:%d], v[%d:%d] op_sel:[1,0]" % (A0, A1, A0, A1, A2, A2 + 1))
 
 
-def low_product(a: Asm, x: List[int], y: List[int], out: List[int], ny: int = 8):
+def low_product(a: Asm, x: List[int], y: List[int], out: List[int]):
     """out[0..7] = (x*y) mod 2^256 by product scanning, with the column
     accumulator placed so no digit needs a copy on even columns: column c
     even accumulates in the aligned pair (out[c], out[c+1]) (the digit stays
     in out[c]), column c odd in (A0, A1) with its digit copied to out[c]; one
     v_pk_mov_b32 per column moves (high word, carry word) on.  Column 0's
     single product cannot carry; the carries of column 6 would only reach
-    column 8, so they are not tracked.  ``ny`` < 8: y's limbs from ny up are
-    zero in every lane (only the terms with y[0..ny-1] are formed).  Uses
-    T4..T6, vcc, s[S_T+6:S_T+7]."""
+    column 8, so they are not tracked.  Uses T4..T6, vcc, s[S_T+6:S_T+7]."""
     A0, A1, A2 = T[4], T[5], T[6]
     for c in range(8):
         pair = (out[c], out[c + 1]) if c % 2 == 0 else (A0, A1)
-        for n, i in enumerate(range(max(0, c - ny + 1), c + 1)):
+        for n, i in enumerate(range(0, c + 1)):
             add = "0" if c == 0 else "v[%d:%d]" % pair
             a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, %s" % (
                 pair[0], pair[1], sp(S_T + 6), v(x[i]), v(y[c - i]), add))
@@ -1698,11 +1696,6 @@ def low_product(a: Asm, x: List[int], y: List[int], out: List[int], ny: int = 8)
                 A0, A1, out[c], out[c + 1], "0" if c == 0 else "v[%d:%d]" % (A2, A2 + 1)))
 
 
-# MUL with an operand below 2^64 in every lane takes two limb rows (A/B
-# knob: MYTHGPU_MUL_SHORT=0 always forms the full low product)
-MUL_SHORT = os.environ.get("MYTHGPU_MUL_SHORT", "1") != "0"
-
-
 def h_mul(a, bank, root, mask, dc=False, w32=False, ip=False):
     """MUL in line in each (variant, bank) handler, unlike the other heavy
     ops: no record copy, no branch to a shared body, no run-time variant
@@ -1712,32 +1705,8 @@ def h_mul(a, bank, root, mask, dc=False, w32=False, ip=False):
         load_masks(a, fld(bank, F_MOFF))
     a.read_slot(X, fld(bank, F_A))
     a.read_slot(Y, fld(bank, F_B))
-    # an operand below 2^64 in every active lane (41 % of the C2 corpus's
-    # MUL waves under generator v8): two limb rows, out of line
-    if not MUL_SHORT:
-        low_product(a, X, Y, R)
-        finish(a, bank, R, root, mask)
-        return
-    lab_ys, lab_xs, lab_fin = a.uniq("mys"), a.uniq("mxs"), a.uniq("mfin")
-    t = T[4]
-    for opnd, lab in ((Y, lab_ys), (X, lab_xs)):
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(opnd[2]), v(opnd[3]), v(opnd[4])))
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(opnd[5]), v(opnd[6])))
-        a("v_or_b32 %s, %s, %s" % (v(t), v(t), v(opnd[7])))
-        a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
-        a("s_cmp_eq_u64 vcc, exec")
-        a("s_cbranch_scc1 %s" % lab)
     low_product(a, X, Y, R)
-    a.label(lab_fin)
     finish(a, bank, R, root, mask)
-    a.cold()
-    a.label(lab_ys)
-    low_product(a, X, Y, R, ny=2)
-    a("s_branch %s" % lab_fin)
-    a.label(lab_xs)
-    low_product(a, Y, X, R, ny=2)
-    a("s_branch %s" % lab_fin)
-    a.hot()
 
 
 def clz256(a: Asm, vals: List[int], out: int, t: List[int]):

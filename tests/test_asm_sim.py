@@ -113,9 +113,9 @@ def test_division_one_limb_waves(rep):
 
 @pytest.mark.parametrize("small", ["y", "x", "both", "none"])
 def test_mul_short_operand_waves(small):
-    """MUL where one operand is below 2^64 in every lane takes the two-row
-    product (asmgen.h_mul): either side, both, and a wave where the check
-    fails (one lane wide), against the oracle at several widths."""
+    """MUL waves whose operands are below 2^64 in every lane (either side,
+    both, or all but one lane) against the oracle at several widths (round
+    4 measured a two-row product for such waves and dropped it)."""
     rng = random.Random(len(small))
     for w in (256, 160, 64):
         x, y = N.bv_var("x", w), N.bv_var("y", w)
