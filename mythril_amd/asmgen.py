@@ -126,11 +126,18 @@ SLOT_VARIANT = {"LEAFD", "RELOADD", "SPILL_LDS", "SPILL_SCR", "RELOAD_LDS"}
 # LEAFD / RELOADD: variant = slot | WAITD when the handler waits for its own
 # loads (its consumer is the very next record; the translator folds the wait)
 V_WAITD = 16
+# SPILL_SCR / RELOADD: the value is one limb (limbs 1..7 zero): one dword of
+# scratch instead of eight (the translator decides at the spill)
+V_NARROW = 32
 
 
 def canon_var(name: str, var: int) -> int:
-    if name in ("LEAFD", "RELOADD"):
+    if name == "LEAFD":
         return var & (V_WAITD | 15) if (var & 15) < NREG else 0
+    if name == "RELOADD":
+        return var & (V_NARROW | V_WAITD | 15) if (var & 15) < NREG else 0
+    if name == "SPILL_SCR":
+        return var & (V_NARROW | 15) if (var & 15) < NREG else 0
     if name in SLOT_VARIANT:
         return var if var < NREG else 0      # the variant is the register slot
     if name == "EXTRACTN":
@@ -957,13 +964,17 @@ def h_reload_lds(a: Asm, bank: int, slot: int):
     dispatch(a, 1 - bank)
 
 
-def h_spill_scr(a: Asm, bank: int, slot: int):
-    """Scratch spill straight from slot ``slot`` (the variant)."""
-    fa = FB + 8 * slot
+def h_spill_scr(a: Asm, bank: int, var: int):
+    """Scratch spill straight from slot ``var & 15``; NARROW: a one-limb
+    value, one dword (its RELOADD zeroes limbs 1..7)."""
+    fa = FB + 8 * (var & 15)
     prologue(a, bank)
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
-    a("scratch_store_dwordx4 off, v[%d:%d], %s" % (fa, fa + 3, s(S_T)))
-    a("scratch_store_dwordx4 off, v[%d:%d], %s offset:16" % (fa + 4, fa + 7, s(S_T)))
+    if var & V_NARROW:
+        a("scratch_store_dword off, v%d, %s" % (fa, s(S_T)))
+    else:
+        a("scratch_store_dwordx4 off, v[%d:%d], %s" % (fa, fa + 3, s(S_T)))
+        a("scratch_store_dwordx4 off, v[%d:%d], %s offset:16" % (fa + 4, fa + 7, s(S_T)))
     dispatch(a, 1 - bank)
 
 
@@ -1363,8 +1374,12 @@ def h_reloadd(a: Asm, bank: int, var: int):
     fd = FB + 8 * (var & 15)
     prologue(a, bank)
     a("s_add_u32 %s, %s, %s" % (s(S_T), IN["scr"], s(fld(bank, F_IMM))))
-    a("scratch_load_dwordx4 v[%d:%d], off, %s" % (fd, fd + 3, s(S_T)))
-    a("scratch_load_dwordx4 v[%d:%d], off, %s offset:16" % (fd + 4, fd + 7, s(S_T)))
+    if var & V_NARROW:                 # one dword; limbs 1..7 of a one-limb value
+        a("scratch_load_dword v%d, off, %s" % (fd, s(S_T)))
+        moves(a, [fd + j for j in range(1, 8)], [None] * 7)
+    else:
+        a("scratch_load_dwordx4 v[%d:%d], off, %s" % (fd, fd + 3, s(S_T)))
+        a("scratch_load_dwordx4 v[%d:%d], off, %s offset:16" % (fd + 4, fd + 7, s(S_T)))
     _wait_if_flagged(a, var)
     dispatch(a, 1 - bank)
 
@@ -2539,6 +2554,7 @@ def write_outputs(csrc: str) -> None:
            "#define MGA_V_DC %d" % V_DC, "#define MGA_V_W32 %d" % V_W32,
            "#define MGA_V_IP %d" % V_IP, "#define MGA_V_NW %d" % V_NW,
            "#define MGA_V_WAITD %d" % V_WAITD,
+           "#define MGA_V_NARROW %d" % V_NARROW,
            "#define MGA_V_NEG %d" % V_NEG, "#define MGA_V_GEN %d" % V_GEN,
            "#define MGA_HID(aop, var, bank) ((((aop) * MGA_NVAR) + (var)) * 2 + (bank))",
            "#define MGA_FB %d" % FB, "#define MGA_NREG %d" % NREG,

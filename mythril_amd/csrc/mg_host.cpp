@@ -112,6 +112,17 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
     // at most 32 bits); registers start uninitialised
     bool clean[MG_NREG];
     for (int k = 0; k < MG_NREG; ++k) clean[k] = false;
+    // narrow_spill[s]: scratch spill slot s holds a one-limb value (limb 0
+    // stored only; its reloads zero limbs 1..7).  A reload never moves above
+    // the spill of its slot (the hoisting below), so the flag is set first.
+    // (slots past 2^16, which no validated program has, stay wide)
+    std::vector<char> narrow_spill;
+    auto set_narrow = [&](uint32_t k, bool v) {
+        if (k >= (1u << 16)) return;
+        if (k >= narrow_spill.size()) narrow_spill.resize(k + 1, 0);
+        narrow_spill[k] = v;
+    };
+    auto is_narrow = [&](uint32_t k) { return k < narrow_spill.size() && narrow_spill[k]; };
     // slots whose LEAFD loads may still be in flight: a WAITVM record goes
     // before the first instruction that reads or writes one of them
     uint32_t pending = 0;
@@ -229,11 +240,23 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             break;
         case MG_SPILL:              // spills and reloads: the variant is the slot
             if (imm < n_lds) { aop = MGA_SPILL_LDS; var = a; r[5] = imm * 2u * 256u * 16u; }
-            else { aop = MGA_SPILL_SCR; var = a; r[5] = (imm - n_lds) * 32u; }
+            else {                  // a one-limb value: one dword of scratch traffic
+                aop = MGA_SPILL_SCR; var = a; r[5] = (imm - n_lds) * 32u;
+#ifdef MG_NO_NARROW_SPILL                   /* A/B builds: every spill eight dwords */
+                const bool nf = false;
+#else
+                const bool nf = clean[a] && imm - n_lds < (1u << 16);
+#endif
+                set_narrow(imm - n_lds, nf);
+                if (nf) var |= MGA_V_NARROW;
+            }
             break;
         case MG_RELOAD:
             if (imm < n_lds) { aop = MGA_RELOAD_LDS; var = d; r[5] = imm * 2u * 256u * 16u; }
-            else { aop = MGA_RELOADD; var = d; r[5] = (imm - n_lds) * 32u; }
+            else {
+                aop = MGA_RELOADD; var = d; r[5] = (imm - n_lds) * 32u;
+                if (is_narrow(imm - n_lds)) var |= MGA_V_NARROW;
+            }
             break;
         case MG_ADD: aop = MGA_ADD; goto masked;
         case MG_SUB: aop = MGA_SUB; goto masked;

@@ -812,32 +812,44 @@ class Wave:
             if act[l]:
                 self.mem.write32(addrs[l], int(data[l]))
 
-    def i_scratch_store_dwordx4(self, a, pc):
+    def _scratch_store(self, a, n):
         if a[0] != "off":
             raise SimError("scratch: vaddr form not modelled")
-        src, n = self.vidx(a[1], None, False)
+        src, _ = self.vidx(a[1], None, False)
         off = self.sread(a[2]) + (self._soff(a[3]) if len(a) > 3 else 0)
         act = self._act()
         for l in range(NL):
             if act[l]:
-                if off + 16 > len(self.scratch[l]):
+                if off + 4 * n > len(self.scratch[l]):
                     raise SimError("scratch out of bounds")
-                for i in range(4):
+                for i in range(n):
                     self._check(("v", src + i))
                     struct.pack_into("<I", self.scratch[l], off + 4 * i, int(self.v[src + i][l]))
 
-    def i_scratch_load_dwordx4(self, a, pc):
-        dst, n = self.vidx(a[0], None, False)
+    def _scratch_load(self, a, n):
+        dst, _ = self.vidx(a[0], None, False)
         if a[1] != "off":
             raise SimError("scratch: vaddr form not modelled")
         off = self.sread(a[2]) + (self._soff(a[3]) if len(a) > 3 else 0)
         act = self._act()
         vals = [[struct.unpack_from("<I", self.scratch[l], off + 4 * i)[0] for l in range(NL)]
-                for i in range(4)]
-        for i in range(4):
+                for i in range(n)]
+        for i in range(n):
             def apply(i=i):
                 self.v[dst + i] = np.where(act, np.array(vals[i], dtype=np.uint64), self.v[dst + i])
             self._defer("vm", ("v", dst + i), apply)
+
+    def i_scratch_store_dwordx4(self, a, pc):
+        self._scratch_store(a, 4)
+
+    def i_scratch_store_dword(self, a, pc):
+        self._scratch_store(a, 1)
+
+    def i_scratch_load_dwordx4(self, a, pc):
+        self._scratch_load(a, 4)
+
+    def i_scratch_load_dword(self, a, pc):
+        self._scratch_load(a, 1)
 
     def i_ds_write_b128(self, a, pc):
         addr = self.vread(a[0], valu=False)
