@@ -73,13 +73,18 @@ def default_units(workload):
     return {"c2": 4096, "c5": 2 * STREAM_QUERIES}.get(workload, STREAM_QUERIES)
 
 
+# leaf policy of the eval-mode batch compile: per program ("auto",
+# ir.AUTO_SCRATCH_SHARE) unless MYTHRIL_GPU_LEAF_REMAT names one
+BENCH_REMAT = os.environ.get("MYTHRIL_GPU_LEAF_REMAT", "auto")
+
+
 def compile_unit(item):
     """(workload, dag_id) -> (dag_id, Program, node count, int32-op weight)."""
     from mythril_amd.ir import compile_constraints
     from mythril_amd.roofline import dag_work
     workload, dag_id = item
     roots = workload_roots(workload, dag_id)
-    prog = compile_constraints(roots)
+    prog = compile_constraints(roots, leaf_remat=BENCH_REMAT)
     nodes, weight = dag_work(roots, prog.table_sizes)
     return dag_id, prog, nodes, weight
 
@@ -116,7 +121,7 @@ def kernel_key(lib_digest, workload, dags, assign_log2, jit, corpus=None):
     workload and the programs evaluated (``programs_digest``).  bench.py
     reports ``traffic`` only when every field matches."""
     from mythril_amd import ir
-    key = {"asm_digest": lib_digest, "leaf_remat": ir.LEAF_REMAT, "jit": bool(jit),
+    key = {"asm_digest": lib_digest, "leaf_remat": BENCH_REMAT, "jit": bool(jit),
            "workload": workload, "dags": dags, "assign_log2": assign_log2}
     if corpus is not None:
         key["programs"] = programs_digest(corpus)

@@ -1087,22 +1087,59 @@ def lw_tables(constraints, probes) -> set:
 COMPILER = _os.environ.get("MYTHRIL_GPU_COMPILER", "native")
 
 
+# "auto" (the eval-mode batch path, bench.compile_unit): a program whose
+# 256-bit scratch-tier reloads exceed this share of its instructions under
+# scratch2 is compiled again under "scratch" (leaves never take a scratch
+# slot: regenerated instead).  Round 4, after one-dword narrow spills: C3 /
+# C4 run 3.3 / 2.6 % faster under "scratch" (their spills are HBM-bound),
+# C2 1.1 % slower (VALU-bound: regeneration costs more than the traffic);
+# per program the share is at most 1.8 % on the C2 corpus and a median
+# 4.1 / 2.0 / 1.8 % on C3 / C4 / C5 (profiles/r04/remat_r4r/, remat_c2_r4/).
+AUTO_SCRATCH_SHARE = 0.02
+
+
+def scratch_reload_share(p: Program, lds_tier: int = LDS_TIER) -> float:
+    """256-bit reloads from per-lane scratch slots (spill slot index at or
+    above the kernel's LDS tier) per instruction of ``p``."""
+    code = p.code
+    if not len(code):
+        return 0.0
+    op = code[:, 0] & 0xFF
+    width = (code[:, 0] >> 8) & 0x3FF
+    hit = (op == I.RELOAD) & (width > 32) & (code[:, 2] >= lds_tier)
+    return float(hit.sum()) / len(code)
+
+
 def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = (),
                         table_sizes: Optional[Dict[str, int]] = None,
                         default_entries: int = 2, nreg: int = I.NREG,
                         extra_consts: Sequence[int] = (), leaf_pools: bool = False,
                         const_keys: bool = False, solve: bool = False, search_hints: bool = False,
-                        abi_presets: bool = False) -> Program:
+                        abi_presets: bool = False, leaf_remat: Optional[str] = None) -> Program:
     """Compile constraints (see :func:`compile_constraints_py`) with the
-    compiler ``COMPILER`` names."""
+    compiler ``COMPILER`` names, under the leaf policy ``leaf_remat``
+    (default ``LEAF_REMAT``; "auto": see ``AUTO_SCRATCH_SHARE``)."""
+    global LEAF_REMAT
+    policy = leaf_remat or LEAF_REMAT
+    if policy == "auto":
+        args = (constraints, probes, table_sizes, default_entries, nreg, extra_consts,
+                leaf_pools, const_keys, solve, search_hints, abi_presets)
+        p = compile_constraints(*args, leaf_remat="scratch2")
+        if scratch_reload_share(p) > AUTO_SCRATCH_SHARE:
+            p = compile_constraints(*args, leaf_remat="scratch")
+        return p
     if COMPILER == "py":
-        return compile_constraints_py(constraints, probes, table_sizes, default_entries, nreg,
-                                      extra_consts, leaf_pools, const_keys, solve, search_hints,
-                                      abi_presets)
+        saved, LEAF_REMAT = LEAF_REMAT, policy
+        try:
+            return compile_constraints_py(constraints, probes, table_sizes, default_entries, nreg,
+                                          extra_consts, leaf_pools, const_keys, solve, search_hints,
+                                          abi_presets)
+        finally:
+            LEAF_REMAT = saved
     from .ccompile import compile_native
     return compile_native(constraints, probes, table_sizes, default_entries, nreg, extra_consts,
-                          leaf_pools, const_keys, solve, search_hints=search_hints,
-                          abi_presets=abi_presets)
+                          leaf_pools, const_keys, solve, leaf_remat=policy,
+                          search_hints=search_hints, abi_presets=abi_presets)
 
 
 def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] = (),

@@ -198,3 +198,22 @@ def test_corpus_dag_with_leaf_pools_through_ir(dag_id):
         asg = to_oracle(prog, lv)
         root, _ = ir_sim.run(prog, lv)
         assert root == R.eval_constraints(roots, asg)
+
+
+def test_auto_leaf_policy_picks_per_program():
+    """leaf_remat="auto" (the eval-mode batch compile): scratch2, unless the
+    program's 256-bit scratch reloads exceed ir.AUTO_SCRATCH_SHARE of its
+    instructions — then "scratch" (leaves regenerated, never in scratch)."""
+    import numpy as np
+    import bench
+    from mythril_amd import ir
+    for w, d in (("c2", 3), ("c3", 0), ("c3", 40)):
+        roots = bench.workload_roots(w, d)
+        auto = ir.compile_constraints(roots, leaf_remat="auto")
+        s2 = ir.compile_constraints(roots, leaf_remat="scratch2")
+        want = s2 if ir.scratch_reload_share(s2) <= ir.AUTO_SCRATCH_SHARE else \
+            ir.compile_constraints(roots, leaf_remat="scratch")
+        assert np.array_equal(auto.code, want.code) and np.array_equal(auto.consts, want.consts)
+        if w == "c3":
+            assert ir.scratch_reload_share(s2) > ir.AUTO_SCRATCH_SHARE
+            assert ir.scratch_reload_share(auto) < ir.scratch_reload_share(s2)
