@@ -207,13 +207,17 @@ def test_auto_leaf_policy_picks_per_program():
     import numpy as np
     import bench
     from mythril_amd import ir
-    for w, d in (("c2", 3), ("c3", 0), ("c3", 40)):
+    switched = 0
+    for w, d in (("c2", 3), ("c3", 0), ("c3", 4), ("c3", 40)):
         roots = bench.workload_roots(w, d)
         auto = ir.compile_constraints(roots, leaf_remat="auto")
         s2 = ir.compile_constraints(roots, leaf_remat="scratch2")
-        want = s2 if ir.scratch_reload_share(s2) <= ir.AUTO_SCRATCH_SHARE else \
-            ir.compile_constraints(roots, leaf_remat="scratch")
+        over = ir.scratch_reload_share(s2) > ir.AUTO_SCRATCH_SHARE
+        want = ir.compile_constraints(roots, leaf_remat="scratch") if over else s2
         assert np.array_equal(auto.code, want.code) and np.array_equal(auto.consts, want.consts)
-        if w == "c3":
-            assert ir.scratch_reload_share(s2) > ir.AUTO_SCRATCH_SHARE
+        if over:
+            switched += 1
             assert ir.scratch_reload_share(auto) < ir.scratch_reload_share(s2)
+        if w == "c2":
+            assert not over
+    assert switched >= 1
