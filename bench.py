@@ -340,7 +340,10 @@ def main():
 
     # host-side corpus compile (before any GPU initialisation, so fork is safe)
     ncpu = os.cpu_count() or 1
-    workers = max(1, min(16, ncpu // max(1, world)))
+    # (MYTHGPU_BENCH_WORKERS: profiled runs, where every forked worker also
+    # carries the profiler's GPU context, keep the process count low)
+    workers = int(os.environ.get("MYTHGPU_BENCH_WORKERS", "0")) or \
+        max(1, min(16, ncpu // max(1, world)))
     t0 = time.time()
     corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world, args.workload),
                           args.workload)

@@ -12,6 +12,9 @@ cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 P=gpurun_out/prof${PROF_TAG:+_$PROF_TAG}
 mkdir -p $P
 export MYTHGPU_JIT_CACHE=/tmp/mg_jitcache
+# under rocprofv3 every forked compile worker holds a GPU context too: keep
+# the bench's host workers few (the box allows 16 GPU processes)
+export MYTHGPU_BENCH_WORKERS=4
 ARGS="$@"
 SQ_ARGS=${PROF_TAG:+$ARGS}
 SQ_ARGS=${SQ_ARGS:---dags 512}
