@@ -41,10 +41,12 @@ typedef struct mg_batch mg_batch;
 typedef struct mg_jit mg_jit;
 
 /* Device candidate generator for one leaf (free variable / table cell),
- * generator v8 (restated bit-exactly by oracle/gen_ref.py):
+ * generator v9 (restated bit-exactly by oracle/gen_ref.py):
  *   salt = prog_seed * 0xD1B54A32D192ED03 ^ (leaf + 1) * 0x8CB92BA72F3D8DD7
  *   ss   = seed ^ salt
- *   r0   = SplitMix64(ss ^ index)                   (one step, state += golden)
+ *   s    = (ss ^ index) + 0x9E3779B97F4A7C15        (mod 2^64)
+ *   z    = (s ^ (s >> 32)) * 0xBF58476D1CE4E5B9     (mod 2^64)
+ *   r0   = z ^ (z >> 32)                            (v5-v8: SplitMix64(ss ^ index))
  *   x    = lo(r0) ^ hi(r0)                          (32 bits)
  *   cls  = mulhi(((lo32(index >> 6) ^ lo32(ss)) * 0x2545F491 mod 2^32)
  *                ^ hi32(ss), 100)                   (one class per leaf per

@@ -1064,51 +1064,71 @@ def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
 # ---------------------------------------------------------------------------
 
 GOLD = 0x9E3779B97F4A7C15
-MIX1, MIX2 = 0xBF58476D1CE4E5B9, 0x94D049BB133111EB
+MIX1 = 0xBF58476D1CE4E5B9                         # the one 64-bit multiplier (generator v9)
+MIX2 = 0x94D049BB133111EB                         # v8's second SplitMix64 multiplier
+# A/B knob only: MYTHGPU_GEN_MIX=8 renders v8's SplitMix64 finaliser (the
+# oracle restates v9 alone, so such a build fails parity by design)
+GEN_MIX = int(os.environ.get("MYTHGPU_GEN_MIX", "9"))
 PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
 CLS_MUL = 0x2545F491                              # class remix (generator v7/v8)
 # the wave's class in SALU when its first active index starts a 64-group
 # (A/B knob: MYTHGPU_GEN_SALU_CLASS=0 draws per lane in every wave)
 GEN_SALU_CLASS = os.environ.get("MYTHGPU_GEN_SALU_CLASS", "1") != "0"
-# SplitMix64 constants live in SGPRs during a LEAF (S_X..S_X+5; s95 = saved m0)
+# mixer constants live in SGPRs s[S_K:S_K+5], set once at entry
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
 S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
 
 
 def load_sm64_consts(a: Asm):
-    for reg, val in ((K_GOLD_LO, GOLD), (K_GOLD_HI, GOLD >> 32), (K_M1_LO, MIX1),
-                     (K_M1_HI, MIX1 >> 32), (K_M2_LO, MIX2), (K_M2_HI, MIX2 >> 32)):
+    consts = [(K_GOLD_LO, GOLD), (K_GOLD_HI, GOLD >> 32), (K_M1_LO, MIX1), (K_M1_HI, MIX1 >> 32)]
+    if GEN_MIX == 8:
+        consts += [(K_M2_LO, MIX2), (K_M2_HI, MIX2 >> 32)]
+    for reg, val in consts:
         a("s_mov_b32 %s, 0x%x" % (s(reg), val & 0xFFFFFFFF))
 
 
-def mul64_const(a: Asm, z: List[int], klo: int, khi: int, t: List[int]):
-    """z *= K (mod 2^64), K in SGPRs; t: aligned pairs t[0]:t[1], t[2]:t[3]
-    (t[3] is read as don't-care, never written).  hi cross terms with one
-    v_mul_lo and the low word of a mad; the full low product with a mad."""
-    a("v_mul_lo_u32 %s, %s, %s" % (v(t[2]), v(z[0]), s(khi)))                        # lo*khi
-    a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(t[0]), v(z[1]), s(klo), vp(t[2])))
-    a("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (vp(z[0]), v(z[0]), s(klo)))   # lo*klo
-    a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[0])))
-
-
 def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
-    """SplitMix64 on the per-lane state st = (lo, hi): st += GOLD; z =
-    mix(st).  Constants in SGPRs (load_sm64_consts); t: 4 temps with
+    """The candidate mixer (generator v9) on the per-lane state st = (lo,
+    hi): st += GOLD; u = st ^ (st >> 32); z = u * MIX1 (mod 2^64); r0 =
+    z ^ (z >> 32).  Every step is a bijection of 64-bit words, so distinct
+    candidate indices give distinct r0 per leaf.  v8 ran SplitMix64's
+    finaliser (three 64-bit xorshifts, two 64-bit multiplies: 19 VALU); the
+    32-bit-aligned xorshifts are one v_xor each and one multiply stays
+    (8 VALU).  Constants in SGPRs (load_sm64_consts); t: 4 temps with
     t[0]:t[1] and t[2]:t[3] aligned; t[3] holds GOLD_HI on entry (set once
-    per leaf, preserved).  Uses vcc (also as the mads' junk carry-out)."""
+    per leaf; read as the don't-care high half of the cross-term addend).
+    Uses vcc (also as the mads' junk carry-out)."""
     a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(K_GOLD_LO), v(st[0])))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[3]), v(st[1])))
-    a("v_lshrrev_b64 %s, 30, %s" % (vp(t[0]), vp(st[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(st[0]), v(t[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(st[1]), v(t[1])))
-    mul64_const(a, z, K_M1_LO, K_M1_HI, t)
-    a("v_lshrrev_b64 %s, 27, %s" % (vp(t[0]), vp(z[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
-    mul64_const(a, z, K_M2_LO, K_M2_HI, t)
-    a("v_lshrrev_b64 %s, 31, %s" % (vp(t[0]), vp(z[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(t[0])))
-    a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[1])))
+    if GEN_MIX == 8:
+        _splitmix_v8(a, st, z, t)
+        return
+    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(st[0]), v(st[1])))                    # u_lo
+    # z = u * MIX1 with u = (z[0], st[1]): the two cross terms' low word
+    # (lo * K_hi by v_mul_lo, hi * K_lo + it by the low half of a mad), the
+    # full low product by a mad, the cross word added to its high half
+    a("v_mul_lo_u32 %s, %s, %s" % (v(t[2]), v(z[0]), s(K_M1_HI)))
+    a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(t[0]), v(st[1]), s(K_M1_LO), vp(t[2])))
+    a("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (vp(z[0]), v(z[0]), s(K_M1_LO)))
+    a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[0])))
+    a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(z[1])))                       # r0_lo
+
+
+def _splitmix_v8(a: Asm, st: List[int], z: List[int], t: List[int]):
+    """v8's SplitMix64 finaliser on st (A/B knob MYTHGPU_GEN_MIX=8 only)."""
+    def mul64(klo, khi):
+        a("v_mul_lo_u32 %s, %s, %s" % (v(t[2]), v(z[0]), s(khi)))
+        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(t[0]), v(z[1]), s(klo), vp(t[2])))
+        a("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (vp(z[0]), v(z[0]), s(klo)))
+        a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[0])))
+    src = st
+    for sh, k in ((30, (K_M1_LO, K_M1_HI)), (27, (K_M2_LO, K_M2_HI)), (31, None)):
+        a("v_lshrrev_b64 %s, %d, %s" % (vp(t[0]), sh, vp(src[0])))
+        a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(src[0]), v(t[0])))
+        a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(src[1]), v(t[1])))
+        if k:
+            mul64(*k)
+        src = z
 
 
 def _uniform_limbs(a: Asm, dst: List[int], z: List[int], x: int):

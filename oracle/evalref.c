@@ -439,12 +439,11 @@ static void eval_dag(const dag_t* g, const V* leaves, V* vals) {
 
 static uint32_t mulhi32(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 
+/* v9 mixer: s += GOLD; z = (s ^ (s >> 32)) * MIX1; r0 = z ^ (z >> 32) */
 static uint64_t sm64(uint64_t* s) {
     *s += 0x9E3779B97F4A7C15ull;
-    uint64_t z = *s;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
+    uint64_t z = (*s ^ (*s >> 32)) * 0xBF58476D1CE4E5B9ull;
+    return z ^ (z >> 32);
 }
 
 static void gen_leaf(uint64_t seed, uint64_t prog_seed, uint32_t leaf, uint64_t idx, uint32_t w,

@@ -14,11 +14,12 @@ def _mulhi(a, b):
 
 
 def _sm64(s):
+    """v9 mixer: s += GOLD; u = s ^ (s >> 32); z = u * MIX1; r0 = z ^ (z >> 32)
+    (all mod 2^64; v5-v8 ran SplitMix64's finaliser)."""
     s = (s + 0x9E3779B97F4A7C15) & M64
-    z = s
-    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
-    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
-    return s, z ^ (z >> 31)
+    u = s ^ (s >> 32)
+    z = (u * 0xBF58476D1CE4E5B9) & M64
+    return s, z ^ (z >> 32)
 
 
 CLS_MUL = 0x2545F491

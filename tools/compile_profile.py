@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--graph", default="", help="write gprof's call graph here")
+    ap.add_argument("--time", action="store_true",
+                    help="no profiler: build -O2 and print the wall time per query (best of 5)")
     args = ap.parse_args()
     import numpy as np
     import mythril_amd.model as M
@@ -60,6 +62,21 @@ def main():
         with open(corpus, "wb") as fh:
             fh.write(b"".join(recs) * args.reps)
         exe = os.path.join(d, "prof")
+        if args.time:
+            import time
+            subprocess.run(["g++", "-std=c++17", "-O2", "-I" + os.path.join(ROOT, "include"),
+                            os.path.join(ROOT, "tests", "fuzz_compile.cpp"),
+                            os.path.join(ROOT, "mythril_amd", "csrc", "mg_compile.cpp"), "-o", exe],
+                           check=True)
+            import resource
+            best = []
+            for _ in range(5):
+                u0 = resource.getrusage(resource.RUSAGE_CHILDREN).ru_utime
+                subprocess.run([exe, corpus, "0"], cwd=d, check=True, capture_output=True)
+                best.append(resource.getrusage(resource.RUSAGE_CHILDREN).ru_utime - u0)
+            print("native compile: %.0f us user CPU per query (best of 5, %d queries x %d reps)"
+                  % (min(best) * 1e6 / (len(seen) * args.reps), len(seen), args.reps))
+            return
         subprocess.run(["g++", "-std=c++17", "-O2", "-pg", "-I" + os.path.join(ROOT, "include"),
                         os.path.join(ROOT, "tests", "fuzz_compile.cpp"),
                         os.path.join(ROOT, "mythril_amd", "csrc", "mg_compile.cpp"), "-o", exe],
