@@ -1074,6 +1074,9 @@ CLS_MUL = 0x2545F491                              # class remix (generator v7/v8
 # the wave's class in SALU when its first active index starts a 64-group
 # (A/B knob: MYTHGPU_GEN_SALU_CLASS=0 draws per lane in every wave)
 GEN_SALU_CLASS = os.environ.get("MYTHGPU_GEN_SALU_CLASS", "1") != "0"
+# compiled programs: the aligned wave's class dispatch carries no waterfall
+# state (A/B knob: MYTHGPU_GEN_JIT_FLAT=0 keeps the interpreter's layout)
+GEN_JIT_FLAT = os.environ.get("MYTHGPU_GEN_JIT_FLAT", "1") != "0"
 # mixer constants live in SGPRs s[S_K:S_K+5], set once at entry
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
 S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
@@ -1255,6 +1258,75 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
         a("s_mov_b64 %s, -1" % sp(rest))
 
+    dst = X if dst is None else dst
+
+    def classes(lab_out):
+        # the class dispatch on s[sc] and the four classes' code, every exit
+        # at lab_out
+        l_uni, l_small, l_bnd = a.uniq("guni"), a.uniq("gsml"), a.uniq("gbnd")
+        a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["pu"])))
+        a("s_cbranch_scc1 %s" % l_uni)                   # cls < pct_uniform
+        a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["ps"])))
+        a("s_cbranch_scc1 %s" % l_small)
+        a("s_cmp_lt_u32 %s, %s" % (s(sc), s(f["pb"])))
+        a("s_cbranch_scc1 %s" % l_bnd)
+        a("s_cmp_eq_u32 %s, 0" % s(f["pn"]))
+        a("s_cbranch_scc1 %s" % l_uni)                   # pool class, empty pool
+        _pool_loads(a, dst, lo, f, tt)                   # pool
+        a("s_branch %s" % lab_out)
+        a.label(l_bnd)
+        _boundary_loads(a, dst, lo, f, tt)
+        a("s_branch %s" % lab_out)
+        a.label(l_small)                                 # small: r0 (< 2^64)
+        a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
+        moves(a, dst[2:], [None] * 6)
+        a("s_branch %s" % lab_out)
+        a.label(l_uni)
+        _uniform_limbs(a, dst, z, tt[0])
+
+    if GEN_SALU_CLASS and JIT and GEN_JIT_FLAT:
+        # compiled programs (straight-line, cold code at the program's end):
+        # the wave-uniform class runs the dispatch with no waterfall state
+        # at all; an unaligned wave takes a cold copy of mixer + dispatch
+        # inside its own waterfall
+        lab_wdone = a.uniq("gwdone")
+        a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
+        a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
+        a("s_and_b32 %s, %s, 63" % (s(rest), s(sc)))
+        a("s_cbranch_scc1 %s" % lab_slow)
+        a("s_lshr_b64 %s, %s, 6" % (sp(sc), sp(sc)))
+        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T)))
+        a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
+        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
+        a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
+        sm64(a, st, z, tt)
+        classes(lab_done)
+        a.label(lab_done)
+        if wait:
+            a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
+        a.cold()
+        a.label(lab_slow)
+        lane_class()
+        sm64(a, st, z, tt)
+        a("s_mov_b64 %s, exec" % sp(save))
+        a.label(lab_loop)
+        a("v_readfirstlane_b32 %s, %s" % (s(sc), v(cls)))
+        a("v_cmp_eq_u32 vcc, %s, %s" % (s(sc), v(cls)))
+        a("s_and_saveexec_b64 %s, vcc" % sp(rest))
+        a("s_andn2_b64 %s, %s, exec" % (sp(rest), sp(rest)))   # lanes still to do
+        classes(lab_wdone)
+        a.label(lab_wdone)
+        a("s_mov_b64 exec, %s" % sp(rest))
+        a("s_cbranch_execnz %s" % lab_again)
+        a("s_mov_b64 exec, %s" % sp(save))
+        a("s_branch %s" % lab_done)
+        # another group in this wave: its loads are in flight into other lanes
+        # of dst; settle them before the next class writes dst
+        a.label(lab_again)
+        a("s_waitcnt vmcnt(0)")
+        a("s_branch %s" % lab_loop)
+        a.hot()
+        return
     if GEN_SALU_CLASS:
         a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
         a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
@@ -1270,7 +1342,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         lane_class()
     a.label(lab_join)
     sm64(a, st, z, tt)
-    dst = X if dst is None else dst
     a("s_mov_b64 %s, exec" % sp(save))
     a("s_cmp_lg_u64 %s, 0" % sp(rest))
     a("s_cbranch_scc1 %s" % lab_loop)                # per-lane classes: the waterfall

@@ -1203,6 +1203,7 @@ def source_digest() -> str:
     knobs = {"coalesce": COALESCE, "flush": COLD_FLUSH, "asm": G.digest(),
              "div_bits_first": G.DIV_BITS_FIRST, "div_stage_skip": G.DIV_STAGE_SKIP,
              "gen_salu_class": G.GEN_SALU_CLASS, "gen_mix": G.GEN_MIX,
+             "gen_jit_flat": G.GEN_JIT_FLAT,
              "probe": G._PROBE,
              "leaf_remat": ir.LEAF_REMAT, "keep_clean": ir.KEEP_CLEAN}
     h.update(repr(sorted(knobs.items())).encode())
