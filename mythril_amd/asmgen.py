@@ -1209,14 +1209,22 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     cls, lo = T[8], z[0]
     g = S_CUR
     in_record = dst is not None and dst != X
-    if in_record:
-        f = {"w": g + 0, "poff": fld(bank, LEAFD_POFF), "pn": fld(bank, LEAFD_PN),
-             "pu": g + 3, "ps": g + 4, "pb": g + 5, "salt": fld(bank, LEAFD_SALT)}
+    flat = GEN_SALU_CLASS and JIT and GEN_JIT_FLAT
+
+    def record_fields():
+        # width and class thresholds from the LEAFD record (in a compiled
+        # program they are constants: set after the branches that skip
+        # them, they fold into the compares as literals)
         a("s_movk_i32 %s, 0x100" % s(f["w"]))
         pk = fld(bank, LEAFD_PCT)
         a("s_and_b32 %s, %s, 0xff" % (s(f["pu"]), s(pk)))
         a("s_bfe_u32 %s, %s, 0x80008" % (s(f["ps"]), s(pk)))
         a("s_bfe_u32 %s, %s, 0x80010" % (s(f["pb"]), s(pk)))
+    if in_record:
+        f = {"w": g + 0, "poff": fld(bank, LEAFD_POFF), "pn": fld(bank, LEAFD_PN),
+             "pu": g + 3, "ps": g + 4, "pb": g + 5, "salt": fld(bank, LEAFD_SALT)}
+        if not flat:
+            record_fields()
     else:
         f = {"w": g + 0, "poff": g + 1, "pn": g + 2, "pu": g + 3, "ps": g + 4, "pb": g + 5,
              "salt": g + 6}
@@ -1229,7 +1237,12 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
     if not in_record:
         a("s_waitcnt lgkmcnt(0)")
-    a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(f["salt"])))     # ss = seed ^ salt
+    if flat and in_record:                           # ss = seed ^ salt, the salt as literals
+        seed = int(PINNED["seed"][2:].split(":")[0])
+        a("s_xor_b32 %s, %s, %s" % (s(S_T), s(seed), s(f["salt"])))
+        a("s_xor_b32 %s, %s, %s" % (s(S_T + 1), s(seed + 1), s(f["salt"] + 1)))
+    else:
+        a("s_xor_b64 %s, %s, %s" % (sp(S_T), IN["seed"], sp(f["salt"])))     # ss = seed ^ salt
     a("v_xor_b32 %s, %s, %s" % (v(st[0]), s(S_T), OP_IDX_LO))
     a("v_xor_b32 %s, %s, %s" % (v(st[1]), s(S_T + 1), OP_IDX_HI))
     # v8 class: cls = mulhi(((lo32(idx >> 6) ^ lo32(ss)) * CLS_MUL) ^ hi32(ss), 100)
@@ -1284,7 +1297,7 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a.label(l_uni)
         _uniform_limbs(a, dst, z, tt[0])
 
-    if GEN_SALU_CLASS and JIT and GEN_JIT_FLAT:
+    if flat:
         # compiled programs (straight-line, cold code at the program's end):
         # the wave-uniform class runs the dispatch with no waterfall state
         # at all; an unaligned wave takes a cold copy of mixer + dispatch
@@ -1299,6 +1312,8 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
         a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
         a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
+        if in_record:
+            record_fields()
         sm64(a, st, z, tt)
         classes(lab_done)
         a.label(lab_done)
@@ -1306,6 +1321,8 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
             a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
         a.cold()
         a.label(lab_slow)
+        if in_record:
+            record_fields()
         lane_class()
         sm64(a, st, z, tt)
         a("s_mov_b64 %s, exec" % sp(save))

@@ -288,7 +288,6 @@ _CMP = {"s_cmp_eq_u32": lambda a, b: a == b, "s_cmp_lg_u32": lambda a, b: a != b
 # ---------------------------------------------------------------------------
 
 RECORD_SGPRS = frozenset(range(BANK0, BANK0 + 8))
-_LIVE: Dict[int, List[frozenset]] = {}
 _TARGETS: Dict[int, frozenset] = {}
 
 
@@ -307,26 +306,68 @@ def _branch_targets(lines: Sequence[str]) -> frozenset:
     return hit
 
 
-def _live_after(lines: Sequence[str]) -> List[frozenset]:
-    """For each template line, the SGPRs some LATER line reads (an
-    over-approximation of liveness: later writes are ignored)."""
+_REACH: Dict[int, object] = {}
+
+
+def _reach_reads(lines: Sequence[str]):
+    """(R, at): R[i] = the SGPRs some line on a control-flow path from line
+    i reads (i included; later writes ignored, so an over-approximation of
+    liveness, but along the template's branches and fall-throughs rather
+    than its text order); at: label -> line index.  A branch materializes
+    only what its target may read, so a value the fall-through path uses
+    as a literal stays unmaterialized there."""
     key = id(lines)
-    hit = _LIVE.get(key)
-    if hit is not None and len(hit) == len(lines):
+    hit = _REACH.get(key)
+    if hit is not None and len(hit[0]) == len(lines):
         return hit
-    out: List[frozenset] = [frozenset()] * len(lines)
-    acc: set = set()
-    for i in range(len(lines) - 1, -1, -1):
-        out[i] = frozenset(acc)
-        t = lines[i].strip()
-        if not t or t.startswith("@@") or t.endswith(":"):
+    n = len(lines)
+    uses: List[frozenset] = []
+    succ: List[Tuple[int, ...]] = []
+    at: Dict[str, int] = {}
+    parsed = []
+    for i, l in enumerate(lines):
+        t = _subst(l.strip(), "x")
+        parsed.append(t)
+        if t.endswith(":"):
+            at[t[:-1]] = i
+    for i, t in enumerate(parsed):
+        nxt = (i + 1,) if i + 1 < n else ()
+        if not t or t.endswith(":"):
+            uses.append(frozenset())
+            succ.append(nxt)
             continue
-        m, ops, _ = parse(_subst(t, "x"))
+        if t.startswith("@@"):
+            uses.append(frozenset())
+            succ.append(())                      # END / HALT / CALL: no fall-through
+            continue
+        m, ops, _ = parse(t)
+        u = set()
         for x in ops[n_dest(m):] if not m.startswith(("s_set_gpr_idx", "s_cmp", "s_bitcmp")) else ops:
             r = sreg(x)
             if r:
-                acc.update(range(r[0], r[0] + r[1]))
-    _LIVE[key] = out
+                u.update(range(r[0], r[0] + r[1]))
+        uses.append(frozenset(u))
+        if m == "s_branch":
+            succ.append((at[ops[0]],) if ops[0] in at else ())
+        elif m.startswith("s_cbranch"):
+            succ.append(nxt + ((at[ops[0]],) if ops[0] in at else ()))
+        elif m.startswith(("s_setpc", "s_endpgm")):
+            succ.append(())
+        else:
+            succ.append(nxt)
+    R = [set(u) for u in uses]
+    changed = True
+    while changed:
+        changed = False
+        for i in range(n - 1, -1, -1):
+            acc = R[i]
+            k = len(acc)
+            for j in succ[i]:
+                acc |= R[j]
+            if len(acc) != k:
+                changed = True
+    out = ([frozenset(r) for r in R], at)
+    _REACH[key] = out
     return out
 
 
@@ -350,7 +391,12 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
     them on every path, and after a label only the record fields are known.
     GPR-index state must agree on every path into a label (checked)."""
     st = _State(rec)
-    live = _live_after(lines)
+    reach, _ = _reach_reads(lines)
+    label_at = {}                        # label (this record's name) -> template line
+    for k, raw in enumerate(lines):
+        t = raw.strip()
+        if t.endswith(":"):
+            label_at[_subst(t[:-1], tag)] = k
     targets = {l.replace("%=", tag) for l in _branch_targets(lines)}
     hot: List[str] = []
     cold: List[str] = []
@@ -371,10 +417,13 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
                 emit("    s_mov_b32 s%d, 0x%x" % (r, st.known[r]))
                 st.mat.add(r)
 
-    def settle(i):
-        """Before a branch or a join: derived values a later line may read
-        go into their registers."""
-        materialize(sorted(r for r in st.known if r not in RECORD_SGPRS and r in live[i]))
+    def settle(label):
+        """Before a branch to / a fall-through into ``label``: derived values
+        the code from there may read go into their registers."""
+        j = label_at.get(label)
+        need = reach[j] if j is not None else None
+        materialize(sorted(r for r in st.known if r not in RECORD_SGPRS and
+                           (need is None or r in need)))
 
     def written(regs):
         for r in regs:
@@ -446,7 +495,7 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
             dead = False
             incoming = idx_in.pop(lab, "none")
             if fallthrough:
-                settle(i)
+                settle(lab)
                 if incoming != "none" and incoming != st.idx:
                     raise JitUnsupported("index state differs at label %s" % lab)
             elif incoming != "none":
@@ -490,13 +539,13 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
         # ---- control flow ------------------------------------------------
         if m in ("s_cbranch_scc0", "s_cbranch_scc1") and st.scc is not None:
             if st.scc == (1 if m == "s_cbranch_scc1" else 0):
-                settle(i)
+                settle(ops[0])
                 branch_to(ops[0])
                 emit(render("s_branch", ops))
                 fallthrough, dead = False, True
             continue
         if m.startswith("s_cbranch") or m == "s_branch":
-            settle(i)
+            settle(ops[0])
             branch_to(ops[0])
             emit(render(m, ops, mods))
             if m == "s_branch":
