@@ -1139,7 +1139,8 @@ def _uniform_limbs(a: Asm, dst: List[int], z: List[int], x: int):
     x * C_k + r0 (mod 2^64) with x = lo ^ hi of r0 — one v_mad_u64_u32 per
     two limbs (v6; v4 spent a 4-VALU multiply-xorshift per limb).  Uses
     s[S_PAIR..S_PAIR+2] and v[x]."""
-    a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
+    if dst[0] != z[0]:
+        a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(x), v(z[0]), v(z[1])))
     for k, c in enumerate(PAIR_MUL):
         a("s_mov_b32 %s, 0x%x" % (s(S_PAIR + k), c))
@@ -1205,10 +1206,14 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     LEAFD (``in_record``: 256 bits) finds them in its own record instead
     (mg_load_program: pool_off, salt, pool_n, packed thresholds), so no
     descriptor load sits between dispatch and the generator."""
-    st, z, tt = [T[0], T[1]], [T[2], T[3]], [T[4], T[5], T[6], T[7]]
+    in_record = dst is not None and dst != X
+    dst = X if dst is None else dst
+    # the mixer writes r0 straight into the value's first two limbs (the
+    # uniform and small classes keep it there; the load classes read its
+    # low word for their address before the loads overwrite it)
+    st, z, tt = [T[0], T[1]], [dst[0], dst[1]], [T[4], T[5], T[6], T[7]]
     cls, lo = T[8], z[0]
     g = S_CUR
-    in_record = dst is not None and dst != X
     flat = GEN_SALU_CLASS and JIT and GEN_JIT_FLAT
 
     def record_fields():
@@ -1271,7 +1276,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a("v_mul_hi_u32 %s, %s, %s" % (v(cls), v(cls), s(sc)))
         a("s_mov_b64 %s, -1" % sp(rest))
 
-    dst = X if dst is None else dst
 
     def classes(lab_out):
         # the class dispatch on s[sc] and the four classes' code, every exit
@@ -1291,7 +1295,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         _boundary_loads(a, dst, lo, f, tt)
         a("s_branch %s" % lab_out)
         a.label(l_small)                                 # small: r0 (< 2^64)
-        a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
         moves(a, dst[2:], [None] * 6)
         a("s_branch %s" % lab_out)
         a.label(l_uni)
@@ -1377,7 +1380,6 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     _boundary_loads(a, dst, lo, f, tt)
     a("s_branch %s" % lab_done)
     a.label(lab_small)                               # small: r0 (< 2^64)
-    a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     moves(a, dst[2:], [None] * 6)
     a("s_branch %s" % lab_done)
     a.label(lab_uni)
