@@ -12,9 +12,10 @@ cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 P=gpurun_out/prof${PROF_TAG:+_$PROF_TAG}
 mkdir -p $P
 export MYTHGPU_JIT_CACHE=/tmp/mg_jitcache
-# under rocprofv3 every forked compile worker holds a GPU context too: keep
-# the bench's host workers few (the box allows 16 GPU processes)
-export MYTHGPU_BENCH_WORKERS=4
+# under rocprofv3 every forked compile worker holds a GPU context too, and a
+# pool's SIGTERM at shutdown can leave a counter pass hung in the profiler's
+# signal handler (r4p6 WRITE_SIZE pass): profiled runs compile in-process
+export MYTHGPU_BENCH_WORKERS=1
 ARGS="$@"
 SQ_ARGS=${PROF_TAG:+$ARGS}
 SQ_ARGS=${SQ_ARGS:---dags 512}
