@@ -220,3 +220,30 @@ def test_corpus_programs_do_not_depend_on_build_history():
     with mp.get_context("spawn").Pool(2) as pool:
         a, b = pool.map(_program_digests, orders)
     assert a == b
+
+
+def test_branch_materializes_only_what_its_target_reads():
+    """jit.specialize: a derived scalar is written to its register before a
+    branch only when the code from the branch target may read it; on the
+    fall-through path it stays a literal."""
+    from mythril_amd.jit import specialize
+    b = jit.BANK0
+    lines = [
+        "    s_and_b32 s80, s%d, 0xff" % b,          # derived: s80 = rec[0] & 0xff
+        "    s_add_u32 s81, s%d, 1" % (b + 1),       # derived: s81 = rec[1] + 1
+        "    s_cmp_eq_u32 s82, 0",
+        "    s_cbranch_scc1 .Ltgt%=",
+        "    s_cmp_lt_u32 s83, s80",                 # fall-through reads s80 only
+        "    s_branch .Ldone%=",
+        ".Ltgt%=:",
+        "    s_add_u32 s84, s81, s83",               # the target reads s81 only
+        ".Ldone%=:",
+        "    s_nop 0",
+    ]
+    rec = [0x1234, 41, 0, 0, 0, 0, 0, 0]
+    hot, cold, _ = specialize(lines, rec, "t")
+    text = "\n".join(hot + cold)
+    before = text.split("s_cbranch_scc1")[0]
+    assert "s_mov_b32 s81, 0x2a" in before          # the target's read, materialized
+    assert "s_mov_b32 s80" not in text              # never materialized ...
+    assert "s_cmp_lt_u32 s83, 52" in text           # ... the compare takes it inline
