@@ -52,6 +52,8 @@ BANK = (40, 48)            # s[40:47], s[48:55]: the two record banks
 S_BASE = 56                # s[56:57] handler base PC
 S_CODE = 58                # s[58:59] translated code
 S_IP = 60                  # byte offset of the next record to prefetch
+S_FAST = S_IP              # compiled programs (no prefetch): bit 0 = generator
+                           # mode with no leaf store (jit.program_asm sets it)
 S_VAR = 61                 # heavy ops: variant bits | op << 4
 S_CONST = 62               # s[62:63] constant pool
 S_CUR = 64                 # s[64:71] current record of a heavy op / LEAF descriptor
@@ -1189,7 +1191,8 @@ def _pool_loads(a: Asm, dst: List[int], lo: int, f, tt: List[int]):
     a("global_load_dwordx4 v[%d:%d], %s, %s offset:16" % (dst[4], dst[7], v(e), sp(S_CONST)))
 
 
-def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = True):
+def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = True,
+              nested: bool = False):
     """dst[0..7] (default X) <- generator value of leaf C for candidate
     first + lane; the boundary / pool lanes arrive by loads into dst, waited
     for unless wait=False (LEAFD: the translator places the WAITVM).
@@ -1322,7 +1325,11 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a.label(lab_done)
         if wait:
             a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
-        a.cold()
+        lab_after = a.uniq("gafter")
+        if nested:                                       # already out of line
+            a("s_branch %s" % lab_after)
+        else:
+            a.cold()
         a.label(lab_slow)
         if in_record:
             record_fields()
@@ -1345,7 +1352,10 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a.label(lab_again)
         a("s_waitcnt vmcnt(0)")
         a("s_branch %s" % lab_loop)
-        a.hot()
+        if nested:
+            a.label(lab_after)
+        else:
+            a.hot()
         return
     if GEN_SALU_CLASS:
         a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
@@ -1456,6 +1466,34 @@ def h_leafd(a: Asm, bank: int, var: int):
     fd = [FB + 8 * slot + j for j in range(8)]
     prologue(a, bank)
     lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
+    if JIT and GEN_SALU_CLASS and GEN_JIT_FLAT:
+        # compiled programs: one flag test per leaf for the common case
+        # (generator mode, no leaf store); the rest in a cold copy
+        lab_gen = a.uniq("lgen")
+        a("s_bitcmp1_b32 %s, 0" % s(S_FAST))
+        a("s_cbranch_scc0 %s" % lab_gen)
+        _gen_leaf(a, bank, dst=fd, wait=False)
+        a.label(lab_done)
+        _wait_if_flagged(a, var)
+        dispatch(a, 1 - bank)
+        a.cold()
+        a.label(lab_gen)
+        a("s_bitcmp1_b32 %s, 0" % IN["mode"])
+        a("s_cbranch_scc0 %s" % lab_mem)
+        _gen_leaf(a, bank, dst=fd, wait=False, nested=True)
+        _store_soa(a, fd, IN["lout"], fld(bank, F_C), wait_vm=True)
+        a("s_branch %s" % lab_done)
+        a.label(lab_mem)
+        _soa_base(a, IN["leaves"], fld(bank, F_C))
+        lane_offset(a, T[0])
+        for j in range(8):
+            a("global_load_dword %s, %s, %s" % (v(fd[j]), v(T[0]), sp(S_T)))
+            if j < 7:
+                _soa_step(a)
+        a("s_branch %s" % lab_done)
+        a.hot()
+        a.flush_cold()
+        return
     a("s_bitcmp1_b32 %s, 0" % IN["mode"])
     a("s_cbranch_scc0 %s" % lab_mem)                 # (generator mode in line)
     _gen_leaf(a, bank, dst=fd, wait=False)

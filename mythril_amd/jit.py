@@ -1117,6 +1117,11 @@ def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
         fps.append(records_fingerprint(full))
     tag = tag or entry.lstrip(".L")
     out = [entry + ":"]
+    if G.GEN_SALU_CLASS and G.GEN_JIT_FLAT:
+        # s[S_FAST] bit 0: generator mode and no leaf store — the one test a
+        # compiled LEAFD makes on its common path (asmgen.h_leafd)
+        out.append("    s_cmp_eq_u64 %s, 0" % G.PINNED["lout"])
+        out.append("    s_cselect_b32 s%d, %s, 0" % (G.S_FAST, G.PINNED["mode"]))
     pending_cold: List[str] = []
     flush_no = 0
     for i, r in enumerate(recs):

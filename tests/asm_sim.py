@@ -430,6 +430,9 @@ class Wave:
     def i_s_cmp_lg_u64(self, a, pc):
         self.scc = int(self.sread(a[0], 64) != self.sread(a[1], 64))
 
+    def i_s_cselect_b32(self, a, pc):
+        self.swrite(a[0], self.sread(a[1]) if self.scc else self.sread(a[2]))
+
     def i_s_cselect_b64(self, a, pc):
         self.swrite(a[0], self.sread(a[1], 64) if self.scc else self.sread(a[2], 64))
 

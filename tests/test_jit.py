@@ -57,6 +57,10 @@ def test_jit_corpus_dag_generator_mode(dag_id, n_lds):
     r_j, pr_j, lo_j, _ = asm_sim.simulate(prog, gen=(SEED, dag_id, first, lg), n_lds=n_lds,
                                           want_leaves=True, jit=True)
     assert np.array_equal(lo_i, lo_j) and np.array_equal(pr_i, pr_j) and np.array_equal(r_i, r_j)
+    # no leaf store: compiled leaves take their one-flag common path
+    # (asmgen.h_leafd, S_FAST); same roots and probes
+    r_f, pr_f, _, _ = asm_sim.simulate(prog, gen=(SEED, dag_id, first, lg), n_lds=n_lds, jit=True)
+    assert np.array_equal(pr_f, pr_j) and np.array_equal(r_f, r_j)
     for lane in range(0, 64, 7):
         asg = unpack(prog, lo_j[:, :, lane])
         want = R.evaluate(list(roots), R.Assignment(asg.vars, asg.arrays, asg.funcs))
