@@ -1088,6 +1088,8 @@ def load_sm64_consts(a: Asm):
     consts = [(K_GOLD_LO, GOLD), (K_GOLD_HI, GOLD >> 32), (K_M1_LO, MIX1), (K_M1_HI, MIX1 >> 32)]
     if GEN_MIX == 8:
         consts += [(K_M2_LO, MIX2), (K_M2_HI, MIX2 >> 32)]
+    else:                       # v9 frees s[100:101]: two uniform-limb multipliers
+        consts += [(K_M2_LO, PAIR_MUL[0]), (K_M2_HI, PAIR_MUL[1])]
     for reg, val in consts:
         a("s_mov_b32 %s, 0x%x" % (s(reg), val & 0xFFFFFFFF))
 
@@ -1144,10 +1146,14 @@ def _uniform_limbs(a: Asm, dst: List[int], z: List[int], x: int):
     if dst[0] != z[0]:
         a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(x), v(z[0]), v(z[1])))
+    # v9: the first two multipliers are resident in s[100:101] (set at entry)
+    regs = [K_M2_LO, K_M2_HI, S_PAIR + 2] if GEN_MIX != 8 else [S_PAIR + k for k in range(3)]
     for k, c in enumerate(PAIR_MUL):
-        a("s_mov_b32 %s, 0x%x" % (s(S_PAIR + k), c))
+        if regs[k] >= S_K + 4 and GEN_MIX != 8:
+            continue
+        a("s_mov_b32 %s, 0x%x" % (s(regs[k]), c))
     for k in range(3):
-        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(x), s(S_PAIR + k),
+        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(x), s(regs[k]),
                                                  vp(z[0])))
 
 
