@@ -53,7 +53,8 @@ S_BASE = 56                # s[56:57] handler base PC
 S_CODE = 58                # s[58:59] translated code
 S_IP = 60                  # byte offset of the next record to prefetch
 S_FAST = S_IP              # compiled programs (no prefetch): bit 0 = generator
-                           # mode with no leaf store (jit.program_asm sets it)
+                           # mode, no leaf store, wave group aligned to 64
+                           # candidates (jit.program_asm sets it)
 S_VAR = 61                 # heavy ops: variant bits | op << 4
 S_CONST = 62               # s[62:63] constant pool
 S_CUR = 64                 # s[64:71] current record of a heavy op / LEAF descriptor
@@ -1081,11 +1082,14 @@ GEN_SALU_CLASS = os.environ.get("MYTHGPU_GEN_SALU_CLASS", "1") != "0"
 GEN_JIT_FLAT = os.environ.get("MYTHGPU_GEN_JIT_FLAT", "1") != "0"
 # mixer constants live in SGPRs s[S_K:S_K+5], set once at entry
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
+S_GROUP = K_GOLD_LO        # compiled programs: lo32(idx >> 6) of the wave (jit.program_asm)
 S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a LEAF
 
 
 def load_sm64_consts(a: Asm):
-    consts = [(K_GOLD_LO, GOLD), (K_GOLD_HI, GOLD >> 32), (K_M1_LO, MIX1), (K_M1_HI, MIX1 >> 32)]
+    # (GOLD goes in as literals; s[96:97] hold a compiled program's wave
+    # group, S_GROUP, set at the program's entry)
+    consts = [(K_M1_LO, MIX1), (K_M1_HI, MIX1 >> 32)]
     if GEN_MIX == 8:
         consts += [(K_M2_LO, MIX2), (K_M2_HI, MIX2 >> 32)]
     else:                       # v9 frees s[100:101]: two uniform-limb multipliers
@@ -1105,7 +1109,7 @@ def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
     t[0]:t[1] and t[2]:t[3] aligned; t[3] holds GOLD_HI on entry (set once
     per leaf; read as the don't-care high half of the cross-term addend).
     Uses vcc (also as the mads' junk carry-out)."""
-    a("v_add_co_u32 %s, vcc, %s, %s" % (v(st[0]), s(K_GOLD_LO), v(st[0])))
+    a("v_add_co_u32 %s, vcc, 0x%x, %s" % (v(st[0]), GOLD & 0xFFFFFFFF, v(st[0])))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[3]), v(st[1])))
     if GEN_MIX == 8:
         _splitmix_v8(a, st, z, t)
@@ -1198,7 +1202,7 @@ def _pool_loads(a: Asm, dst: List[int], lo: int, f, tt: List[int]):
 
 
 def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = True,
-              nested: bool = False):
+              nested: bool = False, aligned: bool = False):
     """dst[0..7] (default X) <- generator value of leaf C for candidate
     first + lane; the boundary / pool lanes arrive by loads into dst, waited
     for unless wait=False (LEAFD: the translator places the WAITVM).
@@ -1248,7 +1252,7 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a("s_load_dwordx8 s[%d:%d], %s, %s" % (g, g + 7, sp(S_T), s(S_T + 2)))
     # st = seed ^ salt ^ idx (v5: the counter itself, SplitMix64's finaliser
     # spreads it; no idx * GOLD multiply); idx = first + lane arrives ready
-    a("v_mov_b32 %s, %s" % (v(tt[3]), s(K_GOLD_HI)))
+    a("v_mov_b32 %s, 0x%x" % (v(tt[3]), GOLD >> 32))
     if not in_record:
         a("s_waitcnt lgkmcnt(0)")
     if flat and in_record:                           # ss = seed ^ salt, the salt as literals
@@ -1309,6 +1313,21 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         a.label(l_uni)
         _uniform_limbs(a, dst, z, tt[0])
 
+    if flat and aligned:
+        # compiled program, wave known aligned (S_FAST): its group is in
+        # s[S_GROUP] since the program's entry — the class is four SALU
+        a("s_xor_b32 %s, %s, %s" % (s(sc), s(S_GROUP), s(S_T)))
+        a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
+        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
+        a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
+        if in_record:
+            record_fields()
+        sm64(a, st, z, tt)
+        classes(lab_done)
+        a.label(lab_done)
+        if wait:
+            a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
+        return
     if flat:
         # compiled programs (straight-line, cold code at the program's end):
         # the wave-uniform class runs the dispatch with no waterfall state
@@ -1478,7 +1497,7 @@ def h_leafd(a: Asm, bank: int, var: int):
         lab_gen = a.uniq("lgen")
         a("s_bitcmp1_b32 %s, 0" % s(S_FAST))
         a("s_cbranch_scc0 %s" % lab_gen)
-        _gen_leaf(a, bank, dst=fd, wait=False)
+        _gen_leaf(a, bank, dst=fd, wait=False, aligned=True)
         a.label(lab_done)
         _wait_if_flagged(a, var)
         dispatch(a, 1 - bank)

@@ -1118,10 +1118,19 @@ def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
     tag = tag or entry.lstrip(".L")
     out = [entry + ":"]
     if G.GEN_SALU_CLASS and G.GEN_JIT_FLAT:
-        # s[S_FAST] bit 0: generator mode and no leaf store — the one test a
-        # compiled LEAFD makes on its common path (asmgen.h_leafd)
+        # s[S_FAST] bit 0: generator mode, no leaf store and a wave whose
+        # first active index starts a group of 64 (every active lane in one
+        # group) — the one test a compiled LEAFD makes on its common path
+        # (asmgen.h_leafd); s[S_GROUP] = lo32(that index >> 6), the group
+        # the leaves' classes are drawn for
+        g = G.S_GROUP
         out.append("    s_cmp_eq_u64 %s, 0" % G.PINNED["lout"])
         out.append("    s_cselect_b32 s%d, %s, 0" % (G.S_FAST, G.PINNED["mode"]))
+        out.append("    v_readfirstlane_b32 s%d, %s" % (g, G.PINNED["idx_lo"]))
+        out.append("    v_readfirstlane_b32 s%d, %s" % (g + 1, G.PINNED["idx_hi"]))
+        out.append("    s_and_b32 s%d, s%d, 63" % (G.S_T, g))
+        out.append("    s_cselect_b32 s%d, 0, s%d" % (G.S_FAST, G.S_FAST))
+        out.append("    s_lshr_b64 s[%d:%d], s[%d:%d], 6" % (g, g + 1, g, g + 1))
     pending_cold: List[str] = []
     flush_no = 0
     for i, r in enumerate(recs):
