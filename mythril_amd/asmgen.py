@@ -1449,6 +1449,41 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     if mask:
         load_masks(a, fld(bank, F_MOFF))
     lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
+    if JIT and GEN_SALU_CLASS and GEN_JIT_FLAT:
+        # compiled programs: the common case (generator mode, no leaf store,
+        # aligned wave) behind one flag test, as in h_leafd
+        def masked():
+            if mask:
+                a("s_waitcnt lgkmcnt(0)")
+                for j in range(8):
+                    a("v_and_b32 %s, %s, %s" % (v(X[j]), s(S_M + j), v(X[j])))
+        lab_gen = a.uniq("lgen")
+        a("s_bitcmp1_b32 %s, 0" % s(S_FAST))
+        a("s_cbranch_scc0 %s" % lab_gen)
+        _gen_leaf(a, bank, aligned=True)
+        masked()
+        a.label(lab_done)
+        finish(a, bank, X, root, mask)
+        a.cold()
+        a.label(lab_gen)
+        a("s_bitcmp1_b32 %s, 0" % IN["mode"])
+        a("s_cbranch_scc0 %s" % lab_mem)
+        _gen_leaf(a, bank, nested=True)
+        masked()
+        _store_soa(a, X, IN["lout"], fld(bank, F_C))
+        a("s_branch %s" % lab_done)
+        a.label(lab_mem)
+        _soa_base(a, IN["leaves"], fld(bank, F_C))
+        lane_offset(a, T[0])
+        for j in range(8):
+            a("global_load_dword %s, %s, %s" % (v(X[j]), v(T[0]), sp(S_T)))
+            if j < 7:
+                _soa_step(a)
+        a("s_waitcnt vmcnt(0)")
+        a("s_branch %s" % lab_done)
+        a.hot()
+        a.flush_cold()
+        return
     a("s_bitcmp1_b32 %s, 0" % IN["mode"])
     a("s_cbranch_scc0 %s" % lab_mem)                 # (generator mode in line)
     _gen_leaf(a, bank)
