@@ -1096,6 +1096,23 @@ COMPILER = _os.environ.get("MYTHRIL_GPU_COMPILER", "native")
 # per program the share is at most 1.8 % on the C2 corpus and a median
 # 4.1 / 2.0 / 1.8 % on C3 / C4 / C5 (profiles/r04/remat_r4r/, remat_c2_r4/).
 AUTO_SCRATCH_SHARE = 0.02
+# ... and a program with (almost) no heavy arithmetic — multiply, division,
+# overflow test: the VALU-bound part of C2 — is compiled under "always"
+# (leaves never spilled, regenerated at each use: generator v9 and the
+# compiled leaf's one-flag path made that cheaper than any spill).  Final
+# round-4 kernel, whole workloads (profiles/r04/pol_r4/): "always" C3 / C4 /
+# C5 +19 / +19 / +6.6 % over the scratch rule, C2 -2.7 %; every C2 program
+# has >= 4 % heavy records, C3 / C4 / C5 programs at most 0.3 %.
+AUTO_ALWAYS_HEAVY = 0.01
+_HEAVY = (I.MUL, I.UDIV, I.UREM, I.SDIV, I.SREM, I.SMOD, I.UMULNO)
+
+
+def heavy_share(p: Program) -> float:
+    """Multiply / division / overflow-test records per instruction of ``p``."""
+    if not len(p.code):
+        return 0.0
+    op = p.code[:, 0] & 0xFF
+    return float(np.isin(op, _HEAVY).sum()) / len(p.code)
 
 
 def scratch_reload_share(p: Program, lds_tier: int = LDS_TIER) -> float:
@@ -1118,14 +1135,17 @@ def compile_constraints(constraints: Sequence[Node], probes: Sequence[Node] = ()
                         abi_presets: bool = False, leaf_remat: Optional[str] = None) -> Program:
     """Compile constraints (see :func:`compile_constraints_py`) with the
     compiler ``COMPILER`` names, under the leaf policy ``leaf_remat``
-    (default ``LEAF_REMAT``; "auto": see ``AUTO_SCRATCH_SHARE``)."""
+    (default ``LEAF_REMAT``; "auto": see ``AUTO_SCRATCH_SHARE`` and
+    ``AUTO_ALWAYS_HEAVY``)."""
     global LEAF_REMAT
     policy = leaf_remat or LEAF_REMAT
     if policy == "auto":
         args = (constraints, probes, table_sizes, default_entries, nreg, extra_consts,
                 leaf_pools, const_keys, solve, search_hints, abi_presets)
         p = compile_constraints(*args, leaf_remat="scratch2")
-        if scratch_reload_share(p) > AUTO_SCRATCH_SHARE:
+        if heavy_share(p) < AUTO_ALWAYS_HEAVY:
+            p = compile_constraints(*args, leaf_remat="always")
+        elif scratch_reload_share(p) > AUTO_SCRATCH_SHARE:
             p = compile_constraints(*args, leaf_remat="scratch")
         return p
     if COMPILER == "py":

@@ -201,23 +201,26 @@ def test_corpus_dag_with_leaf_pools_through_ir(dag_id):
 
 
 def test_auto_leaf_policy_picks_per_program():
-    """leaf_remat="auto" (the eval-mode batch compile): scratch2, unless the
-    program's 256-bit scratch reloads exceed ir.AUTO_SCRATCH_SHARE of its
-    instructions — then "scratch" (leaves regenerated, never in scratch)."""
+    """leaf_remat="auto" (the eval-mode batch compile): "always" for a
+    program with almost no heavy arithmetic (ir.AUTO_ALWAYS_HEAVY), else
+    scratch2, unless the program's 256-bit scratch reloads exceed
+    ir.AUTO_SCRATCH_SHARE of its instructions — then "scratch"."""
     import numpy as np
     import bench
     from mythril_amd import ir
-    switched = 0
-    for w, d in (("c2", 3), ("c3", 0), ("c3", 4), ("c3", 40)):
+    picked = []
+    for w, d in (("c2", 3), ("c2", 5), ("c3", 0), ("c3", 4), ("c4", 8)):
         roots = bench.workload_roots(w, d)
         auto = ir.compile_constraints(roots, leaf_remat="auto")
         s2 = ir.compile_constraints(roots, leaf_remat="scratch2")
-        over = ir.scratch_reload_share(s2) > ir.AUTO_SCRATCH_SHARE
-        want = ir.compile_constraints(roots, leaf_remat="scratch") if over else s2
+        if ir.heavy_share(s2) < ir.AUTO_ALWAYS_HEAVY:
+            pol = "always"
+        elif ir.scratch_reload_share(s2) > ir.AUTO_SCRATCH_SHARE:
+            pol = "scratch"
+        else:
+            pol = "scratch2"
+        want = ir.compile_constraints(roots, leaf_remat=pol)
         assert np.array_equal(auto.code, want.code) and np.array_equal(auto.consts, want.consts)
-        if over:
-            switched += 1
-            assert ir.scratch_reload_share(auto) < ir.scratch_reload_share(s2)
-        if w == "c2":
-            assert not over
-    assert switched >= 1
+        picked.append((w, pol))
+    assert all(p != "always" for w, p in picked if w == "c2")     # VALU-bound: spills stay
+    assert all(p == "always" for w, p in picked if w != "c2")
