@@ -95,12 +95,9 @@ def build_corpus(n_dags, workers, dag_ids=None, workload="c2", start="fork"):
     uses the GPU)."""
     ids = list(range(n_dags)) if dag_ids is None else list(dag_ids)
     items = [(workload, d) for d in ids]
-    if workers <= 1:
-        return [compile_unit(it) for it in items]
-    import multiprocessing as mp
-    ctx = mp.get_context(start)
-    with ctx.Pool(workers) as pool:
-        return sorted(pool.map(compile_unit, items, chunksize=16), key=lambda t: t[0])
+    from mythril_amd.procmap import process_map
+    return sorted(process_map(compile_unit, items, workers, start, chunksize=16),
+                  key=lambda t: t[0])
 
 
 def programs_digest(corpus) -> str:

@@ -77,6 +77,20 @@ typedef struct mg_gen {
     uint64_t first_index;   /* candidate index of the first lane (sharding) */
 } mg_gen;
 
+/* One context per (device, host thread).  SURVEY §8b proposed
+ * mg_init(uint32_t device_mask, ...) with one context owning several devices;
+ * this ABI deliberately takes ONE device index instead:
+ *   - the multi-GPU design is one process per GPU (bench.py under
+ *     torch.distributed.run) or, inside one process, one context per device
+ *     driven from its own host thread (mythril_amd/model.py
+ *     batch_search_devices: the C calls release the GIL), so a context never
+ *     has to fan a call out over devices itself;
+ *   - a context owns one stream, one workspace and one program cache, all
+ *     per device; a mask would need per-device copies of each behind one
+ *     handle and serialise the devices inside a call.
+ * A mask maps onto this by calling mg_init once per set bit.  Every entry
+ * point makes the context's device current (hipSetDevice) before it touches
+ * device memory, so one thread may drive contexts on different devices. */
 int mg_init(int device, mg_ctx** out);
 void mg_free(mg_ctx* ctx);
 const char* mg_last_error(const mg_ctx* ctx);

@@ -119,14 +119,17 @@ static uint64_t rec_fingerprint(const std::vector<uint32_t>& rec) {
 
 // The identity handler table: the translator then writes handler ids into
 // word 0 (fingerprinted, then mapped through the context's offsets).
+// Built once by a function-local static (thread-safe initialisation: two
+// contexts may load programs from two host threads at once).
 static const uint32_t* identity_handlers() {
-    static uint32_t t[MGA_NUM_HANDLERS];
-    static bool init = false;
-    if (!init) {
-        for (uint32_t h = 0; h < MGA_NUM_HANDLERS; ++h) t[h] = h;
-        init = true;
-    }
-    return t;
+    struct table {
+        uint32_t t[MGA_NUM_HANDLERS];
+        table() {
+            for (uint32_t h = 0; h < MGA_NUM_HANDLERS; ++h) t[h] = h;
+        }
+    };
+    static const table tab;
+    return tab.t;
 }
 
 static uint32_t kernel_lds_slots(const mg_ctx* ctx, uint32_t n_lds) {
@@ -237,10 +240,8 @@ static hipError_t ext_launched(mg_ctx* ctx, hipStream_t s) {
         }
     hipEvent_t ev = nullptr;
     hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e != hipSuccess) {                 // no event: fall back to waiting now
-        (void)hipStreamSynchronize(s);
-        return e;
-    }
+    if (e != hipSuccess)                   // no event: wait now; nothing stays pending
+        return hipStreamSynchronize(s);
     ctx->ext.push_back({s, ev, true});
     return hipEventRecord(ev, s);
 }
@@ -721,6 +722,10 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
                       uint64_t n_assign, uint64_t* d_root_bits, uint64_t* d_first_sat,
                       void* stream) {
     if (!ctx || !b) return fail(ctx, MG_E_ARG, "null argument");
+    if (b->ctx != ctx) return fail(ctx, MG_E_ARG, "batch belongs to another context");
+    // like every other entry point: the caller's thread may have another
+    // device current (two contexts on two devices driven from one thread)
+    HIPCHECK(ctx, hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     const uint64_t words = (n_assign + 63) / 64;
     for (uint32_t p0 = 0; p0 < b->n; p0 += 65535) {
@@ -742,6 +747,7 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
 int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand,
                     int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves) {
     if (!ctx || !b || !gen || (b->n && !first_sat)) return fail(ctx, MG_E_ARG, "null argument");
+    if (b->ctx != ctx) return fail(ctx, MG_E_ARG, "batch belongs to another context");
     if (witness_leaves && max_leaves < b->max_leaves)
         return fail(ctx, MG_E_ARG, "witness rows hold %u leaves, a program has %u", max_leaves,
                     b->max_leaves);

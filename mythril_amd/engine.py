@@ -30,7 +30,13 @@ EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_pro
 
 
 class EngineUnavailable(RuntimeError):
-    pass
+    """No usable engine; ``slot`` > 0 when only an extra context of a device
+    (model.DEVICES listing it again) could not be created."""
+
+    def __init__(self, msg: str = "", slot: int = 0, device: int = 0):
+        super().__init__(msg)
+        self.slot = slot
+        self.device = device
 
 
 class EngineError(RuntimeError):
@@ -367,7 +373,7 @@ def limbs_to_int(limbs) -> int:
 
 
 _engines: Dict[Tuple[int, int], Engine] = {}
-_failed: Dict[int, str] = {}
+_failed: Dict[Tuple[int, int], str] = {}
 _engines_lock = threading.Lock()
 
 
@@ -375,22 +381,25 @@ def get_engine(device: int = 0, slot: int = 0) -> Engine:
     """The engine (one HIP context) of ``device``; ``slot`` > 0 gives further
     independent contexts on the same device (a device listed twice in
     ``MYTHRIL_GPU_DEVICES`` is searched from two host threads, and a context
-    serves one thread at a time).  An initialisation failure is remembered,
-    so later calls raise EngineUnavailable at once instead of retrying
-    mg_init."""
+    serves one thread at a time).  An initialisation failure is remembered
+    per (device, slot), so later calls raise EngineUnavailable at once
+    instead of retrying mg_init; a failed extra slot (e.g. out of memory for
+    one more context) does not mark the device's first context failed, and
+    the exception carries ``slot`` so callers can tell the two apart."""
     with _engines_lock:
         e = _engines.get((device, slot))
         if e is None:
-            if device in _failed:
-                raise EngineUnavailable(_failed[device])
+            for key in ((device, 0), (device, slot)):
+                if key in _failed:
+                    raise EngineUnavailable(_failed[key], slot=key[1], device=device)
             try:
                 e = Engine(device)
             except EngineUnavailable as x:
-                _failed[device] = str(x)
-                raise
+                _failed[(device, slot)] = str(x)
+                raise EngineUnavailable(str(x), slot=slot, device=device) from x
             except Exception as x:  # noqa: BLE001 - any init failure means no engine
-                _failed[device] = "%s: %s" % (type(x).__name__, x)
-                raise EngineUnavailable(_failed[device]) from x
+                _failed[(device, slot)] = "%s: %s" % (type(x).__name__, x)
+                raise EngineUnavailable(_failed[(device, slot)], slot=slot, device=device) from x
             _engines[(device, slot)] = e
         return e
 

@@ -459,12 +459,20 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
             out = cold
             fallthrough = False
             continue
+        # code a folded-taken branch skipped (up to a label a kept branch
+        # reaches): nothing in it is emitted or changes the index state —
+        # only where later lines go (@@HALT / @@CALL end a hot block) is kept
+        skipped = dead and not fallthrough
         if t == "@@HALT":
-            emit("    s_setpc_b64 %s" % G.sp(G.JIT_RET))
+            if not skipped:
+                emit("    s_setpc_b64 %s" % G.sp(G.JIT_RET))
             out = cold
             fallthrough = False
             continue
         if t.startswith("@@CALL"):
+            if skipped:
+                out = cold
+                continue
             _, body, bits = t.split()
             kind = "DIV" if "DIV" in body else "UMULNO"
             # the body reads its record from S_CUR and its variant from S_VAR
@@ -510,6 +518,8 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
             emit(t)
             continue
         m, ops, mods = parse(t)
+        if skipped:
+            continue                         # the folded branch's skipped code
         # ---- GPR-index mode: resolved statically ----------------------------
         if m == "s_set_gpr_idx_on":
             r = sreg(ops[0])
@@ -1337,12 +1347,8 @@ def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
     with tempfile.TemporaryDirectory() as d:
         jobs = [(list(items[i:i + chunk]), i, lds_slots, os.path.join(d, "c%d.o" % i))
                 for i in range(0, len(items), chunk)]
-        if workers > 1 and len(jobs) > 1:
-            import multiprocessing as mp
-            with mp.get_context(start).Pool(min(workers, len(jobs))) as pool:
-                objs = pool.map(_chunk_job, jobs, chunksize=1)
-        else:
-            objs = [_chunk_job(j) for j in jobs]
+        from .procmap import process_map
+        objs = process_map(_chunk_job, jobs, workers, start)
         fps = [fp for _, f in objs for fp in f]
         objs = [o for o, _ in objs]
         tab = os.path.join(d, "table.o")

@@ -471,9 +471,19 @@ def search_groups(progs: Sequence[Program], n_cand: int):
     return _search_sets([progs], n_cand)
 
 
-def _search_sets(sets: Sequence[Sequence[Program]], n_cand: int):
+# How _search_sets answered a group (its ``kinds`` list): launched, folded to
+# a constant on the host, or skipped because a sibling group of its query
+# folded to false.
+SEARCHED, GROUND_TRUE, GROUND_FALSE, SKIPPED = "searched", "true", "false", "skipped"
+
+
+def _search_sets(sets: Sequence[Sequence[Program]], n_cand: int,
+                 kinds: Optional[List[str]] = None):
     """:func:`search_groups` over several queries' groups in ONE batched
-    search: a query with a group folded to false contributes no launch."""
+    search: a query with a group folded to false contributes no launch.
+    ``kinds`` (when given) receives, per group in output order, how it was
+    answered — only SEARCHED and GROUND_FALSE misses say anything about the
+    group itself (a SKIPPED group was never searched)."""
     ground = [[_ground_value(p) for p in progs] for progs in sets]
     dead = [any(g is False for g in gs) for gs in ground]
     stats.ground_false += sum(dead)
@@ -484,7 +494,17 @@ def _search_sets(sets: Sequence[Sequence[Program]], n_cand: int):
     out = []
     for gs, d in zip(ground, dead):
         for g in gs:
-            out.append((-1, None) if d else next(found) if g is None else (0, Assignment()))
+            if g is False:
+                kind, r = GROUND_FALSE, (-1, None)
+            elif d:
+                kind, r = SKIPPED, (-1, None)
+            elif g is None:
+                kind, r = SEARCHED, next(found)
+            else:
+                kind, r = GROUND_TRUE, (0, Assignment())
+            out.append(r)
+            if kinds is not None:
+                kinds.append(kind)
     return out
 
 
@@ -856,6 +876,28 @@ def _take(d: dict, key):
 _engine_failed: Optional[str] = None
 
 
+def _engine_failure(e: EngineUnavailable, current: Optional[str]) -> Optional[str]:
+    """What ``_engine_failed`` becomes after ``e``: a device's first context
+    failing disables the GPU path; an extra context (slot > 0, a device
+    listed twice in DEVICES) failing does not — that query falls back to z3,
+    the repeat is dropped from DEVICES and the device's working contexts
+    keep serving."""
+    global DEVICES
+    slot = getattr(e, "slot", 0)
+    if slot == 0:
+        return str(e)
+    # keep the device's working contexts (slots 0 .. slot-1) only
+    dev, kept, out = getattr(e, "device", 0), 0, []
+    for d in DEVICES:
+        if d == dev:
+            if kept >= slot:
+                continue
+            kept += 1
+        out.append(d)
+    DEVICES = out
+    return current
+
+
 def _prefilter(key, constraints, timeout: int, enforce_execution_time: bool = False):
     """GPU path of get_model: a model, or None (miss / rejected witness).
     The witness check gets what is left of the execution time (``_deadline``)."""
@@ -871,7 +913,7 @@ def _prefilter(key, constraints, timeout: int, enforce_execution_time: bool = Fa
         try:
             hit = gpu_search(nodes, budget_ms=min(timeout, SEARCH_BUDGET_MS))
         except EngineUnavailable as e:
-            _engine_failed = str(e)
+            _engine_failed = _engine_failure(e, _engine_failed)
             raise
         finally:
             stats.gpu_time += time.perf_counter() - t0
@@ -976,16 +1018,22 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
             t0 = time.perf_counter()
             flat = [p for _, progs in pending for p in progs]
             n_cand = _n_cand(flat, min(timeout, SEARCH_BUDGET_MS))
-            hits = iter(_search_sets([progs for _, progs in pending], n_cand))
+            kinds: List[str] = []
+            hits = iter(_search_sets([progs for _, progs in pending], n_cand, kinds))
+            kinds_it = iter(kinds)
             stats.gpu_time += time.perf_counter() - t0
             for cs, progs in pending:
                 found = [next(hits) for _ in progs]
+                how = [next(kinds_it) for _ in progs]
                 stats.gpu_queries += 1
-                stats.gpu_candidates += sum(n_cand if k < 0 else k + 1 for k, _ in found)
-                for p, (k, _) in zip(progs, found):
-                    if k < 0 and p.group_key is not None:
-                        _note_miss(p.group_key, GROUND_MISS if _ground_value(p) is False
-                                   else n_cand)
+                stats.gpu_candidates += sum(n_cand if k < 0 else k + 1
+                                            for (k, _), h in zip(found, how) if h == SEARCHED)
+                for p, (k, _), h in zip(progs, found, how):
+                    # only a group that was launched (or folded to false)
+                    # missed; a group skipped for a false sibling was not
+                    # searched, and its key must not block later queries
+                    if k < 0 and p.group_key is not None and h in (SEARCHED, GROUND_FALSE):
+                        _note_miss(p.group_key, GROUND_MISS if h == GROUND_FALSE else n_cand)
                 if any(k < 0 for k, _ in found):
                     # the set goes straight to z3 only when the batch searched
                     # it as far as get_model alone would have; otherwise
@@ -996,7 +1044,7 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
                     a = _merge([w for _, w in found])
                     _remember(_batch_witness, cs, (a, progs))
         except EngineUnavailable as e:
-            _engine_failed = str(e)
+            _engine_failed = _engine_failure(e, _engine_failed)
             log.debug("GPU pre-filter unavailable: %s", e)
         except Exception as e:  # noqa: BLE001
             stats.errors += 1

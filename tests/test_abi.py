@@ -39,3 +39,28 @@ def test_version_without_gpu():
 def test_ir_header_matches_python_table():
     from mythril_amd import irdefs
     assert irdefs.NUM_OPS == 37 and irdefs.ROOT == 32 and irdefs.CDWX == 36 and irdefs.TRASH == irdefs.NREG - 1
+
+
+def test_every_device_entry_point_sets_its_device():
+    """every exported entry point that touches device
+    memory or launches (HIP calls, launches, device blocks) makes its
+    context's device current first, so one host thread may drive contexts
+    on different devices.  Source scan of the C ABI (runs without a GPU)."""
+    import re
+    src = open(os.path.join(build.ROOT, "mythril_amd", "csrc", "mg_api.cpp")).read()
+    host_only = {"mg_version", "mg_config", "mg_translate", "mg_asm_digest", "mg_last_error",
+                 "mg_last_kernel_ms", "mg_runtime_info", "mg_init"}
+    bodies = {}
+    for m in re.finditer(r"^(?:int|void|float|const char\*) (mg_\w+)\([^;{]*\)\s*\{", src, re.M):
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"{": 1, "}": -1}.get(src[i], 0)
+            i += 1
+        bodies[m.group(1)] = src[m.end():i]
+    assert {"mg_batch_eval_gen", "mg_batch_search", "mg_load_program", "mg_eval"} <= set(bodies)
+    touches = re.compile(r"\bhip[A-Z]\w*\(|\blaunch\(|dev_alloc\(|dev_release\(|workspace\(")
+    missing = [f for f, b in bodies.items()
+               if f not in host_only and touches.search(b) and "hipSetDevice" not in b]
+    assert missing == []
+    # mg_init selects the device it is given
+    assert "hipSetDevice(device)" in bodies["mg_init"]

@@ -15,7 +15,6 @@ test checked lane by lane.
 """
 
 import ctypes as C
-import multiprocessing as mp
 import os
 
 import numpy as np
@@ -49,12 +48,14 @@ def _oracle_unit(item):
 def units():
     """Every bench unit of C2, C3 and C4 with its oracle root bits (spawned
     workers: this process may already hold the GPU)."""
+    from mythril_amd.procmap import process_map
     out = {}
-    ctx = mp.get_context("spawn")
-    with ctx.Pool(min(16, os.cpu_count() or 1)) as pool:
-        for w, n in FULL.items():
-            out[w] = sorted(pool.map(_oracle_unit, [(w, d) for d in range(n)], chunksize=8),
-                            key=lambda t: t[0])
+    for w, n in FULL.items():
+        # a worker that dies (an abort in the C oracle) raises
+        # BrokenProcessPool at once instead of hanging the module (round 4)
+        out[w] = sorted(process_map(_oracle_unit, [(w, d) for d in range(n)],
+                                    min(16, os.cpu_count() or 1), "spawn", chunksize=8),
+                        key=lambda t: t[0])
     return out
 
 

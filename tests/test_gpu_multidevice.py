@@ -15,7 +15,7 @@ import pytest
 
 import mythril_amd.model as M
 from mythril_amd import workloads as W
-from mythril_amd.engine import device_slots, get_engine
+from mythril_amd.engine import EngineError, device_slots, get_engine
 
 pytestmark = pytest.mark.gpu
 N_CAND = 1 << 20
@@ -101,3 +101,51 @@ def test_get_model_with_two_contexts(engine, two_contexts):
     assert (m1 is None) == (m2 is None)
     if m1 is not None:
         assert _same(m1.assignment, m2.assignment)
+
+
+def test_batch_eval_gen_sets_its_device_and_refuses_a_foreign_batch(engine, two_contexts):
+    """mg_batch_eval_gen makes its context's device
+    current like every other entry point, so a thread that last used another
+    context (here the second slot, on another host thread) still launches on
+    the right device and gets the one-context result; a batch created on one
+    context and launched through the other is refused (MG_E_ARG)."""
+    import ctypes as C
+    import threading
+    from mythril_amd.ir import compile_constraints
+    from mythril_amd.corpus import make_dag
+    hip = C.CDLL("libamdhip64.so.7", mode=C.RTLD_GLOBAL)
+    e0, e1 = get_engine(0, 0), get_engine(0, 1)
+    progs = [compile_constraints(make_dag(d)[0]) for d in (3, 17, 250)]
+    n, words = 1 << 14, (1 << 14) // 64
+    out = {}
+
+    def run(eng, tag):
+        loaded = [eng.load(p, prog_seed=k) for k, p in enumerate(progs)]
+        d_bits = C.c_void_p()
+        assert hip.hipMalloc(C.byref(d_bits), C.c_size_t(len(progs) * words * 8)) == 0
+        try:
+            b = eng.batch_create(loaded)
+            try:
+                hip.hipSetDevice(0)
+                eng.batch_eval_gen(b, 0x5EED, 64, n, d_bits.value)
+                hip.hipDeviceSynchronize()
+                host = np.zeros(len(progs) * words, np.uint64)
+                assert hip.hipMemcpy(host.ctypes.data_as(C.c_void_p), d_bits, C.c_size_t(host.nbytes), 2) == 0
+                out[tag] = host
+            finally:
+                eng.batch_free(b)
+        finally:
+            hip.hipFree(d_bits)
+
+    run(e0, "main")
+    t = threading.Thread(target=run, args=(e1, "thread"))
+    t.start()
+    t.join()
+    assert np.array_equal(out["main"], out["thread"])
+    loaded = [e0.load(p) for p in progs]
+    b = e0.batch_create(loaded)
+    try:
+        with pytest.raises(EngineError, match="another context"):
+            e1.batch_eval_gen(b, 1, 0, 64)
+    finally:
+        e0.batch_free(b)

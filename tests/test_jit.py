@@ -251,3 +251,29 @@ def test_branch_materializes_only_what_its_target_reads():
     assert "s_mov_b32 s81, 0x2a" in before          # the target's read, materialized
     assert "s_mov_b32 s80" not in text              # never materialized ...
     assert "s_cmp_lt_u32 s83, 52" in text           # ... the compare takes it inline
+
+
+def test_code_skipped_by_a_folded_branch_is_inert():
+    """after a branch folded as taken, the skipped code up to the
+    target emits nothing — a dynamic GPR index, a @@HALT or a @@CALL in it
+    neither raises JitUnsupported nor emits instructions or changes the index
+    state the target sees."""
+    from mythril_amd.jit import specialize
+    b = jit.BANK0
+    lines = [
+        "    s_cmp_eq_u32 s%d, 7" % b,                # rec[0] == 7: folds taken
+        "    s_cbranch_scc1 .Ltgt%=",
+        "    s_set_gpr_idx_on s90, gpr_idx(SRC0)",     # s90 unknown: dynamic index
+        "    v_mov_b32 v0, v8",
+        "    s_set_gpr_idx_off",
+        "@@CALL DIV 3",
+        "@@HALT",
+        ".Ltgt%=:",
+        "    v_mov_b32 v1, v2",
+    ]
+    rec = [7, 0, 0, 0, 0, 0, 0, 0]
+    hot, cold, call = specialize(lines, rec, "t")
+    text = "\n".join(hot + cold)
+    assert call is None
+    assert "s_setpc" not in text and "s_swappc" not in text and "gpr_idx" not in text
+    assert "v_mov_b32 v1, v2" in text and "v_mov_b32 v0" not in text

@@ -716,3 +716,41 @@ def test_constant_groups_are_answered_on_the_host(batch_env, monkeypatch):
     assert eng.batches == [] and M.stats.ground_false == 1 and len(z3_calls) == 1
     fkey = M._group_key(M.dependence_buckets(M._raw_nodes([f]))[0])
     assert M._group_miss[fkey] == M.GROUND_MISS
+
+
+def test_batch_is_possible_notes_misses_only_for_groups_it_searched(batch_env, monkeypatch):
+    """a set with a group folded to false launches
+    nothing, so its live and constant-true sibling groups were never
+    searched and must not enter the group-miss memo (a later query that
+    shares them would skip its search); the false group itself is a miss at
+    any depth."""
+    eng, z3_calls = batch_env
+    monkeypatch.setattr(M, "gpu_search", _REAL_GPU_SEARCH)
+    M.clear_search_memos()
+    bv = symbol_factory.BitVecVal
+    x = symbol_factory.BitVecSym("bx", 256)
+    t = bv(3, 8) == bv(3, 8)
+    f = bv(3, 8) == bv(4, 8)
+    live = ULT(x, bv(5, 256))
+    assert M.batch_is_possible([(f, live, t)], enforce_execution_time=False) == [False]
+    assert eng.batches == []
+    fkey = M._group_key(M.dependence_buckets(M._raw_nodes([f]))[0])
+    lkey = M._group_key(M.dependence_buckets(M._raw_nodes([live]))[0])
+    tkey = M._group_key(M.dependence_buckets(M._raw_nodes([t]))[0])
+    assert M._group_miss.get(fkey) == M.GROUND_MISS
+    assert lkey not in M._group_miss and tkey not in M._group_miss
+    # the live group alone is still searched (and found) afterwards
+    assert M.batch_is_possible([(live,)], enforce_execution_time=False) == [True]
+    assert eng.batches == [1]
+
+
+def test_extra_context_failure_keeps_the_gpu_path(batch_env, monkeypatch):
+    """with a device listed twice, failing to create its second
+    context (slot 1) drops that repeat and falls back for the query; it does
+    not disable the GPU path (only a slot-0 failure does)."""
+    from mythril_amd.engine import EngineUnavailable
+    monkeypatch.setattr(M, "DEVICES", [0, 0, 1])
+    monkeypatch.setattr(M, "_engine_failed", None)
+    assert M._engine_failure(EngineUnavailable("oom", slot=1, device=0), None) is None
+    assert M.DEVICES == [0, 1]
+    assert M._engine_failure(EngineUnavailable("no gpu", slot=0, device=0), None) == "no gpu"
