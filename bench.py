@@ -416,7 +416,7 @@ def main():
         achieved = ops_launch / (kern_ms / 1000.0)
         key = kernel_key(eng.lib.mg_asm_digest().decode(), args.workload, args.dags,
                          args.assign_log2, args.jit, corpus)
-        traffic, traffic_note = None, "no profiles/traffic.json"
+        traffic, traffic_note, sq = None, "no profiles/traffic.json", None
         if os.path.exists(args.traffic_json):
             try:
                 with open(args.traffic_json) as fh:
@@ -425,6 +425,7 @@ def main():
                 hit = next((e for e in entries if e.get("kernel_key") == key), None)
                 if hit is not None:
                     traffic = hit.get("hbm_bytes_per_launch")
+                    sq = hit.get("sq")
                     traffic_note = ("rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch of this "
                                     "kernel (profiles/traffic.json entry with the same "
                                     "kernel_key, %s)" % hit.get("evidence", "profiles/"))
@@ -468,7 +469,17 @@ def main():
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
                          "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kern_ms,
-                         "int32_ops_per_launch": ops_launch},
+                         "int32_ops_per_launch": ops_launch,
+                         # the executed-instruction view (SQ pass of this same
+                         # kernel_key, profiles/traffic.json "sq"): VALU lane-
+                         # instructions issued per second against the same
+                         # peak, and the share of SIMD cycles issuing VALU
+                         "valu_issue": (sq["valu_insts"] * 64 / (kern_ms / 1000.0) / VALU_PEAK_OPS
+                                        if sq and sq.get("valu_insts") else None),
+                         "valu_active": sq.get("valu_active") if sq else None,
+                         "valu_insts_per_node_eval": (sq["valu_insts"] * 64 /
+                                                      (nodes_per_lane * n_assign)
+                                                      if sq and sq.get("valu_insts") else None)},
             "kernel_key": key,
             "runtime": dict(eng.runtime_info(), torch_hip=getattr(torch.version, "hip", None),
                             note="the library's NEEDED libamdhip64.so.7 binds to the runtime "

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Summarise gpurun_out/prof[_<tag>] into profiles/<round>/[<tag>/] and
-profiles/traffic.json.
+profiles/traffic.json (HBM traffic and, since round 5, the SQ pass of the same
+kernel: bench.py reports both only for the kernel_key they were measured on).
 
 usage: tools/prof_summary.py <round> [<tag>]   (tag: the workload profiled
 by ``PROF_TAG=<tag> tools/profile.sh --workload <tag>``; none = the default
@@ -56,8 +57,64 @@ def bench_line(log):
     return None
 
 
+SIMDS = 256 * 4            # MI355X: 256 CUs x 4 SIMDs
+N_XCD = 8
+
+
+def sq_summary(path):
+    """SQ / GRBM counters of the dominant mg_interp dispatch of the SQ pass
+    (the bench launch; the handler-offset query launch is tiny), and what
+    they say per launch:
+      valu_insts      — SQ_INSTS_VALU, wave64 VALU instructions issued;
+      valu_active     — share of the SIMDs' cycles with a VALU instruction
+                        issuing: SQ_ACTIVE_INST_VALU counts quad-cycles
+                        (MI355X_MICROARCH.md), summed over waves, against
+                        GRBM_GUI_ACTIVE / 8 kernel cycles x 1024 SIMDs;
+      valu_active_per_wave — SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (times the
+                        resident waves per SIMD this is the same share when
+                        the SIMDs stay full)."""
+    per = {}
+    for r in csv.DictReader(open(path)):
+        if "mg_interp" in r["Kernel_Name"]:
+            d = per.setdefault(r["Dispatch_Id"], {})
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    if not per:
+        return None
+    c = max(per.values(), key=lambda d: d.get("SQ_WAVE_CYCLES", 0.0))
+    w = c.get("SQ_WAVES") or 1.0
+    summ = {k: c[k] for k in sorted(c)}
+    summ.update({"dispatches": len(per),
+                 "valu_insts": c.get("SQ_INSTS_VALU", 0.0),
+                 "valu_per_wave": c.get("SQ_INSTS_VALU", 0) / w,
+                 "salu_per_wave": c.get("SQ_INSTS_SALU", 0) / w,
+                 "smem_per_wave": c.get("SQ_INSTS_SMEM", 0) / w,
+                 "note": "the dominant mg_interp dispatch of the SQ pass (same bench "
+                         "configuration as the traffic passes); SQ_WAVE_CYCLES / SQ_WAIT_* / "
+                         "SQ_ACTIVE_INST_* count quad-cycles"})
+    if c.get("SQ_WAVE_CYCLES"):
+        summ["valu_active_per_wave"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"]
+        summ["salu_active_per_wave"] = c.get("SQ_ACTIVE_INST_SALU", 0) / c["SQ_WAVE_CYCLES"]
+        summ["wait_inst_per_wave"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
+    if c.get("GRBM_GUI_ACTIVE"):
+        cycles = c["GRBM_GUI_ACTIVE"] / N_XCD
+        summ["kernel_cycles"] = cycles
+        summ["valu_active"] = 4.0 * c.get("SQ_ACTIVE_INST_VALU", 0) / (cycles * SIMDS)
+    return summ
+
+
 fetch_kb = pmc("fetch/**/*counter_collection.csv", "FETCH_SIZE")
 write_kb = pmc("write/**/*counter_collection.csv", "WRITE_SIZE")
+sq = find("sq/**/*counter_collection.csv")
+for log in glob.glob(os.path.join(SRC, "*.log")):
+    shutil.copy(log, os.path.join(DST, os.path.basename(log)))
+summ = None
+if sq:
+    shutil.copy(sq, os.path.join(DST, "sq_counters.csv"))
+    summ = sq_summary(sq)
+    if summ is not None:
+        summ["kernel_key"] = (bench_line("sq.log") or {}).get("kernel_key")
+        json.dump(summ, open(os.path.join(DST, "sq_summary.json"), "w"), indent=1)
+        print("sq", json.dumps(summ))
 if fetch_kb is not None and write_kb is not None:
     # FETCH_SIZE / WRITE_SIZE are in KiB per dispatch; gfx950 FETCH_SIZE counts
     # wide streaming reads at half their bytes (MI355X_MICROARCH.md §HBM):
@@ -73,6 +130,13 @@ if fetch_kb is not None and write_kb is not None:
            "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, per mg_interp "
                    "dispatch of this bench config; read side doubled per the gfx950 "
                    "FETCH_SIZE correction (upper bound)"}
+    if summ is not None:
+        if summ.get("kernel_key") != keys[0]:
+            sys.exit("the SQ pass ran another kernel than the traffic passes: %s vs %s"
+                     % (summ.get("kernel_key"), keys[0]))
+        out["sq"] = {k: summ[k] for k in ("valu_insts", "valu_per_wave", "valu_active",
+                                          "valu_active_per_wave", "kernel_cycles",
+                                          "SQ_WAVES") if k in summ}
     path = "profiles/traffic.json"
     try:
         tj = json.load(open(path))
@@ -85,26 +149,3 @@ if fetch_kb is not None and write_kb is not None:
     entries = [e for e in entries if slot(e["kernel_key"]) != slot(out["kernel_key"])] + [out]
     json.dump({"entries": entries}, open(path, "w"), indent=1)
     print("traffic", out)
-sq = find("sq/**/*counter_collection.csv")
-if sq:
-    shutil.copy(sq, os.path.join(DST, "sq_counters.csv"))
-for log in glob.glob(os.path.join(SRC, "*.log")):
-    shutil.copy(log, os.path.join(DST, os.path.basename(log)))
-if sq:
-    c = {}
-    for r in csv.DictReader(open(sq)):
-        if "mg_interp" in r["Kernel_Name"]:
-            c[r["Counter_Name"]] = c.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    w = c.get("SQ_WAVES") or 1.0
-    summ = {k: c[k] for k in sorted(c)}
-    summ.update({"valu_per_wave": c.get("SQ_INSTS_VALU", 0) / w,
-                 "salu_per_wave": c.get("SQ_INSTS_SALU", 0) / w,
-                 "smem_per_wave": c.get("SQ_INSTS_SMEM", 0) / w,
-                 "note": "sums over the mg_interp dispatches of the SQ pass (C2: --dags 512); "
-                         "SQ cycle counters tick once per 4 shader cycles on CDNA"})
-    if c.get("SQ_WAVE_CYCLES"):
-        summ["valu_active_frac_of_wave_time"] = c.get("SQ_ACTIVE_INST_VALU", 0) / c["SQ_WAVE_CYCLES"]
-        summ["salu_active_frac_of_wave_time"] = c.get("SQ_ACTIVE_INST_SALU", 0) / c["SQ_WAVE_CYCLES"]
-        summ["wait_inst_frac_of_wave_time"] = c.get("SQ_WAIT_INST_ANY", 0) / c["SQ_WAVE_CYCLES"]
-    json.dump(summ, open(os.path.join(DST, "sq_summary.json"), "w"), indent=1)
-    print("sq", json.dumps(summ))

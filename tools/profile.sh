@@ -6,8 +6,8 @@
 # (bench.py --jit-build-only into $MYTHGPU_JIT_CACHE): a process the profiler
 # has attached to the GPU never starts the assembler.
 # usage: [PROF_TAG=c3] tools/profile.sh [bench args...]   (output in
-# gpurun_out/prof[_<tag>]; the SQ pass runs the C2 corpus at --dags 512, other
-# workloads at their bench size)
+# gpurun_out/prof[_<tag>]; every pass runs the bench's own configuration, so
+# the SQ counters are keyed to the same kernel as the traffic: round 5)
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 P=gpurun_out/prof${PROF_TAG:+_$PROF_TAG}
 mkdir -p $P
@@ -17,17 +17,16 @@ export MYTHGPU_JIT_CACHE=/tmp/mg_jitcache
 # signal handler (r4p6 WRITE_SIZE pass): profiled runs compile in-process
 export MYTHGPU_BENCH_WORKERS=1
 ARGS="$@"
-SQ_ARGS=${PROF_TAG:+$ARGS}
-SQ_ARGS=${SQ_ARGS:---dags 512}
 # a counter pass prints nothing for minutes: keep a heartbeat file moving
 # (gpurun's watchdog), stopped when the script ends
 ( while true; do date >> $P/heartbeat.txt; sleep 45; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 timeout -k 10 300 python3 bench.py --jit-build-only $ARGS > $P/prebuild.log 2>&1 || exit 1
-timeout -k 10 300 python3 bench.py --jit-build-only $SQ_ARGS > $P/prebuild_sq.log 2>&1 || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS > $P/kt.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/fetch -o fetch -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > $P/fetch.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -o write -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > $P/write.log 2>&1 || exit 1
-timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU --output-format csv -d $P/sq -o sq -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $SQ_ARGS > $P/sq.log 2>&1 || exit 1
+# SQ instruction / activity counters and GRBM_GUI_ACTIVE (the kernel's
+# cycles, summed over the 8 XCDs) in one pass: 8 SQ + 1 GRBM counters
+timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU GRBM_GUI_ACTIVE --output-format csv -d $P/sq -o sq -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > $P/sq.log 2>&1 || exit 1
 echo profile-ok
