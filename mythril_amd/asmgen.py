@@ -139,7 +139,7 @@ def canon_var(name: str, var: int) -> int:
         return var & (V_WAITD | 15) if (var & 15) < NREG else 0
     if name == "RELOADD":
         return var & (V_NARROW | V_WAITD | 15) if (var & 15) < NREG else 0
-    if name == "SPILL_SCR":
+    if name in ("SPILL_SCR", "SPILL_LDS", "RELOAD_LDS"):
         return var & (V_NARROW | 15) if (var & 15) < NREG else 0
     if name in SLOT_VARIANT:
         return var if var < NREG else 0      # the variant is the register slot
@@ -938,32 +938,48 @@ def h_sext(a, bank, root, mask, dc=False, w32=False, ip=False):
     dispatch(a, 1 - bank)
 
 
-def h_spill_lds(a: Asm, bank: int, slot: int):
-    """LDS spill straight from slot ``slot`` (the variant)."""
-    fa = FB + 8 * slot
+def h_spill_lds(a: Asm, bank: int, var: int):
+    """LDS spill straight from slot ``var & 15``; NARROW: a one-limb value,
+    one dword at the record's dword position of its region (the translator
+    packs one-limb values eight to a region, mg_host.cpp place_spills)."""
+    fa = FB + 8 * (var & 15)
     prologue(a, bank)
-    if JIT:       # the slot's byte offset is the record's: an instruction offset
+    if JIT:       # the halves' byte offsets are the record's: instruction offsets
+        if var & V_NARROW:
+            a("ds_write_b32 %s, v%d offset:@F%d@" % (OP_LDS, fa, F_IMM))
+            return dispatch(a, 1 - bank)
         a("ds_write_b128 %s, v[%d:%d] offset:@F%d@" % (OP_LDS, fa, fa + 3, F_IMM))
-        a("ds_write_b128 %s, v[%d:%d] offset:@F%d+4096@" % (OP_LDS, fa + 4, fa + 7, F_IMM))
+        a("ds_write_b128 %s, v[%d:%d] offset:@F%d@" % (OP_LDS, fa + 4, fa + 7, F_MOFF))
         return dispatch(a, 1 - bank)
     a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
+    if var & V_NARROW:
+        a("ds_write_b32 %s, v%d" % (v(T[0]), fa))
+        return dispatch(a, 1 - bank)
+    a("v_add_u32 %s, %s, %s" % (v(T[1]), s(fld(bank, F_MOFF)), OP_LDS))
     a("ds_write_b128 %s, v[%d:%d]" % (v(T[0]), fa, fa + 3))
-    a("ds_write_b128 %s, v[%d:%d] offset:4096" % (v(T[0]), fa + 4, fa + 7))
+    a("ds_write_b128 %s, v[%d:%d]" % (v(T[1]), fa + 4, fa + 7))
     dispatch(a, 1 - bank)
 
 
-def h_reload_lds(a: Asm, bank: int, slot: int):
-    """LDS reload straight into slot ``slot`` (the variant); the dispatch's
-    lgkmcnt wait covers the reads."""
-    fd = FB + 8 * slot
+def h_reload_lds(a: Asm, bank: int, var: int):
+    """LDS reload straight into slot ``var & 15``; the dispatch's lgkmcnt wait
+    covers the reads.  NARROW: one dword, limbs 1..7 zeroed."""
+    fd = FB + 8 * (var & 15)
     prologue(a, bank)
     if JIT:
-        a("ds_read_b128 v[%d:%d], %s offset:@F%d@" % (fd, fd + 3, OP_LDS, F_IMM))
-        a("ds_read_b128 v[%d:%d], %s offset:@F%d+4096@" % (fd + 4, fd + 7, OP_LDS, F_IMM))
+        lo, hi = (OP_LDS, " offset:@F%d@" % F_IMM), (OP_LDS, " offset:@F%d@" % F_MOFF)
+    else:
+        a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
+        lo = hi = (v(T[0]), "")
+        if not var & V_NARROW:
+            a("v_add_u32 %s, %s, %s" % (v(T[1]), s(fld(bank, F_MOFF)), OP_LDS))
+            hi = (v(T[1]), "")
+    if var & V_NARROW:
+        a("ds_read_b32 v%d, %s%s" % ((fd,) + lo))
+        moves(a, [fd + j for j in range(1, 8)], [None] * 7)
         return dispatch(a, 1 - bank)
-    a("v_add_u32 %s, %s, %s" % (v(T[0]), s(fld(bank, F_IMM)), OP_LDS))
-    a("ds_read_b128 v[%d:%d], %s" % (fd, fd + 3, v(T[0])))
-    a("ds_read_b128 v[%d:%d], %s offset:4096" % (fd + 4, fd + 7, v(T[0])))
+    a("ds_read_b128 v[%d:%d], %s%s" % ((fd, fd + 3) + lo))
+    a("ds_read_b128 v[%d:%d], %s%s" % ((fd + 4, fd + 7) + hi))
     dispatch(a, 1 - bank)
 
 

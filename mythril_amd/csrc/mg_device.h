@@ -6,6 +6,23 @@
 #include <stdint.h>
 #include "mythgpu.h"
 
+/* LDS spill area of one 256-lane block: n_lds REGIONS of 8 KiB, each two
+ * 4 KiB HALVES laid out [lane] x 16 B (conflict-free ds_*_b128).  The
+ * translator places a 256-bit value in any two free halves and a one-limb
+ * value in one dword of a half (mg_host.cpp place_spills).  With six regions
+ * (the default tier: 3 blocks x 48 KiB of the CU's 160 KiB) a 13th half
+ * fills the CU to 3 x 52 KiB. */
+#define MG_BLOCK_LANES 256u
+static inline uint32_t mg_lds_halves(uint32_t n_lds) {
+    return 2u * n_lds + (n_lds == 6u ? 1u : 0u);
+}
+static inline uint32_t mg_lds_half_offset(uint32_t h) {   /* byte offset of lane 0 */
+    return h * MG_BLOCK_LANES * 16u;
+}
+static inline uint32_t mg_lds_bytes(uint32_t n_lds) {
+    return mg_lds_halves(n_lds) * MG_BLOCK_LANES * 16u;
+}
+
 /* Device form of a leaf generator descriptor (mg_leafgen + host-computed
  * fields): 8 words, read by the kernels with one scalar load. */
 struct mg_leafgen_dev {

@@ -5,6 +5,7 @@
 // kernel from indexing outside the register file, the spill area, the
 // constant pool, the leaf table or the probe buffer.
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -102,6 +103,179 @@ static uint32_t slots_read(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint
     return d_operand ? m : m & ~(1u << d);
 }
 
+// ---- spill placement ----------------------------------------------------------
+//
+// The compiler numbers spill slots lowest-free; the translator decides where
+// each spilled VALUE lives (round 5).  An interval runs from a SPILL to the
+// last RELOAD of its slot before the slot's next SPILL.  Placement packs the
+// intervals into the n_lds LDS regions (8 KiB each: 8 dword positions per
+// lane, [half][lane] x 16 B) greedily by scratch bytes saved per unit of LDS
+// capacity x time: a 256-bit value takes a whole region for its interval, a
+// one-limb value (Bool results, values of <= 32 bits: limbs 1..7 are zero,
+// values being canonical) one dword position.  The rest goes to per-lane
+// scratch, re-coloured lowest-free in start order (the fewest 32-byte
+// scratch positions).  Every scratch spill is written back to HBM when its
+// L2 line is evicted (profiles/r05: WRITE_SIZE ~ the static scratch store
+// bytes) while reloads often hit L2, so what LDS takes off is mostly HBM
+// writes.  A SPILL whose slot is never reloaded is dropped.
+enum : uint32_t {
+    PL_SPILLREL = 1u << 31,   // a SPILL / RELOAD with a placement
+    PL_LDS = 1u << 30,        // in LDS (else scratch)
+    PL_NARROW = 1u << 29,     // one dword (reload zeroes limbs 1..7)
+    PL_DEAD = 1u << 28,       // a SPILL nobody reloads: emit nothing
+    PL_OFF = (1u << 28) - 1,  // byte offset (LDS: region/half/dword; scratch: 32 * position)
+};
+
+static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, uint32_t n_lds,
+                                          std::vector<uint32_t>& place2) {
+    struct Iv { uint32_t start, end, reloads; bool narrow; uint32_t loc, loc2; };
+    std::vector<uint32_t> place(n_ins, 0);
+    std::vector<Iv> ivs;
+    std::vector<int> open;                  // spill slot -> open interval (or -1)
+    std::vector<int> owner(n_ins, -1);      // SPILL / RELOAD instruction -> interval
+    bool narrow_reg[MG_NREG];
+    for (int k = 0; k < MG_NREG; ++k) narrow_reg[k] = false;
+    for (uint32_t i = 0; i < n_ins; ++i) {
+        const uint32_t* in = code + 4 * i;
+        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
+        const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF;
+        if (op == MG_SPILL) {
+            if (imm >= open.size()) open.resize(imm + 1, -1);
+            open[imm] = (int)ivs.size();
+#ifdef MG_NO_NARROW_SPILL                   /* A/B builds: every spill eight dwords */
+            ivs.push_back({i, i, 0, false, 0, 0});
+#else
+            ivs.push_back({i, i, 0, a < MG_NREG && narrow_reg[a], 0, 0});
+#endif
+            owner[i] = open[imm];
+            continue;
+        }
+        if (op == MG_RELOAD) {
+            const int k = imm < open.size() ? open[imm] : -1;
+            if (k >= 0) {
+                ivs[k].end = i;
+                ivs[k].reloads++;
+            }
+            owner[i] = k;
+            if (d < MG_NREG) narrow_reg[d] = k >= 0 ? ivs[k].narrow : w <= 32;
+            continue;
+        }
+        const bool writes = op != MG_NOP && op != MG_OUT && op != MG_ROOT;
+        if (writes && d < MG_NREG) narrow_reg[d] = is_compare(op) || w <= 32;
+    }
+    // LDS: 4-dword HALVES (half h: region h / 2, part h % 2, 4 KiB = 256
+    // lanes x 16 B).  A 256-bit value takes two free halves (any two: the
+    // record carries both offsets), a one-limb value one dword of a half.
+    // With six regions a 13th half fills the CU (mg_lds_bytes).  Three
+    // greedy orders (bytes saved per LDS capacity x time; bytes saved;
+    // start), the one leaving the fewest scratch bytes wins.
+    const uint32_t nhalf = mg_lds_halves(n_lds), npos = nhalf * 4;
+    std::vector<uint32_t> cand;
+    for (uint32_t k = 0; k < ivs.size(); ++k)
+        if (ivs[k].reloads) cand.push_back(k);
+    auto saved = [&](const Iv& v) { return (v.narrow ? 4.0 : 32.0) * (1.0 + v.reloads); };
+    auto density = [&](const Iv& v) {
+        return saved(v) / ((double)(v.end - v.start + 1) * (v.narrow ? 1.0 : 8.0));
+    };
+    std::vector<uint32_t> best_loc, best_loc2;
+    double best_cost = -1.0;
+    for (int pass = 0; pass < 3; ++pass) {
+        std::vector<uint32_t> byprio = cand;
+        if (pass == 0)
+            std::stable_sort(byprio.begin(), byprio.end(), [&](uint32_t x, uint32_t y) {
+                return density(ivs[x]) > density(ivs[y]);
+            });
+        else if (pass == 1)
+            std::stable_sort(byprio.begin(), byprio.end(), [&](uint32_t x, uint32_t y) {
+                return saved(ivs[x]) > saved(ivs[y]);
+            });
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> used(npos);
+        auto free_at = [&](uint32_t p, uint32_t s, uint32_t e) {
+            for (auto& u : used[p])
+                if (!(u.second < s || e < u.first)) return false;
+            return true;
+        };
+        auto half_free = [&](uint32_t h, uint32_t s, uint32_t e) {
+            for (uint32_t j = 0; j < 4; ++j)
+                if (!free_at(h * 4 + j, s, e)) return false;
+            return true;
+        };
+        auto half_load = [&](uint32_t h) {
+            int load = 0;
+            for (uint32_t j = 0; j < 4; ++j) load += (int)used[h * 4 + j].size();
+            return load;
+        };
+        std::vector<uint32_t> loc(ivs.size(), 0), loc2(ivs.size(), 0);
+        double cost = 0.0;
+        for (uint32_t k : byprio) {
+            const Iv& v = ivs[k];
+            bool placed = false;
+            if (!v.narrow) {
+                // the two free halves with the fewest narrow tenants
+                int h0 = -1, h1 = -1;
+                for (uint32_t h = 0; h < nhalf; ++h) {
+                    if (!half_free(h, v.start, v.end)) continue;
+                    if (h0 < 0 || half_load(h) < half_load((uint32_t)h0)) { h1 = h0; h0 = (int)h; }
+                    else if (h1 < 0 || half_load(h) < half_load((uint32_t)h1)) h1 = (int)h;
+                }
+                if (h0 >= 0 && h1 >= 0) {
+                    for (uint32_t j = 0; j < 4; ++j) {
+                        used[h0 * 4 + j].push_back({v.start, v.end});
+                        used[h1 * 4 + j].push_back({v.start, v.end});
+                    }
+                    loc[k] = PL_LDS | mg_lds_half_offset((uint32_t)h0);
+                    loc2[k] = mg_lds_half_offset((uint32_t)h1);
+                    placed = true;
+                }
+            } else {
+                // a free dword in the half already holding the most narrow
+                // intervals (keeps whole halves free for 256-bit values)
+                int best = -1, best_load = -1;
+                for (uint32_t p = 0; p < npos; ++p) {
+                    if (!free_at(p, v.start, v.end)) continue;
+                    const int load = half_load(p / 4);
+                    if (load > best_load) { best_load = load; best = (int)p; }
+                }
+                if (best >= 0) {
+                    used[best].push_back({v.start, v.end});
+                    loc[k] = PL_LDS | PL_NARROW |
+                             (mg_lds_half_offset((uint32_t)best / 4) + ((uint32_t)best % 4) * 4u);
+                    placed = true;
+                }
+            }
+            if (!placed) cost += (v.narrow ? 4.0 : 32.0) * (1.0 + 0.5 * v.reloads);
+        }
+        if (best_cost < 0.0 || cost < best_cost) {
+            best_cost = cost;
+            best_loc = loc;
+            best_loc2 = loc2;
+        }
+    }
+    for (uint32_t k = 0; k < ivs.size(); ++k) {
+        ivs[k].loc = best_loc.empty() ? 0u : best_loc[k];
+        ivs[k].loc2 = best_loc2.empty() ? 0u : best_loc2[k];
+    }
+    // scratch: lowest free 32-byte position at each interval's start
+    std::vector<uint32_t> scr_end;          // position -> end of its last interval
+    for (uint32_t k = 0; k < ivs.size(); ++k) {
+        Iv& v = ivs[k];
+        if (!v.reloads) { v.loc = PL_DEAD; continue; }
+        if (v.loc & PL_LDS) continue;
+        uint32_t p = 0;
+        while (p < scr_end.size() && scr_end[p] >= v.start) ++p;
+        if (p == scr_end.size()) scr_end.push_back(0);
+        scr_end[p] = v.end;
+        v.loc = (v.narrow ? PL_NARROW : 0u) | p * 32u;
+    }
+    place2.assign(n_ins, 0);
+    for (uint32_t i = 0; i < n_ins; ++i)
+        if (owner[i] >= 0) {
+            place[i] = PL_SPILLREL | ivs[owner[i]].loc;
+            place2[i] = ivs[owner[i]].loc2;
+        }
+    return place;
+}
+
 void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
                       uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
     pool.base = n_consts;
@@ -112,17 +286,13 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
     // at most 32 bits); registers start uninitialised
     bool clean[MG_NREG];
     for (int k = 0; k < MG_NREG; ++k) clean[k] = false;
-    // narrow_spill[s]: scratch spill slot s holds a one-limb value (limb 0
-    // stored only; its reloads zero limbs 1..7).  A reload never moves above
-    // the spill of its slot (the hoisting below), so the flag is set first.
-    // (slots past 2^16, which no validated program has, stay wide)
-    std::vector<char> narrow_spill;
-    auto set_narrow = [&](uint32_t k, bool v) {
-        if (k >= (1u << 16)) return;
-        if (k >= narrow_spill.size()) narrow_spill.resize(k + 1, 0);
-        narrow_spill[k] = v;
+    // where every spilled value lives (LDS region / dword, or scratch), per
+    // SPILL / RELOAD instruction (place_spills)
+    std::vector<uint32_t> place2;           // a 256-bit LDS value's second half
+    const std::vector<uint32_t> place = place_spills(code, n_ins, n_lds, place2);
+    auto scratch_reload = [&](uint32_t i) {
+        return (code[4 * i] & 0xFF) == MG_RELOAD && !(place[i] & PL_LDS);
     };
-    auto is_narrow = [&](uint32_t k) { return k < narrow_spill.size() && narrow_spill[k]; };
     // slots whose LEAFD loads may still be in flight: a WAITVM record goes
     // before the first instruction that reads or writes one of them
     uint32_t pending = 0;
@@ -155,7 +325,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
     for (uint32_t q = 0; q < n_ins; ++q) {
         const uint32_t* in = code + 4 * order[q];
         const bool leafd = (in[0] & 0xFF) == MG_LEAF && ((in[0] >> 8) & 0x3FF) == 256;
-        if (!leafd && ((in[0] & 0xFF) != MG_RELOAD || in[2] < n_lds)) continue;
+        if (!leafd && !scratch_reload(order[q])) continue;
         const uint32_t rd = in[1] & 0xFF, slot = leafd ? 0xFFFFFFFFu : in[2];
         uint32_t t = q;
         while (t > 0 && q - t < 24) {
@@ -181,7 +351,9 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             break;
         }
         const uint32_t* in = code + 4 * order[pc];
-        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, imm = in[2];
+        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF;
+        const uint32_t pl = place[order[pc]];
+        if (op == MG_SPILL && (pl & PL_DEAD)) continue;     // never reloaded
         const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
                        c = (in[1] >> 24) & 0xFF;
         // a store-chain link: t = (a == b) of wide values, consumed only by
@@ -216,14 +388,16 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             }
         }
         const bool leafd = op == MG_LEAF && w == 256;
-        const bool reloadd = op == MG_RELOAD && imm >= n_lds;
+        const bool reloadd = op == MG_RELOAD && !(pl & PL_LDS);
         if (pending && (slots_touched(op, d, a, b, c) & pending)) wait_vm();
         if (leafd || reloadd) pending |= 1u << d;
         uint32_t* r = emit();
         uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
         const bool writes = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
         // result fits one limb: Bool results, or values of at most 32 bits
-        const bool narrow = is_compare(op) || (writes && w <= 32);
+        // (a reload: the placement's view of the spilled value)
+        const bool narrow = is_compare(op) || (writes && w <= 32) ||
+                            (op == MG_RELOAD && (pl & PL_NARROW));
         const bool w32 = has_w32(op) && w <= 32;       // compares: w = operand width
         if (w32) var |= MGA_V_W32;
         if (writes && narrow && clean[d]) var |= MGA_V_DC;
@@ -232,32 +406,23 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         int aop = MGA_NOP;
         switch (op) {
         case MG_NOP: aop = MGA_NOP; break;
-        case MG_CONST: aop = MGA_CONST; r[5] = imm * 32u; break;
+        case MG_CONST: aop = MGA_CONST; r[5] = in[2] * 32u; break;
         case MG_LEAF:
-            aop = MGA_LEAF; r[4] = imm;
+            aop = MGA_LEAF; r[4] = in[2];
             if (leafd) { aop = MGA_LEAFD; var = d; }
             else if (maskv) { var |= MGA_V_MASK; r[7] = pool.add(mask_lt(w)); }
             break;
         case MG_SPILL:              // spills and reloads: the variant is the slot
-            if (imm < n_lds) { aop = MGA_SPILL_LDS; var = a; r[5] = imm * 2u * 256u * 16u; }
-            else {                  // a one-limb value: one dword of scratch traffic
-                aop = MGA_SPILL_SCR; var = a; r[5] = (imm - n_lds) * 32u;
-#ifdef MG_NO_NARROW_SPILL                   /* A/B builds: every spill eight dwords */
-                const bool nf = false;
-#else
-                const bool nf = clean[a] && imm - n_lds < (1u << 16);
-#endif
-                set_narrow(imm - n_lds, nf);
-                if (nf) var |= MGA_V_NARROW;
-            }
+        case MG_RELOAD: {           // (| NARROW: one dword, limbs 1..7 zero)
+            const bool lds = pl & PL_LDS;
+            const bool nf = pl & PL_NARROW;
+            if (op == MG_SPILL) { aop = lds ? MGA_SPILL_LDS : MGA_SPILL_SCR; var = a; }
+            else { aop = lds ? MGA_RELOAD_LDS : MGA_RELOADD; var = d; }
+            if (nf) var |= MGA_V_NARROW;
+            r[5] = (pl & PL_SPILLREL) ? (pl & PL_OFF) : 0u;
+            if (lds && !nf) r[7] = place2[order[pc]];     // limbs 4..7 (second half)
             break;
-        case MG_RELOAD:
-            if (imm < n_lds) { aop = MGA_RELOAD_LDS; var = d; r[5] = imm * 2u * 256u * 16u; }
-            else {
-                aop = MGA_RELOADD; var = d; r[5] = (imm - n_lds) * 32u;
-                if (is_narrow(imm - n_lds)) var |= MGA_V_NARROW;
-            }
-            break;
+        }
         case MG_ADD: aop = MGA_ADD; goto masked;
         case MG_SUB: aop = MGA_SUB; goto masked;
         case MG_MUL: aop = MGA_MUL; goto masked;
@@ -286,7 +451,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         case MG_ITE: aop = MGA_ITE; break;
         case MG_CONCAT: {           // R = a << imm | b: static limb shift in the variant
             aop = MGA_CONCATQ;
-            const uint32_t q = imm >> 5, bs = imm & 31;
+            const uint32_t q = in[2] >> 5, bs = in[2] & 31;
             var = q | (bs ? 8u : 0u);
             r[4] = 8 * a + 8 - q - (bs ? 1 : 0);
             r[5] = bs ? 32 - bs : 0;
@@ -294,8 +459,8 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             break;
         }
         case MG_EXTRACT:            // R = (a >> imm) & mask(w)
-            r[4] = 8 * a + (imm >> 5) + 8;
-            r[5] = imm & 31;
+            r[4] = 8 * a + (in[2] >> 5) + 8;
+            r[5] = in[2] & 31;
             if (w > 32) {           // static result limbs; top-limb mask inline
                 aop = MGA_EXTRACTN;
                 var = (w + 31) / 32 - 1;
@@ -307,13 +472,13 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             break;
         case MG_SEXT: {             // from imm bits to w bits: 16-word mask entry
             aop = MGA_SEXT;
-            r[5] = imm;
-            std::vector<uint32_t> m = mask_lt(imm), m2 = mask_lt(w);
+            r[5] = in[2];
+            std::vector<uint32_t> m = mask_lt(in[2]), m2 = mask_lt(w);
             m.insert(m.end(), m2.begin(), m2.end());
             r[7] = pool.add(m);
             break;
         }
-        case MG_OUT: aop = MGA_OUT; r[4] = imm; break;
+        case MG_OUT: aop = MGA_OUT; r[4] = in[2]; break;
         case MG_ROOT: aop = MGA_ROOT; break;
         case MG_MOV: aop = MGA_MOV; break;
         case MG_BCAST: aop = MGA_BCAST; var = 0; break;

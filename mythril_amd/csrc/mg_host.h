@@ -12,6 +12,7 @@
 #include "mythgpu.h"
 #include "mythgpu_ir.h"
 #include "mg_asm_handlers.h"
+#include "mg_device.h"
 
 #define MG_VERSION 3
 

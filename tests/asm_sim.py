@@ -865,6 +865,27 @@ class Wave:
                     self._check(("v", src + i))
                     struct.pack_into("<I", self.lds, int(addr[l]) + off + 4 * i, int(self.v[src + i][l]))
 
+    def i_ds_write_b32(self, a, pc):
+        addr = self.vread(a[0], valu=False)
+        src, _ = self.vidx(a[1], None, False)
+        off = self._soff(a[2]) if len(a) > 2 else 0
+        act = self._act()
+        self._check(("v", src))
+        for l in range(NL):
+            if act[l]:
+                struct.pack_into("<I", self.lds, int(addr[l]) + off, int(self.v[src][l]))
+
+    def i_ds_read_b32(self, a, pc):
+        dst, _ = self.vidx(a[0], None, False)
+        addr = self.vread(a[1], valu=False)
+        off = self._soff(a[2]) if len(a) > 2 else 0
+        act = self._act()
+        vals = [struct.unpack_from("<I", self.lds, int(addr[l]) + off)[0] for l in range(NL)]
+
+        def apply():
+            self.v[dst] = np.where(act, np.array(vals, dtype=np.uint64), self.v[dst])
+        self._defer("lgkm", ("v", dst), apply)
+
     def i_ds_read_b128(self, a, pc):
         dst, _ = self.vidx(a[0], None, False)
         addr = self.vread(a[1], valu=False)

@@ -5,6 +5,7 @@ hot kernel) through an instruction-level simulator of its exact text
 the oracle (oracle/smtlib_ref.py, oracle/gen_ref.py); the same cases run on
 the MI355X in test_gpu_parity.py."""
 
+import collections
 import random
 
 import numpy as np
@@ -296,3 +297,35 @@ def test_index_mode_text_invariants():
             assert not (op.startswith("v_") or op.startswith("ds_") or
                         op.startswith("global_") or op.startswith("scratch_") or
                         op.startswith("s_cbranch") or op == "s_branch"), (t, u)
+
+
+@pytest.mark.parametrize("workload,unit,n_lds,jit", [("c3", 16, 6, False), ("c3", 16, 6, True),
+                                                     ("c3", 40, 2, True), ("c5", 33, 6, True),
+                                                     ("c4", 9, 6, False)])
+def test_spill_placement_stand_in_units(workload, unit, n_lds, jit):
+    """Spill placement (mg_host.cpp place_spills, round 5): one-limb values
+    packed eight to an LDS region, 256-bit values in whole regions, the rest
+    in re-coloured scratch positions, spills nobody reloads dropped.  A bench
+    unit of the spill-heaviest stand-in workloads, interpreted and compiled,
+    must give the oracle's root bit on every lane, and its records must use
+    the narrow LDS and scratch variants."""
+    import bench
+    from mythril_amd import asmgen
+    from mythril_amd.engine import translate_records
+    _, prog, _, _ = bench.compile_unit((workload, unit))
+    rec, _ = translate_records(prog, n_lds)
+    fams = collections.Counter()
+    for h in rec.reshape(-1, 8)[:, 0]:
+        name, var = asmgen.AOPS[int(h) // (2 * asmgen.NVAR)], (int(h) // 2) % asmgen.NVAR
+        fams[(name, bool(var & asmgen.V_NARROW) if name in (
+            "SPILL_LDS", "RELOAD_LDS", "SPILL_SCR", "RELOADD") else False)] += 1
+    assert fams[("SPILL_LDS", True)] and fams[("RELOAD_LDS", True)] and fams[("SPILL_SCR", False)]
+    lg = default_leafgen(prog)
+    first = 64 * 1001 + unit
+    root, _, lout, _ = asm_sim.simulate(prog, gen=(SEED, unit, first, lg), n_lds=n_lds,
+                                        want_leaves=True, jit=jit)
+    roots = bench.workload_roots(workload, unit)
+    for lane in range(64):
+        asg = unpack(prog, lout[:, :, lane])
+        want = R.eval_constraints(list(roots), R.Assignment(asg.vars, asg.arrays, asg.funcs))
+        assert bool(root[lane]) == bool(want), lane
