@@ -241,7 +241,10 @@ class World:
         return t
 
     def query(self, extra: Sequence[S.Bool] = ()) -> List[N.Node]:
-        return [c.raw for c in list(self.constraints) + list(extra)]
+        q = Query(c.raw for c in list(self.constraints) + list(extra))
+        if extra:                              # a module's check: "open" unless labelled
+            q.label = _CHECK_LABELS.pop(id(extra[-1]), "open")
+        return q
 
 
 class Tx:
@@ -367,6 +370,34 @@ BEC_FUNCS = sorted(selector(s) for s in (
 _BAL, _ALLOW, _OWNER_PAUSED, _TOTAL = 1, 2, 3, 0
 
 
+# Ground-truth labels of the integer module's checks: a
+# check the path itself rules out — SafeMath's own ``require`` on the same
+# operands, appended before the query is posed — is UNSAT by construction and
+# its label names that require; any other check is "open" (satisfiable or not:
+# tests/planted.py looks for a model).  The label belongs to the check as
+# created on its path (the wrapper object: hash-consing gives the same node to
+# the same check expression on different paths, e.g. BECToken's multiply
+# check after one or two receivers); the query streams do not depend on it.
+_CHECK_LABELS: Dict[int, str] = {}
+
+
+def _label(chk: S.Bool, label: str) -> S.Bool:
+    _CHECK_LABELS[id(chk)] = label
+    return chk
+
+
+class Query(list):
+    """One query (a list of Bool DAG nodes, what get_model receives) with the
+    generator's label: "unsat: <the require that rules it out>", "open" (a
+    check nothing on the path rules out) or "path" (an is_possible query)."""
+
+    label = "path"
+
+
+def query_label(q: Sequence[N.Node]) -> str:
+    return getattr(q, "label", "path")
+
+
 def _when_not_paused(t: Tx) -> None:
     packed = t.sload(bv(_OWNER_PAUSED))                        # owner | paused << 160
     paused = bv(0xFF) & S.UDiv(packed, bv(1 << 160))
@@ -391,12 +422,14 @@ def _bec_transfer(t: Tx, checks: List[S.Bool], from_arg: bool) -> None:
         t.require(S.Not(S.UGT(value, allow)))
     # SafeMath.sub: assert(b <= a); SUB annotated by the integer module
     t.require(S.Not(S.UGT(value, bal_from)))
-    checks.append(S.Not(S.BVSubNoUnderflow(bal_from, value, False)))
+    checks.append(_label(S.Not(S.BVSubNoUnderflow(bal_from, value, False)),
+                         "unsat: SafeMath.sub require(value <= balances[from])"))
     t.sstore(slot_from, bal_from - value)
     slot_to = t.mapping(to, _BAL)
     bal_to = t.sload(slot_to)
     s = bal_to + value
-    checks.append(S.Not(S.BVAddNoOverflow(bal_to, value, False)))
+    checks.append(_label(S.Not(S.BVAddNoOverflow(bal_to, value, False)),
+                         "unsat: SafeMath.add require(balances[to] + value >= balances[to])"))
     t.require(S.Not(S.ULT(s, bal_to)))                         # SafeMath.add: assert(c >= a)
     t.sstore(slot_to, s)
 
@@ -409,20 +442,28 @@ def _bec_batch(t: Tx, checks: List[S.Bool], receivers: int) -> None:
     cnt = t.calldata.word(off + bv(4))                          # _receivers.length
     value = t.arg(1)
     amount = cnt * value
-    checks.append(S.Not(S.BVMulNoOverflow(cnt, value, False)))
+    # the loop leaves after `receivers` iterations (i < cnt not taken), so
+    # cnt <= receivers: one receiver cannot overflow cnt * value; two can
+    # (the BEC bug: cnt = 2, value = 2^255)
+    checks.append(_label(S.Not(S.BVMulNoOverflow(cnt, value, False)),
+                         "open" if receivers >= 2 else
+                         "unsat: loop exit (i < cnt not taken after 1 receiver) gives cnt <= 1"))
     t.require(S.And(S.UGT(cnt, bv(0)), S.Not(S.UGT(cnt, bv(20)))))
     slot_s = t.mapping(t.sender(), _BAL)
     bal_s = t.sload(slot_s)
     t.require(S.And(S.UGT(value, bv(0)), S.Not(S.ULT(bal_s, amount))))
     t.require(S.Not(S.UGT(amount, bal_s)))
-    checks.append(S.Not(S.BVSubNoUnderflow(bal_s, amount, False)))
+    checks.append(_label(S.Not(S.BVSubNoUnderflow(bal_s, amount, False)),
+                         "unsat: SafeMath.sub require(amount <= balances[sender])"))
     t.sstore(slot_s, bal_s - amount)
     for i in range(receivers):
         t.jumpi(S.ULT(bv(i), cnt), taken=True)                 # for (i < cnt)
         rcv = bv(ADDR_MASK) & t.calldata.word(off + bv(36 + 32 * i))
         slot_r = t.mapping(rcv, _BAL)
         bal_r = t.sload(slot_r)
-        checks.append(S.Not(S.BVAddNoOverflow(bal_r, value, False)))
+        checks.append(_label(S.Not(S.BVAddNoOverflow(bal_r, value, False)),
+                             "unsat: SafeMath.add require(balances[receiver] + value >= "
+                             "balances[receiver])"))
         t.require(S.Not(S.ULT(bal_r + value, bal_r)))
         t.sstore(slot_r, bal_r + value)
     t.jumpi(S.ULT(bv(receivers), cnt), taken=False)
@@ -438,7 +479,8 @@ def _bec_approve(t: Tx, checks: List[S.Bool], increase: bool) -> None:
     slot = t.sha3(S.Concat(spender, outer))                     # allowed[owner][spender]
     if increase:
         cur = t.sload(slot)
-        checks.append(S.Not(S.BVAddNoOverflow(cur, value, False)))
+        checks.append(_label(S.Not(S.BVAddNoOverflow(cur, value, False)),
+                             "unsat: SafeMath.add require(allowed + value >= allowed)"))
         t.require(S.Not(S.ULT(cur + value, cur)))
         t.sstore(slot, cur + value)
     else:
