@@ -89,6 +89,20 @@ def shape_lines(eng, n_queries, n_sample=48):
         for qi, (i, _) in zip(qmap, hits):
             solved[qi] = solved[qi] and i >= 0
         needed = sum(n_cand if i < 0 else i + 1 for i, _ in hits)
+        # recall against the ground-truth labels (tests/golden/recall_labels.json:
+        # planted models for SAT, the generator's SafeMath requires for UNSAT)
+        recall = None
+        lab_path = os.path.join(ROOT, "tests", "golden", "recall_labels.json")
+        if os.path.exists(lab_path):
+            rows = json.load(open(lab_path))["streams"].get(name, [])
+            lab = {r["i"]: r["label"] for r in rows if r["i"] < len(qs)}
+            sat = [i for i, l in lab.items() if l == "sat"]
+            recall = {"sat_labelled": len(sat), "found": sum(solved[i] for i in sat),
+                      "recall": sum(solved[i] for i in sat) / max(1, len(sat)),
+                      "missed": [i for i in sat if not solved[i]],
+                      "unsat_labelled": sum(l == "unsat" for l in lab.values()),
+                      "unsat_found": sum(solved[i] for i, l in lab.items() if l == "unsat"),
+                      "unknown_found": sum(solved[i] for i, l in lab.items() if l == "unknown")}
         ins_cand = sum((n_cand if i < 0 else i + 1) * p.n_ins for (i, _), p in zip(hits, progs))
         # the drop-in get_model, one query at a time (no z3 here: a miss
         # raises SolverUnavailable after the GPU search): "cold" compiles
@@ -145,6 +159,7 @@ def shape_lines(eng, n_queries, n_sample=48):
                                            for b in (8, 12, 16, 18, 20)}},
             "get_model": cold,
             "get_model_stream": stream,
+            "recall": recall,
         }
     return out
 
