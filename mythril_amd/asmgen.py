@@ -2179,6 +2179,9 @@ DIV_Z6 = 54                     # lanes with vn[0..5] == 0 (bank B)
 DIV_STAGE_SKIP = int(os.environ.get("MYTHGPU_DIV_STAGE_SKIP", "6"))
 DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm:
                                 # unused by division)
+# the one-limb short division's second ("unlikely") quotient correction behind
+# a branch (round 5; A/B knob: MYTHGPU_DIV_SHORT_BRANCH=0 is the round-4 step)
+DIV_SHORT_BRANCH = os.environ.get("MYTHGPU_DIV_SHORT_BRANCH", "1") != "0"
 
 
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
@@ -2305,8 +2308,9 @@ def _udivrem_short(a: Asm, want_rem: bool, z: int):
     remainder = r >> b.  Same contract as udivrem: lanes with Y == 0 divide
     0 by 1 (s[z:z+1] marks them).  Registers: d = Y0, b = T2, c / r = T3,
     A = T4:T5, P = T6:T7, CR = T8, dinv = T10, QH = T11."""
-    d, b, c, r, dinv = Y[0], T[2], T[3], T[3], T[10]
-    A0, A1, P0, CR, QH = T[4], T[5], T[6], T[8], T[11]
+    d, b, c, dinv = Y[0], T[2], T[3], T[10]
+    A0, A1, Q0, Q1, CR, t, QH = T[4], T[5], T[6], T[7], T[8], T[9], T[11]
+    r = A1                        # the running remainder, hi half of the mad addend
     bz = S_T + 4
     a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(d)))                   # Y == 0
     a("v_cndmask_b32_e64 %s, %s, 1, %s" % (v(d), v(d), sp(z)))
@@ -2320,10 +2324,48 @@ def _udivrem_short(a: Asm, want_rem: bool, z: int):
     a("v_mov_b32 %s, 0" % v(R[0]))
     bitshift_left(a, X + [R[0]], c, bz, 9, S_T)                       # u = X << b
     _reciprocal(a, d, dinv)
+    if not DIV_SHORT_BRANCH:
+        return _udivrem_short_r4(a, want_rem, z)
     a("v_mov_b32 %s, %s" % (v(r), v(R[0])))                           # r = u[8] < d
     lt = sp(S_T + 2)
     for j in reversed(range(8)):
-        # (A1:A0) = dinv * r + (r:u[j]); q = A1 + 1; r' = u[j] - q * d
+        # Moller-Granlund 2-by-1 (their Algorithm 4): (Q1:Q0) = dinv * r +
+        # (r:u[j]); q = Q1 + 1; r' = u[j] - q * d; r' > Q0: q--, r' += d.  The
+        # second correction (r' >= d: q++, r' -= d) is the paper's "unlikely"
+        # one: a branch over it (round 5: 14 -> 10 VALU per digit; the
+        # remainder stays in the addend's high half, r = A1)
+        a("v_mov_b32 %s, %s" % (v(A0), v(X[j])))
+        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (Q0, Q1, sp(S_T + 6), v(dinv), v(r),
+                                                           A0, A1))
+        a("v_add_u32 %s, 1, %s" % (v(QH), v(Q1)))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(t), v(QH), v(d)))
+        a("v_sub_u32 %s, %s, %s" % (v(CR), v(A0), v(t)))
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (lt, v(CR), v(Q0)))           # r' > q0: q--, r' += d
+        a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(R[j]), sp(S_T + 4), v(QH), lt))
+        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(t), v(d), lt))
+        a("v_add_u32 %s, %s, %s" % (v(r), v(CR), v(t)))
+        a("v_cmp_ge_u32 vcc, %s, %s" % (v(r), v(d)))                     # r' >= d: q++, r' -= d
+        skip = a.uniq("dss")
+        a("s_cbranch_vccz %s" % skip)
+        lab = exec_begin(a, None, S_T + 2)
+        a("v_add_u32 %s, 1, %s" % (v(R[j]), v(R[j])))
+        a("v_sub_u32 %s, %s, %s" % (v(r), v(r), v(d)))
+        exec_end(a, lab, S_T + 2)
+        a.label(skip)
+    if want_rem:
+        a("v_lshrrev_b32 %s, %s, %s" % (v(X[0]), v(b), v(r)))
+        moves(a, X[1:], [None] * 7)
+
+
+def _udivrem_short_r4(a: Asm, want_rem: bool, z: int):
+    """The round-4 digit loop of _udivrem_short (both corrections in line,
+    14 VALU per digit), kept for the A/B knob; entered after the common
+    normalisation and reciprocal."""
+    d, b, r, dinv = Y[0], T[2], T[3], T[10]
+    A0, A1, P0, CR, QH = T[4], T[5], T[6], T[8], T[11]
+    a("v_mov_b32 %s, %s" % (v(r), v(R[0])))
+    lt = sp(S_T + 2)
+    for j in reversed(range(8)):
         a("v_mov_b32 %s, %s" % (v(A0), v(X[j])))
         a("v_mov_b32 %s, %s" % (v(A1), v(r)))
         a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (A0, A1, sp(S_T + 6), v(dinv), v(r),
@@ -2331,11 +2373,11 @@ def _udivrem_short(a: Asm, want_rem: bool, z: int):
         a("v_add_u32 %s, 1, %s" % (v(QH), v(A1)))
         a("v_mul_lo_u32 %s, %s, %s" % (v(P0), v(QH), v(d)))
         a("v_sub_u32 %s, %s, %s" % (v(CR), v(X[j]), v(P0)))
-        a("v_cmp_gt_u32_e64 %s, %s, %s" % (lt, v(CR), v(A0)))           # r' > q0: q--, r' += d
+        a("v_cmp_gt_u32_e64 %s, %s, %s" % (lt, v(CR), v(A0)))
         a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(QH), sp(S_T + 4), v(QH), lt))
         a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), lt))
         a("v_add_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
-        a("v_cmp_ge_u32_e64 %s, %s, %s" % (lt, v(CR), v(d)))            # r' >= d: q++, r' -= d
+        a("v_cmp_ge_u32_e64 %s, %s, %s" % (lt, v(CR), v(d)))
         a("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (v(R[j]), sp(S_T + 4), v(QH), lt))
         a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), lt))
         a("v_sub_u32 %s, %s, %s" % (v(r), v(CR), v(P0)))

@@ -6,6 +6,7 @@
 // constant pool, the leaf table or the probe buffer.
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -162,6 +163,27 @@ static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, 
         }
         const bool writes = op != MG_NOP && op != MG_OUT && op != MG_ROOT;
         if (writes && d < MG_NREG) narrow_reg[d] = is_compare(op) || w <= 32;
+    }
+    // A/B knob (MYTHGPU_SPILL_PLACE=0): the round-4 rule — a spill slot
+    // below n_lds is one whole LDS region, the rest scratch at its own slot
+    static const bool legacy = [] {
+        const char* e = getenv("MYTHGPU_SPILL_PLACE");
+        return e && e[0] == '0';
+    }();
+    if (legacy) {
+        for (uint32_t i = 0; i < n_ins; ++i) {
+            if (owner[i] < 0) continue;
+            const Iv& v = ivs[owner[i]];
+            const uint32_t slot = code[4 * i + 2];
+            uint32_t loc = slot < n_lds ? PL_LDS | mg_lds_half_offset(2 * slot)
+                                        : (v.narrow ? PL_NARROW : 0u) | (slot - n_lds) * 32u;
+            place[i] = PL_SPILLREL | loc;
+            if (slot < n_lds) place[i] &= ~PL_NARROW;
+        }
+        place2.assign(n_ins, 0);
+        for (uint32_t i = 0; i < n_ins; ++i)
+            if (owner[i] >= 0 && code[4 * i + 2] < n_lds) place2[i] = mg_lds_half_offset(2 * code[4 * i + 2] + 1);
+        return place;
     }
     // LDS: 4-dword HALVES (half h: region h / 2, part h % 2, 4 KiB = 256
     // lanes x 16 B).  A 256-bit value takes two free halves (any two: the

@@ -112,6 +112,37 @@ def test_division_one_limb_waves(rep):
         assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
 
 
+# (d, u1, u0) where the Moller-Granlund 2-by-1 step (r:u) = (u1:u0) needs
+# its second, "unlikely" correction (r' >= d): found by brute force over the
+# algorithm restated in Python (round 5 moved that correction behind a branch)
+MG_SECOND_CORRECTION = [(2322326124, 2251310039, 4214312352), (2267272354, 2057016691, 4168275397),
+                        (2996589211, 2755454550, 4001446354)]
+
+
+def test_short_division_second_correction():
+    """The one-limb short division's rare second quotient correction: lanes
+    that need it, lanes that do not, in one wave, at several digit positions
+    (a normalised divisor, so the step sees (u1:u0) itself, and shifted
+    divisors, which move it)."""
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    probes = [N.bv_op("bvudiv", x, y), N.bv_op("bvurem", x, y)]
+    prog = compile_constraints([], probes)
+    rng = random.Random(7)
+    asgs = []
+    for lane in range(64):
+        d, u1, u0 = MG_SECOND_CORRECTION[lane % 3]
+        pos = rng.randrange(7)
+        xv = ((u1 << 32) | u0) << (32 * pos) | rng.getrandbits(32 * pos)
+        if lane % 5 == 4:
+            xv, d = rng.getrandbits(256), rng.getrandbits(32) | 1
+        asgs.append(PA(vars={"x": xv, "y": d}))
+    root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+    for a, asg in enumerate(asgs):
+        want = R.evaluate(probes, R.Assignment(asg.vars))
+        got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+        assert got == want, (a, hex(asg.vars["x"]), hex(asg.vars["y"]))
+
+
 @pytest.mark.parametrize("small", ["y", "x", "both", "none"])
 def test_mul_short_operand_waves(small):
     """MUL waves whose operands are below 2^64 in every lane (either side,
