@@ -16,6 +16,7 @@ sources are newer."""
 
 from __future__ import annotations
 
+import collections.abc as _abc
 import ctypes
 import json
 import os
@@ -259,12 +260,59 @@ def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
     return _program(code, raw, ncv.value, meta)
 
 
+class LeafRecords(_abc.Sequence):
+    """``Program.leaves`` of a native compile, decoded on first use: the
+    compiler sends them as one string ("name TAB width TAB kind TAB source TAB
+    chunk TAB entry" per line) plus their widths.  A search that misses —
+    most compiles of a LASER stream — only needs the count and the widths
+    (``model.search_leafgen``); a big search group has hundreds of leaves."""
+
+    __slots__ = ("_rs", "_items", "widths")
+
+    def __init__(self, rs: str, widths: Sequence[int]):
+        self._rs = rs
+        self._items = None
+        self.widths = list(widths)
+
+    def _decode(self):
+        from .ir import Leaf
+        items = []
+        if self.widths:
+            for line in self._rs.split("\n"):
+                name, w, kind, source, chunk, entry = line.split("\t")
+                items.append(Leaf(name, int(w), kind, source, int(chunk), int(entry)))
+        self._items = items
+        self._rs = None
+        return items
+
+    def __len__(self):
+        return len(self.widths)
+
+    def __getitem__(self, i):
+        return (self._items if self._items is not None else self._decode())[i]
+
+    def __iter__(self):
+        return iter(self._items if self._items is not None else self._decode())
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self):
+        return repr(list(self))
+
+    def __reduce__(self):               # pickled (compile workers) as the list
+        return (list, (list(self),))
+
+
 def _program(code, raw: bytes, ncv: int, meta):
     from . import ir
     consts = np.frombuffer(raw, dtype="<u4").reshape(-1, 8).astype(np.uint32)
     const_values = [int.from_bytes(raw[32 * i:32 * i + 32], "little") for i in range(ncv)]
     Leaf = ir.Leaf
-    leaves = [Leaf(*row) for row in meta["leaves"]]
+    if meta.get("leaves_rs") is not None:
+        leaves = LeafRecords(meta["leaves_rs"], meta["leaf_widths"])
+    else:
+        leaves = [Leaf(*row) for row in meta["leaves"]]
     hist_counts = dict(meta["hist"])
     stats = {"lnodes": meta["lnodes"], "n_ins": int(code.shape[0]), "spills": meta["spills"],
              "reloads": meta["reloads"],

@@ -2702,6 +2702,8 @@ static void jstr(std::string& o, const std::string& s) {
     o.push_back('"');
     for (unsigned char ch : s) {
         if (ch == '"' || ch == '\\') { o.push_back('\\'); o.push_back((char)ch); }
+        else if (ch == '\n') o += "\\n";
+        else if (ch == '\t') o += "\\t";
         else if (ch < 0x20) { char b[8]; std::snprintf(b, sizeof b, "\\u%04x", ch); o += b; }
         else o.push_back((char)ch);
     }
@@ -2980,17 +2982,55 @@ static void compile(const mgc_input* in, mgc_result* res) {
     tp[7] = now_us();
     // -- metadata ---------------------------------------------------------------
     std::string& o = res->meta;
-    o = "{\"leaves\":[";
+    // the leaves as ONE string, "name TAB width TAB kind TAB source TAB chunk
+    // TAB entry" records separated by newlines: a big search group has
+    // hundreds of leaves, and a caller that never unpacks a witness (a miss)
+    // never needs more than their count and widths (ccompile.LeafRecords
+    // splits it on first use); the widths also come as their own list
+    bool plain = true;                       // no separator inside a name
+    for (const Leaf& L : lw.leaves)
+        plain = plain && L.name.find_first_of("\t\n") == std::string::npos &&
+                L.source.find_first_of("\t\n") == std::string::npos;
+    if (!plain) {
+        o = "{\"leaves\":[";
+        for (size_t i = 0; i < lw.leaves.size(); i++) {
+            const Leaf& L = lw.leaves[i];
+            if (i) o += ",";
+            o += "[";
+            jstr(o, L.name);
+            o += "," + std::to_string(L.width) + ",";
+            jstr(o, KIND_NAMES[L.kind]);
+            o += ",";
+            jstr(o, L.source);
+            o += "," + std::to_string(L.chunk) + "," + std::to_string(L.entry) + "]";
+        }
+        o += "],\"leaves_rs\":null";
+    } else {
+        o = "{\"leaves_rs\":";
+    }
+    if (plain) {
+        std::string rs;
+        for (size_t i = 0; i < lw.leaves.size(); i++) {
+            const Leaf& L = lw.leaves[i];
+            if (i) rs += '\n';
+            rs += L.name;
+            rs += '\t';
+            rs += std::to_string(L.width);
+            rs += '\t';
+            rs += KIND_NAMES[L.kind];
+            rs += '\t';
+            rs += L.source;
+            rs += '\t';
+            rs += std::to_string(L.chunk);
+            rs += '\t';
+            rs += std::to_string(L.entry);
+        }
+        jstr(o, rs);
+    }
+    o += ",\"leaf_widths\":[";
     for (size_t i = 0; i < lw.leaves.size(); i++) {
-        const Leaf& L = lw.leaves[i];
         if (i) o += ",";
-        o += "[";
-        jstr(o, L.name);
-        o += "," + std::to_string(L.width) + ",";
-        jstr(o, KIND_NAMES[L.kind]);
-        o += ",";
-        jstr(o, L.source);
-        o += "," + std::to_string(L.chunk) + "," + std::to_string(L.entry) + "]";
+        o += std::to_string(lw.leaves[i].width);
     }
     o += "],\"n_lds\":" + std::to_string(al.n_lds);
     o += ",\"n_probes\":" + std::to_string(probe_chunks);

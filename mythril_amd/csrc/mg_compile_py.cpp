@@ -23,7 +23,7 @@
 
 namespace {
 
-PyObject *s_op, *s_sort, *s_width, *s_dom, *s_args, *s_params, *s_id;
+PyObject *s_op, *s_sort, *s_width, *s_dom, *s_args, *s_params, *s_id, *s_enc;
 
 struct Flat {
     std::vector<int32_t> op, sort, width, dom, arg_off{0}, args, str, cval_off;
@@ -64,66 +64,62 @@ bool str_of(PyObject* v, Flat& f, int32_t& out) {
     return true;
 }
 
-// one node's own fields (operands already indexed)
-bool add_node(PyObject* node, PyObject* ops, int other, Flat& f) {
+// A node's own fields as the walk needs them, computed once per node and
+// cached on it (Node._enc): (op code, sort code, width, dom, id, p0, p1,
+// name or None, numeral limbs as bytes or None).  Nodes are immutable and
+// hash-consed, so a LASER stream's later queries, which share most of their
+// DAG with earlier ones, read one tuple per node instead of seven attributes.
+PyObject* encode(PyObject* node, PyObject* ops, int other) {
     PyObject* op = attr(node, s_op);
-    if (!op) return false;
+    if (!op) return nullptr;
     PyObject* code = PyDict_GetItemWithError(ops, op);         // borrowed
     int c = code ? (int)PyLong_AsLong(code) : other;
-    if (PyErr_Occurred()) { Py_DECREF(op); return false; }
+    if (PyErr_Occurred()) { Py_DECREF(op); return nullptr; }
     Py_ssize_t oplen;
     const char* opname = PyUnicode_AsUTF8AndSize(op, &oplen);
-    if (!opname) { Py_DECREF(op); return false; }
+    if (!opname) { Py_DECREF(op); return nullptr; }
     std::string name(opname, (size_t)oplen);
-    Py_DECREF(op);
 
     PyObject* sort = attr(node, s_sort);
-    if (!sort) return false;
+    if (!sort) { Py_DECREF(op); return nullptr; }
     int sc;
     if (PyUnicode_CompareWithASCIIString(sort, "bv") == 0) sc = MGC_SORT_BV;
     else if (PyUnicode_CompareWithASCIIString(sort, "bool") == 0) sc = MGC_SORT_BOOL;
     else sc = MGC_SORT_ARRAY;
     Py_DECREF(sort);
     long long width, dom, id;
-    if (!as_long(node, s_width, width) || !as_long(node, s_dom, dom) || !as_long(node, s_id, id)) return false;
-
-    PyObject* args = attr(node, s_args);
-    if (!args) return false;
-    PyObject* seq = PySequence_Fast(args, "args");
-    Py_DECREF(args);
-    if (!seq) return false;
-    Py_ssize_t na = PySequence_Fast_GET_SIZE(seq);
-    for (Py_ssize_t i = 0; i < na; i++) {
-        auto it = f.index.find(PySequence_Fast_GET_ITEM(seq, i));
-        if (it == f.index.end()) {
-            Py_DECREF(seq);
-            PyErr_SetString(PyExc_RuntimeError, "operand visited after its user");
-            return false;
-        }
-        f.args.push_back(it->second);
+    if (!as_long(node, s_width, width) || !as_long(node, s_dom, dom) || !as_long(node, s_id, id)) {
+        Py_DECREF(op);
+        return nullptr;
     }
-    Py_DECREF(seq);
-
     PyObject* params = attr(node, s_params);
-    if (!params) return false;
+    if (!params) { Py_DECREF(op); return nullptr; }
     PyObject* ps = PySequence_Fast(params, "params");
     Py_DECREF(params);
-    if (!ps) return false;
+    if (!ps) { Py_DECREF(op); return nullptr; }
     Py_ssize_t np_ = PySequence_Fast_GET_SIZE(ps);
     PyObject** pv = PySequence_Fast_ITEMS(ps);
     long long p0 = 0, p1 = 0;
-    int32_t str = -1, cv = -1;
+    PyObject* str = Py_None;
+    PyObject* cval = Py_None;
+    Py_INCREF(Py_None);
+    Py_INCREF(Py_None);
     bool ok = true;
     if (name == "bvnum" && np_ >= 1) {
         size_t nl = (size_t)(width + 31) / 32;
-        cv = (int32_t)f.cval.size();
-        f.cval.resize(f.cval.size() + nl, 0);
-        ok = _PyLong_AsByteArray((PyLongObject*)pv[0], (unsigned char*)(f.cval.data() + cv), 4 * nl, 1, 0) == 0;
+        std::vector<unsigned char> buf(4 * nl, 0);
+        ok = _PyLong_AsByteArray((PyLongObject*)pv[0], buf.data(), buf.size(), 1, 0) == 0;
+        if (ok) {
+            Py_DECREF(cval);
+            cval = PyBytes_FromStringAndSize((const char*)buf.data(), (Py_ssize_t)buf.size());
+            ok = cval != nullptr;
+        }
     } else if ((name == "var" || name == "array") && np_ >= 1) {
-        ok = str_of(pv[0], f, str);
+        Py_DECREF(str); str = pv[0]; Py_INCREF(str);
     } else if (name == "apply" && np_ >= 2) {
-        ok = str_of(pv[0], f, str);
-        if (ok) { p0 = PyLong_AsLongLong(pv[1]); ok = !PyErr_Occurred(); }
+        Py_DECREF(str); str = pv[0]; Py_INCREF(str);
+        p0 = PyLong_AsLongLong(pv[1]);
+        ok = !PyErr_Occurred();
     } else if (name == "extract" && np_ >= 2) {
         p0 = PyLong_AsLongLong(pv[0]);
         p1 = PyLong_AsLongLong(pv[1]);
@@ -132,10 +128,59 @@ bool add_node(PyObject* node, PyObject* ops, int other, Flat& f) {
         p0 = PyLong_AsLongLong(pv[0]);
         ok = !PyErr_Occurred();
     } else if (c == other) {
-        str = f.intern(name.data(), (Py_ssize_t)name.size());
+        Py_DECREF(str); str = op; Py_INCREF(str);
     }
     Py_DECREF(ps);
-    if (!ok) return false;
+    Py_DECREF(op);
+    if (!ok) { Py_XDECREF(str); Py_XDECREF(cval); return nullptr; }
+    PyObject* t = Py_BuildValue("(iiLLLLLNN)", c, sc, width, dom, id, p0, p1, str, cval);
+    if (t && PyObject_SetAttr(node, s_enc, t) < 0) PyErr_Clear();   // a node without the slot
+    return t;
+}
+
+// one node's own fields (operands already indexed; `seq` its args as a fast
+// sequence)
+bool add_node(PyObject* node, PyObject* seq, PyObject* ops, int other, Flat& f) {
+    PyObject* t = PyObject_GetAttr(node, s_enc);
+    if (!t) {
+        PyErr_Clear();
+        t = encode(node, ops, other);
+        if (!t) return false;
+    }
+    if (!PyTuple_Check(t) || PyTuple_GET_SIZE(t) != 9) {
+        Py_DECREF(t);
+        PyErr_SetString(PyExc_TypeError, "Node._enc is not a walk record");
+        return false;
+    }
+    const int c = (int)PyLong_AsLong(PyTuple_GET_ITEM(t, 0));
+    const int sc = (int)PyLong_AsLong(PyTuple_GET_ITEM(t, 1));
+    const long long width = PyLong_AsLongLong(PyTuple_GET_ITEM(t, 2));
+    const long long dom = PyLong_AsLongLong(PyTuple_GET_ITEM(t, 3));
+    const long long id = PyLong_AsLongLong(PyTuple_GET_ITEM(t, 4));
+    const long long p0 = PyLong_AsLongLong(PyTuple_GET_ITEM(t, 5));
+    const long long p1 = PyLong_AsLongLong(PyTuple_GET_ITEM(t, 6));
+    PyObject* so = PyTuple_GET_ITEM(t, 7);
+    PyObject* co = PyTuple_GET_ITEM(t, 8);
+    if (PyErr_Occurred()) { Py_DECREF(t); return false; }
+    Py_ssize_t na = PySequence_Fast_GET_SIZE(seq);
+    for (Py_ssize_t i = 0; i < na; i++) {
+        auto it = f.index.find(PySequence_Fast_GET_ITEM(seq, i));
+        if (it == f.index.end()) {
+            Py_DECREF(t);
+            PyErr_SetString(PyExc_RuntimeError, "operand visited after its user");
+            return false;
+        }
+        f.args.push_back(it->second);
+    }
+    int32_t str = -1, cv = -1;
+    if (so != Py_None && !str_of(so, f, str)) { Py_DECREF(t); return false; }
+    if (co != Py_None) {
+        const Py_ssize_t nb = PyBytes_GET_SIZE(co);
+        cv = (int32_t)f.cval.size();
+        f.cval.resize(f.cval.size() + (size_t)nb / 4, 0);
+        std::memcpy(f.cval.data() + cv, PyBytes_AS_STRING(co), (size_t)nb);
+    }
+    Py_DECREF(t);
     f.op.push_back(c);
     f.sort.push_back(sc);
     f.width.push_back((int32_t)width);
@@ -178,9 +223,11 @@ bool walk(PyObject* root, PyObject* ops, int other, Flat& f) {
         }
         {
             PyObject* n = it.node;
-            Py_DECREF(it.seq);
+            PyObject* seq = it.seq;
             stack.pop_back();
-            if (!add_node(n, ops, other, f)) goto fail;
+            const bool ok = add_node(n, seq, ops, other, f);
+            Py_DECREF(seq);
+            if (!ok) goto fail;
         }
     }
     return true;
@@ -412,5 +459,6 @@ PyMODINIT_FUNC PyInit__mythcc(void) {
     s_args = PyUnicode_InternFromString("args");
     s_params = PyUnicode_InternFromString("params");
     s_id = PyUnicode_InternFromString("id");
+    s_enc = PyUnicode_InternFromString("_enc");
     return PyModule_Create(&module);
 }

@@ -122,7 +122,8 @@ def default_leafgen(program: Program, pct=(50, 70, 85)) -> List[LeafGen]:
     """C2 value distribution: 50 % uniform, 20 % < 2^64, 15 %
     boundary values, 15 % DAG constants +-1 (pool = the program's constants)."""
     n_c = len(program.const_values)
-    return [LeafGen(l.width, 0, n_c, pct[0], pct[1], pct[2]) for l in program.leaves]
+    widths = getattr(program.leaves, "widths", None) or [l.width for l in program.leaves]
+    return [LeafGen(w, 0, n_c, pct[0], pct[1], pct[2]) for w in widths]
 
 
 class LoadedProgram:

@@ -291,10 +291,12 @@ def search_leafgen(prog: Program) -> List[LeafGen]:
     compared with (ir._leaf_pools); otherwise from every constant of the
     query."""
     n_c = len(prog.const_values)
+    # (the widths alone: a native compile's leaves are decoded only when a
+    # witness is unpacked, ccompile.LeafRecords)
+    widths = getattr(prog.leaves, "widths", None) or [l.width for l in prog.leaves]
     if prog.pool_ranges:
-        return [LeafGen(l.width, off, n, 20, 40, 60)
-                for l, (off, n) in zip(prog.leaves, prog.pool_ranges)]
-    return [LeafGen(l.width, 0, n_c, 20, 40, 60) for l in prog.leaves]
+        return [LeafGen(w, off, n, 20, 40, 60) for w, (off, n) in zip(widths, prog.pool_ranges)]
+    return [LeafGen(w, 0, n_c, 20, 40, 60) for w in widths]
 
 
 _SEARCH_CACHE: "OrderedDict[tuple, Program]" = None

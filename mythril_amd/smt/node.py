@@ -33,7 +33,9 @@ class Node:
     """One DAG node.  ``width`` is the bit-width for BV, 1 for BOOL and the
     range width for ARRAY (``dom`` holds the domain width)."""
 
-    __slots__ = ("op", "sort", "width", "dom", "args", "params", "id", "_h")
+    # _enc: the native compiler's walk record of this node (set on its first
+    # walk, csrc/mg_compile_py.cpp encode)
+    __slots__ = ("op", "sort", "width", "dom", "args", "params", "id", "_h", "_enc")
 
     def __init__(self, op, sort, width, dom, args, params):
         self.op = op
