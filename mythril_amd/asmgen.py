@@ -2179,6 +2179,9 @@ DIV_Z6 = 54                     # lanes with vn[0..5] == 0 (bank B)
 DIV_STAGE_SKIP = int(os.environ.get("MYTHGPU_DIV_STAGE_SKIP", "6"))
 DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm:
                                 # unused by division)
+# a wave whose divisors all have their top limb set jumps straight to quotient
+# digit 0 (round 5; A/B knob: MYTHGPU_DIV_J0=0 tests every digit)
+DIV_J0_JUMP = os.environ.get("MYTHGPU_DIV_J0", "1") != "0"
 # the one-limb short division's second ("unlikely") quotient correction behind
 # a branch (round 5; A/B knob: MYTHGPU_DIV_SHORT_BRANCH=0 is the round-4 step)
 DIV_SHORT_BRANCH = os.environ.get("MYTHGPU_DIV_SHORT_BRANCH", "1") != "0"
@@ -2281,8 +2284,21 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     d = vn[7]
     _reciprocal(a, d, dinv)
     a("v_mov_b32 %s, 0" % v(T[9]))                                  # RH of the digit loop
+    # a lane whose divisor moved q limbs has un[k] = 0 for k >= 9 + q and
+    # un[8 + q] < 2^b <= d, so its quotient digits j > q are zero and their
+    # tests below skip; when no lane moved its divisor (a wave of full-width
+    # divisors; zero divisors excluded, they divide 0) only digit 0 can be
+    # nonzero: one scalar test instead of seven per-digit VALU tests (round 5)
+    lab_j0 = a.uniq("dj0")
+    if DIV_J0_JUMP:
+        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(DIV_M[4]), sp(DIV_M[2])))
+        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(DIV_M[1])))
+        a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(z)))
+        a("s_cbranch_scc0 %s" % lab_j0)
     for j in reversed(range(8)):
         u2, u1 = un[j + 8], un[j + 7]
+        if j == 0:
+            a.label(lab_j0)
         skip = a.uniq("dvs")
         a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(u2)))
         a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(u1), v(d)))
