@@ -422,7 +422,38 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
                             (op == MG_RELOAD && (pl & PL_NARROW));
         const bool w32 = has_w32(op) && w <= 32;       // compares: w = operand width
         if (w32) var |= MGA_V_W32;
-        if (writes && narrow && clean[d]) var |= MGA_V_DC;
+        // a one-limb result whose every reader (until the slot is written
+        // again) reads limb 0 only — one-limb (W32) ops, an ITE's condition,
+        // ROOT, a one-dword spill — need not zero limbs 1..7 either: the DC
+        // handler (limb 0 only) serves, and the slot is then marked dirty
+        // (round 5; the Bool results of compares are the common case)
+        static const bool dirty_dc = [] {          // A/B knob MYTHGPU_DIRTY_DC=0: off
+            const char* e = getenv("MYTHGPU_DIRTY_DC");
+            return !(e && e[0] == '0');
+        }();
+        bool dirty = false;
+        if (dirty_dc && writes && narrow && !clean[d] && d < MG_NREG) {
+            dirty = true;
+            bool read = false;
+            for (uint32_t q = pc + 1; q < n_ins && dirty; ++q) {
+                const uint32_t* f = code + 4 * order[q];
+                const uint32_t fop = f[0] & 0xFF, fw = (f[0] >> 8) & 0x3FF, fd = f[1] & 0xFF,
+                               fa = (f[1] >> 8) & 0xFF, fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
+                const uint32_t rd = slots_read(fop, fd, fa, fb, fc);
+                if (rd & (1u << d)) {
+                    read = true;
+                    const bool limb0 =
+                        (has_w32(fop) && fw <= 32 && fop != MG_EXTRACT) ||
+                        (fop == MG_ITE && fc == d && fa != d && fb != d) ||
+                        fop == MG_ROOT ||
+                        (fop == MG_SPILL && (place[order[q]] & PL_NARROW));
+                    if (!limb0) dirty = false;
+                }
+                if (slots_touched(fop, fd, fa, fb, fc) & ~rd & (1u << d)) break;   // rewritten
+            }
+            (void)read;
+        }
+        if (writes && narrow && (clean[d] || dirty)) var |= MGA_V_DC;
         const uint32_t maskv = w32 ? (w < 32 ? MGA_V_MASK : 0) : ((w >= 1 && w < 256) ? MGA_V_MASK : 0);
         r[1] = 8 * d; r[2] = 8 * a; r[3] = 8 * b; r[4] = 8 * c; r[5] = 0; r[6] = w; r[7] = ones;
         int aop = MGA_NOP;
@@ -544,7 +575,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             last_ld = (size_t)(r - rec.data());
             last_ld_hid = MGA_HID(aop, var, bank);
         }
-        if (writes && !nw) clean[d] = narrow;
+        if (writes && !nw) clean[d] = narrow && !dirty;
         bank = mga_is_heavy(aop) ? 0 : 1 - bank;
     }
 }
