@@ -1050,21 +1050,41 @@ static const int MAX_OR = 64;
 static const int BRANCH_DEPTH = 2;
 static const int SELECTOR_WIDTH = 8;
 
-// rewrite memo; an overlay reads through to its parent (solve._Overlay)
+// rewrite memo; an overlay reads through to its parent (solve._Overlay).
+// Overlays live one at a time per solver over a shared dense table: a slot
+// belongs to the overlay whose generation it carries (no hashing, no clear)
+struct OverlayTable {
+    std::vector<int> val, gen;
+    int next_gen = 0;
+};
 struct Memo {
     std::vector<int> dense;                 // base memo: LNode id -> result
-    std::unordered_map<int, int> m;         // overlay: local writes
     const Memo* parent = nullptr;
+    OverlayTable* ov = nullptr;             // overlay: local writes
+    int gen = 0;
     int get(int k) const {
         if (!parent) return (size_t)k < dense.size() ? dense[k] : -1;
-        auto it = m.find(k);
-        if (it != m.end()) return it->second;
+        if ((size_t)k < ov->gen.size() && ov->gen[k] == gen) return ov->val[k];
         return parent->get(k);
     }
     void put(int k, int v) {
-        if (parent) { m[k] = v; return; }
+        if (parent) {
+            if ((size_t)k >= ov->gen.size()) {
+                size_t sz = std::max<size_t>(k + 1, 2 * ov->gen.size());
+                ov->gen.resize(sz, 0);
+                ov->val.resize(sz, -1);
+            }
+            ov->gen[k] = gen;
+            ov->val[k] = v;
+            return;
+        }
         if ((size_t)k >= dense.size()) dense.resize(std::max<size_t>(k + 1, 2 * dense.size()), -1);
         dense[k] = v;
+    }
+    void overlay_on(const Memo* p, OverlayTable* t) {
+        parent = p;
+        ov = t;
+        gen = ++t->next_gen;
     }
 };
 
@@ -1497,9 +1517,33 @@ struct Solver {
 
     template <class V> static bool contains(const V& v, int x) { return std::find(v.begin(), v.end(), x) != v.end(); }
 
+    // atoms of a rewritten root, kept across passes and branches: a rewrite
+    // result holds no defined leaf, so neither do the parts split from it,
+    // and the walk below is a function of that node alone (its splits,
+    // folds and intervals are structural; nodes it builds are hash-consed,
+    // so a repeated walk would build nothing new)
+    struct AtomsOf { Chunks out; bool unsat; };
+    std::unordered_map<int, AtomsOf> atoms_of_;
+    OverlayTable overlay_table_;
+
     Chunks atoms(int root, Memo& memo) {
+        const int r0 = rewrite(root, memo);
+        auto hit = atoms_of_.find(r0);
+        if (hit != atoms_of_.end()) {
+            unsat |= hit->second.unsat;
+            return hit->second.out;
+        }
+        const bool unsat_in = unsat;
+        unsat = false;
+        Chunks out = atoms_walk(r0, memo);
+        atoms_of_.emplace(r0, AtomsOf{out, unsat});
+        unsat |= unsat_in;
+        return out;
+    }
+
+    Chunks atoms_walk(int r0, Memo& memo) {
         Chunks out;
-        Chunks stack{rewrite(root, memo)};
+        Chunks stack{r0};
         const int g = new_stamp();
         while (!stack.empty()) {
             int x = stack.back();
@@ -1924,7 +1968,7 @@ struct Solver {
         for (int d : disj) {
             unsat = false;
             Memo overlay;
-            overlay.parent = run_memo;
+            overlay.overlay_on(run_memo, &overlay_table_);
             Chunks at = atoms(d, overlay);
             if (unsat) { per.emplace_back(); continue; }
             define(at);

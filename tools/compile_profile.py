@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--graph", default="", help="write gprof's call graph here")
+    ap.add_argument("--save", default="", help="also write the corpus (one copy) here")
     ap.add_argument("--time", action="store_true",
                     help="no profiler: build -O2 and print the wall time per query (best of 5)")
     args = ap.parse_args()
@@ -57,6 +58,9 @@ def main():
     names = ("decode", "lower", "solve", "sinks", "schedule", "allocate", "pools", "meta")
     print("per query (us):", ", ".join("%s %.0f" % kv for kv in zip(names, ph)),
           "total %.0f" % ph.sum())
+    if args.save:
+        with open(args.save, "wb") as fh:
+            fh.write(b"".join(recs))
     with tempfile.TemporaryDirectory() as d:
         corpus = os.path.join(d, "corpus.bin")
         with open(corpus, "wb") as fh:
