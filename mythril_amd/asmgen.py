@@ -2185,6 +2185,10 @@ DIV_J0_JUMP = os.environ.get("MYTHGPU_DIV_J0", "1") != "0"
 # the one-limb short division's second ("unlikely") quotient correction behind
 # a branch (round 5; A/B knob: MYTHGPU_DIV_SHORT_BRANCH=0 is the round-4 step)
 DIV_SHORT_BRANCH = os.environ.get("MYTHGPU_DIV_SHORT_BRANCH", "1") != "0"
+# waves whose every divisor fits 64 bits (and not all 32) divide by Moller-
+# Granlund 3-by-2 steps out of line (round 5; A/B knob: MYTHGPU_DIV_SHORT2=0
+# sends them down the general path)
+DIV_SHORT2 = os.environ.get("MYTHGPU_DIV_SHORT2", "1") != "0"
 
 
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
@@ -2225,17 +2229,40 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     # every active lane's divisor fits one limb: short division, out of line
     lab_short, lab_done = a.uniq("dsh"), a.uniq("dsd")
     t = T[4]
-    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[1]), v(Y[2]), v(Y[3])))
-    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[4]), v(Y[5])))
-    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[6]), v(Y[7])))
-    a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
-    a("s_cmp_eq_u64 vcc, exec")
-    a("s_cbranch_scc1 %s" % lab_short)
-    a.cold()
-    a.label(lab_short)
-    _udivrem_short(a, want_rem, z)
-    a("s_branch %s" % lab_done)
-    a.hot()
+    if DIV_SHORT2:
+        # every active lane's divisor fits two limbs: out of line, where
+        # one limb (the one-limb short division) or two (3-by-2 steps) is
+        # decided
+        lab_fit64, lab_two = a.uniq("d64"), a.uniq("d2l")
+        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[2]), v(Y[3]), v(Y[4])))
+        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[5]), v(Y[6])))
+        a("v_or_b32 %s, %s, %s" % (v(t), v(t), v(Y[7])))
+        a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
+        a("s_cmp_eq_u64 vcc, exec")
+        a("s_cbranch_scc1 %s" % lab_fit64)
+        a.cold()
+        a.label(lab_fit64)
+        a("v_cmp_eq_u32 vcc, 0, %s" % v(Y[1]))
+        a("s_cmp_eq_u64 vcc, exec")
+        a("s_cbranch_scc0 %s" % lab_two)
+        _udivrem_short(a, want_rem, z)
+        a("s_branch %s" % lab_done)
+        a.label(lab_two)
+        _udivrem_short2(a, want_rem, z)
+        a("s_branch %s" % lab_done)
+        a.hot()
+    else:
+        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[1]), v(Y[2]), v(Y[3])))
+        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[4]), v(Y[5])))
+        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[6]), v(Y[7])))
+        a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
+        a("s_cmp_eq_u64 vcc, exec")
+        a("s_cbranch_scc1 %s" % lab_short)
+        a.cold()
+        a.label(lab_short)
+        _udivrem_short(a, want_rem, z)
+        a("s_branch %s" % lab_done)
+        a.hot()
     for j in range(0, 8, 2):
         a("v_mov_b64 %s, 0" % vp(R[j]))
     a("v_mov_b32 %s, 0" % v(T[0]))                                       # un[16]
@@ -2371,6 +2398,104 @@ def _udivrem_short(a: Asm, want_rem: bool, z: int):
     if want_rem:
         a("v_lshrrev_b32 %s, %s, %s" % (v(X[0]), v(b), v(r)))
         moves(a, X[1:], [None] * 7)
+
+
+def _udivrem_short2(a: Asm, want_rem: bool, z: int):
+    """udivrem when every active lane's divisor Y fits 64 bits (wave-uniform;
+    some lane needs the second limb): the divisor is normalised to a 64-bit
+    d = d1:d0 with its top bit set (lanes below 2^32 move up one limb, with
+    the dividend), u = X << that shift over 10 limbs, then eight Moller-
+    Granlund 3-by-2 steps (their Algorithm 5, with the 3/2 reciprocal of
+    Algorithm 6) bring in one dividend limb each: (r1:r0:u[j]) / d ->
+    quotient digit R[j], remainder r1:r0 < d.  No limb barrel, no multiply-
+    subtract chain, no per-digit tests.  Same contract as udivrem (lanes
+    with Y == 0 divide 0 by 1, s[z:z+1] marks them).  Registers: d0 / d1 =
+    Y0 / Y1, b = T2, p = T3, r = T4:T5 (r0 low), Q = T6:T7, P = T8:T9,
+    dinv = T10; s[52:53] = lanes shifted by a limb."""
+    d0, d1 = Y[0], Y[1]
+    b, p, dinv = T[2], T[3], T[10]
+    r0, r1, q0, q1, t0, t1 = T[4], T[5], T[6], T[7], T[8], T[9]
+    lq = DIV_M[1]
+    un = X + [R[0], R[1]]
+    dd = vp(Y[0])                                   # (d1:d0) as one 64-bit operand
+    a("v_or_b32 %s, %s, %s" % (v(r0), v(d0), v(d1)))
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(r0)))                   # Y == 0
+    a("v_cndmask_b32_e64 %s, %s, 1, %s" % (v(d0), v(d0), sp(z)))
+    lab = exec_begin(a, z, S_T)
+    moves(a, X, [None] * 8)
+    exec_end(a, lab, S_T)
+    a("v_mov_b64 %s, 0" % vp(R[0]))                                   # un[8], un[9]
+    # divisors below 2^32 (d1 == 0) move up one limb, the dividend with them
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(lq), v(d1)))
+    lab = exec_begin(a, lq, S_T)
+    moves(a, [d1, d0], [d0, None])
+    moves(a, [R[0]] + [X[j] for j in reversed(range(8))],
+          [X[7]] + [X[j - 1] if j else None for j in reversed(range(8))])
+    exec_end(a, lab, S_T)
+    # then by b = clz(d1) bits (d1 != 0 in every lane now)
+    bz = S_T + 4
+    a("v_ffbh_u32 %s, %s" % (v(b), v(d1)))
+    a("v_sub_u32 %s, 32, %s" % (v(p), v(b)))
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(bz), v(b)))
+    bitshift_left(a, [d0, d1], p, bz, 2, S_T)
+    bitshift_left(a, un, p, bz, 10, S_T)
+    # 3/2 reciprocal: dinv = floor((2^96 - 1) / d) - 2^32 from the 2/1
+    # reciprocal of d1 (Algorithm 6)
+    _reciprocal(a, d1, dinv)
+    c1, ge = sp(S_T), sp(S_T + 2)
+    a("v_mul_lo_u32 %s, %s, %s" % (v(p), v(d1), v(dinv)))
+    a("v_add_co_u32 %s, %s, %s, %s" % (v(p), c1, v(p), v(d0)))         # p = d1 v + d0, carry
+    a("v_cmp_ge_u32_e64 %s, %s, %s" % (ge, v(p), v(d1)))
+    a("s_and_b64 %s, %s, %s" % (ge, ge, c1))
+    a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), c1))
+    a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), ge))
+    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(t0), v(d1), c1))
+    a("v_sub_u32 %s, %s, %s" % (v(p), v(p), v(t0)))
+    a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(t0), v(d1), ge))
+    a("v_sub_u32 %s, %s, %s" % (v(p), v(p), v(t0)))
+    a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(q0), sp(S_T + 6), v(dinv), v(d0)))   # (t1:t0) = v d0
+    a("v_add_co_u32 %s, %s, %s, %s" % (v(q1), c1, v(p), v(q1)))       # p += t1, carry
+    a("v_cmp_ge_u64_e64 %s, %s, %s" % (ge, vp(q0), dd))               # (p:t0) >= (d1:d0)
+    a("s_and_b64 %s, %s, %s" % (ge, ge, c1))
+    a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), c1))
+    a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(dinv), sp(S_T + 4), v(dinv), ge))
+    a("v_mov_b64 %s, %s" % (vp(r0), vp(R[0])))                         # r = un[9]:un[8] < d
+    for j in reversed(range(8)):
+        # (q1:q0) = dinv r1 + (r1:r0); r1' = r0 - q1 d1; (r1':r0') = (r1':u[j])
+        # - d0 q1 - d; q1++; r1' >= q0: q1--, r' += d; r' >= d (unlikely):
+        # q1++, r' -= d
+        a("v_mad_u64_u32 %s, %s, %s, %s, %s" % (vp(q0), sp(S_T + 6), v(dinv), v(r1), vp(r0)))
+        a("v_mul_lo_u32 %s, %s, %s" % (v(t1), v(q1), v(d1)))
+        a("v_sub_u32 %s, %s, %s" % (v(r1), v(r0), v(t1)))
+        a("v_mad_u64_u32 %s, %s, %s, %s, 0" % (vp(t0), sp(S_T + 6), v(d0), v(q1)))
+        a("v_sub_co_u32 %s, vcc, %s, %s" % (v(r0), v(X[j]), v(t0)))
+        a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(r1), v(r1), v(t1)))
+        a("v_sub_co_u32 %s, vcc, %s, %s" % (v(r0), v(r0), v(d0)))
+        a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(r1), v(r1), v(d1)))
+        a("v_add_u32 %s, 1, %s" % (v(q1), v(q1)))
+        a("v_cmp_ge_u32_e64 %s, %s, %s" % (ge, v(r1), v(q0)))
+        a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(R[j]), sp(S_T + 4), v(q1), ge))
+        lab = exec_begin(a, S_T + 2, S_T)
+        a("v_add_co_u32 %s, vcc, %s, %s" % (v(r0), v(r0), v(d0)))
+        a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(r1), v(r1), v(d1)))
+        exec_end(a, lab, S_T)
+        a("v_cmp_ge_u64 vcc, %s, %s" % (vp(r0), dd))
+        skip = a.uniq("d2s")
+        a("s_cbranch_vccz %s" % skip)
+        lab = exec_begin(a, None, S_T)
+        a("v_add_u32 %s, 1, %s" % (v(R[j]), v(R[j])))
+        a("v_sub_co_u32 %s, vcc, %s, %s" % (v(r0), v(r0), v(d0)))
+        a("v_subb_co_u32 %s, vcc, %s, %s, vcc" % (v(r1), v(r1), v(d1)))
+        exec_end(a, lab, S_T)
+        a.label(skip)
+    if want_rem:
+        # remainder = r >> (b + 32 in the lanes that moved a limb)
+        a("v_alignbit_b32 %s, %s, %s, %s" % (v(X[0]), v(r1), v(r0), v(b)))
+        a("v_lshrrev_b32 %s, %s, %s" % (v(X[1]), v(b), v(r1)))
+        lab = exec_begin(a, lq, S_T)
+        moves(a, [X[0], X[1]], [X[1], None])
+        exec_end(a, lab, S_T)
+        moves(a, X[2:], [None] * 6)
 
 
 def _udivrem_short_r4(a: Asm, want_rem: bool, z: int):

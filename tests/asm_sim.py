@@ -727,6 +727,9 @@ class Wave:
     def i_v_cmp_gt_u64(self, a, pc):
         self._cmp(a, lambda x, y: x > y, width=64)
 
+    def i_v_cmp_ge_u64(self, a, pc):
+        self._cmp(a, lambda x, y: x >= y, width=64)
+
     def i_v_cndmask_b32(self, a, pc):
         x, y = self.vread(a[1], "SRC0"), self.vread(a[2], "SRC1")
         m = self.lanes_mask(a[3])

@@ -143,6 +143,82 @@ def test_short_division_second_correction():
         assert got == want, (a, hex(asg.vars["x"]), hex(asg.vars["y"]))
 
 
+@pytest.mark.parametrize("rep", range(3))
+def test_division_two_limb_waves(rep):
+    """Waves whose every divisor magnitude fits 64 bits and some lane's does
+    not fit 32 take the 3-by-2 short division (asmgen._udivrem_short2):
+    divisors of 33..64 bits mixed with one-limb and zero divisors (those
+    lanes move up a limb), 2^63, 2^64 - 1, signed operators with small
+    negative divisors, dividends of every length, reciprocal perturbed."""
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    probes = [N.bv_op(op, x, y) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    prog = compile_constraints([], probes)
+    rng = random.Random(90 + rep)
+    edge = [0, 1, 3, (1 << 32) - 1, 1 << 32, (1 << 32) + 1, (1 << 63), (1 << 64) - 1,
+            (1 << 63) + 1, 0xFFFFFFFF00000000, 10 ** 18]
+    asgs = []
+    for lane in range(64):
+        d = rng.choice(edge + [rng.getrandbits(rng.choice((33, 40, 63, 64))),
+                               rng.getrandbits(rng.choice((8, 31, 32)))])
+        if lane == 0:
+            d = (1 << 40) + 7                               # every wave has a two-limb divisor
+        if rep == 2 and rng.random() < 0.5 and d:
+            d = (1 << 256) - d                              # negative: |d| fits 64 bits
+        xv = rng.choice([0, 1, (1 << 256) - 1, 1 << 255, rng.getrandbits(256),
+                         rng.getrandbits(rng.randrange(1, 256)), rng.getrandbits(64)])
+        asgs.append(PA(vars={"x": xv, "y": d}))
+    root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs), rcp_noise=1e-7)
+    for a, asg in enumerate(asgs):
+        want = R.evaluate(probes, R.Assignment(asg.vars))
+        got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+        assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
+
+
+def _div3by2_unlikely(rng):
+    """(d, r, u0) with d normalised to 64 bits and r < d where the 3-by-2
+    step needs its rare final correction (a restatement of Moller-Granlund's
+    Algorithms 5 and 6 over 32-bit words, searched at random)."""
+    B, M = 1 << 32, (1 << 32) - 1
+    while True:
+        d = rng.getrandbits(64) | 1 << 63
+        d1, d0 = d >> 32, d & M
+        v = (B ** 3 - 1) // d - B
+        r = rng.randrange(d)
+        u0 = rng.getrandbits(32)
+        u2, u1 = r >> 32, r & M
+        q = v * u2 + (u2 << 32 | u1)
+        q1, q0 = (q >> 32) & M, q & M
+        r1 = (u1 - q1 * d1) & M
+        rr = ((r1 << 32 | u0) - d0 * q1 - d) % (B * B)
+        if rr >> 32 >= q0:
+            rr = (rr + d) % (B * B)
+        if rr >= d:
+            return d, r, u0
+
+
+def test_two_limb_division_final_correction():
+    """Lanes whose 3-by-2 step needs the final ("unlikely") correction, at
+    several digit positions, next to lanes that do not."""
+    x, y = N.bv_var("x", 256), N.bv_var("y", 256)
+    probes = [N.bv_op("bvudiv", x, y), N.bv_op("bvurem", x, y)]
+    prog = compile_constraints([], probes)
+    rng = random.Random(11)
+    cases = [_div3by2_unlikely(rng) for _ in range(4)]
+    asgs = []
+    for lane in range(64):
+        d, r, u0 = cases[lane % 4]
+        pos = rng.randrange(6)
+        xv = (r << 32 | u0) << (32 * pos) | rng.getrandbits(32 * pos)
+        if lane % 7 == 6:
+            xv, d = rng.getrandbits(256), rng.getrandbits(64) | 1
+        asgs.append(PA(vars={"x": xv, "y": d}))
+    root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+    for a, asg in enumerate(asgs):
+        want = R.evaluate(probes, R.Assignment(asg.vars))
+        got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+        assert got == want, (a, hex(asg.vars["x"]), hex(asg.vars["y"]))
+
+
 @pytest.mark.parametrize("small", ["y", "x", "both", "none"])
 def test_mul_short_operand_waves(small):
     """MUL waves whose operands are below 2^64 in every lane (either side,
