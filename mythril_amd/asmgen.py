@@ -2189,6 +2189,12 @@ DIV_SHORT_BRANCH = os.environ.get("MYTHGPU_DIV_SHORT_BRANCH", "1") != "0"
 # Granlund 3-by-2 steps out of line (round 5; A/B knob: MYTHGPU_DIV_SHORT2=0
 # sends them down the general path)
 DIV_SHORT2 = os.environ.get("MYTHGPU_DIV_SHORT2", "1") != "0"
+# a wave whose every divisor is zero skips the division (round 5; A/B knob:
+# MYTHGPU_DIV_ZERO_EXIT=0 divides 0 by 1 in the one-limb short division)
+DIV_ZERO_EXIT = os.environ.get("MYTHGPU_DIV_ZERO_EXIT", "1") != "0"
+# with the digit-0 jump, the reciprocal after the wave's digit-0 test (round
+# 5; A/B knob: MYTHGPU_DIV_J0_LATE=0 computes it first)
+DIV_J0_LATE = os.environ.get("MYTHGPU_DIV_J0_LATE", "1") != "0"
 
 
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
@@ -2245,8 +2251,20 @@ def udivrem(a: Asm, want_rem: bool, z: int):
         a("v_cmp_eq_u32 vcc, 0, %s" % v(Y[1]))
         a("s_cmp_eq_u64 vcc, exec")
         a("s_cbranch_scc0 %s" % lab_two)
+        if DIV_ZERO_EXIT:
+            # every active lane divides by zero (11 % of the C2 corpus's
+            # division waves): quotient and remainder 0 as the contract says,
+            # the caller applies SMT-LIB's x/0 rules
+            lab_zero = a.uniq("dz")
+            a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(Y[0])))
+            a("s_cmp_eq_u64 %s, exec" % sp(z))
+            a("s_cbranch_scc1 %s" % lab_zero)
         _udivrem_short(a, want_rem, z)
         a("s_branch %s" % lab_done)
+        if DIV_ZERO_EXIT:
+            a.label(lab_zero)
+            moves(a, (X if want_rem else []) + R, [None] * (16 if want_rem else 8))
+            a("s_branch %s" % lab_done)
         a.label(lab_two)
         _udivrem_short2(a, want_rem, z)
         a("s_branch %s" % lab_done)
@@ -2309,30 +2327,48 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(vn[4]), v(vn[5])))
     a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(DIV_Z6), v(t)))
     d = vn[7]
-    _reciprocal(a, d, dinv)
-    a("v_mov_b32 %s, 0" % v(T[9]))                                  # RH of the digit loop
     # a lane whose divisor moved q limbs has un[k] = 0 for k >= 9 + q and
     # un[8 + q] < 2^b <= d, so its quotient digits j > q are zero and their
     # tests below skip; when no lane moved its divisor (a wave of full-width
     # divisors; zero divisors excluded, they divide 0) only digit 0 can be
-    # nonzero: one scalar test instead of seven per-digit VALU tests (round 5)
-    lab_j0 = a.uniq("dj0")
+    # nonzero: one scalar test instead of seven per-digit VALU tests (round 5),
+    # taken before the reciprocal, which such a wave then computes only when
+    # some lane needs digit 0 (DIV_J0_LATE)
+    lab_j0, lab_rem = a.uniq("dj0"), a.uniq("drm")
+    late = DIV_J0_JUMP and DIV_J0_LATE
     if DIV_J0_JUMP:
+        if not late:
+            _reciprocal(a, d, dinv)
+            a("v_mov_b32 %s, 0" % v(T[9]))                          # RH of the digit loop
         a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(DIV_M[4]), sp(DIV_M[2])))
         a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(DIV_M[1])))
         a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(z)))
         a("s_cbranch_scc0 %s" % lab_j0)
-    for j in reversed(range(8)):
-        u2, u1 = un[j + 8], un[j + 7]
-        if j == 0:
-            a.label(lab_j0)
-        skip = a.uniq("dvs")
-        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(u2)))
-        a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(u1), v(d)))
+    if late or not DIV_J0_JUMP:
+        _reciprocal(a, d, dinv)
+        a("v_mov_b32 %s, 0" % v(T[9]))                              # RH of the digit loop
+
+    def digit_test(j, skip):
+        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(un[j + 8])))
+        a("v_cmp_ge_u32_e64 %s, %s, %s" % (sp(S_T + 2), v(un[j + 7]), v(d)))
         a("s_or_b64 vcc, %s, %s" % (sp(S_T), sp(S_T + 2)))
         a("s_cbranch_vccz %s" % skip)
+
+    for j in reversed(range(8)):
+        if j == 0 and DIV_J0_JUMP and not late:
+            a.label(lab_j0)
+        skip = a.uniq("dvs")
+        digit_test(j, skip)
         _div_digit(a, un, vn, j, d, dinv)
         a.label(skip)
+    if late:
+        a("s_branch %s" % lab_rem)
+        a.label(lab_j0)
+        digit_test(0, lab_rem)
+        _reciprocal(a, d, dinv)
+        a("v_mov_b32 %s, 0" % v(T[9]))
+        _div_digit(a, un, vn, 0, d, dinv)
+        a.label(lab_rem)
     if want_rem:
         # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
         a("v_mov_b32 %s, 0" % v(T[0]))

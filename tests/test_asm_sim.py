@@ -174,6 +174,25 @@ def test_division_two_limb_waves(rep):
         assert got == want, (rep, a, hex(asg.vars["x"]), hex(asg.vars["y"]))
 
 
+@pytest.mark.parametrize("w", [256, 64, 8])
+def test_division_by_zero_waves(w):
+    """A wave whose every divisor is zero skips the division (quotient and
+    remainder 0, then SMT-LIB's x/0 rules) — every operator, dividends of
+    both signs, at several widths."""
+    x, y = N.bv_var("x", w), N.bv_var("y", w)
+    probes = [N.bv_op(op, x, y) for op in ("bvudiv", "bvurem", "bvsdiv", "bvsrem", "bvsmod")]
+    prog = compile_constraints([], probes)
+    rng = random.Random(w)
+    M = (1 << w) - 1
+    asgs = [PA(vars={"x": rng.choice([0, 1, M, 1 << (w - 1), rng.getrandbits(w)]), "y": 0})
+            for _ in range(64)]
+    root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+    for a, asg in enumerate(asgs):
+        want = R.evaluate(probes, R.Assignment(asg.vars))
+        got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+        assert got == want, (w, a, hex(asg.vars["x"]))
+
+
 def _div3by2_unlikely(rng):
     """(d, r, u0) with d normalised to 64 bits and r < d where the 3-by-2
     step needs its rare final correction (a restatement of Moller-Granlund's
