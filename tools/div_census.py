@@ -11,10 +11,14 @@ records the widest divisor magnitude of the wave.  Prints one JSON line: the
 fraction of (division, wave) pairs whose divisors all fit 32 / 64 bits, and
 the share of divisions with a constant divisor.
 
-Usage: python tools/div_census.py [--workload c2] [--units 64] [--waves 8]
+With --lengths it also prints, per wave-wide divisor length in limbs (0 = every
+divisor zero), how long the wave's longest dividend is.
+
+Usage: python tools/div_census.py [--workload c2] [--units 64] [--waves 8] [--lengths]
 """
 
 import argparse
+import collections
 import json
 import os
 import sys
@@ -30,6 +34,7 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--units", type=int, default=64)
     ap.add_argument("--waves", type=int, default=8)
+    ap.add_argument("--lengths", action="store_true")
     args = ap.parse_args()
     import bench
     from oracle import evalref, gen_ref
@@ -39,6 +44,7 @@ def main():
     n = 64 * args.waves
     first = 1 << 20
     tot = fit32 = fit64 = const = 0
+    lengths = collections.defaultdict(collections.Counter)
     for d in range(args.units):
         d, prog, _, _ = bench.compile_unit((args.workload, d))
         roots = bench.workload_roots(args.workload, d)
@@ -66,6 +72,11 @@ def main():
                 tot += 1
                 fit32 += mx < (1 << 32)
                 fit64 += mx < (1 << 64)
+                if args.lengths:
+                    mu = max(evalref.node_value(vals, a, r[2]) for a in range(64 * wv, 64 * wv + 64))
+                    lengths[(mx.bit_length() + 31) // 32][(mu.bit_length() + 31) // 32] += 1
+    for nd in sorted(lengths):
+        print("divisor limbs %d: dividend limbs %s" % (nd, dict(sorted(lengths[nd].items()))))
     print(json.dumps({"workload": args.workload, "units": args.units, "waves": args.waves,
                       "division_waves": tot, "const_divisor": const / max(tot, 1),
                       "all_lanes_fit32": fit32 / max(tot, 1), "all_lanes_fit64": fit64 / max(tot, 1)}))
