@@ -1135,6 +1135,7 @@ struct Solver {
     Memo* run_memo = &base_memo;
     std::unordered_map<int, int> depth;
     bool unsat = false;
+    bool dead = false;                      // run: a root folded to false
 
     std::vector<std::pair<int, bool>> rw_stack_;
 
@@ -2121,6 +2122,17 @@ struct Solver {
             Chunks every;
             for (int r : order) {
                 Chunks at = atoms(r, memo);
+                const int rr = rewrite(r, memo);
+                if (ln[rr].op == MG_CONST && !(ln[rr].imm.w[0] & 1)) {
+                    // a root folded to false under the construction: the
+                    // group needs no program beyond it (model._ground_value)
+                    dead = true;
+                    roots = {rr};
+                    defs_out.clear();
+                    lw.birth = saved_birth;
+                    run_memo = &base_memo;
+                    return;
+                }
                 append(every, at);
                 found += define(at);
             }
@@ -2918,6 +2930,10 @@ static void compile(const mgc_input* in, mgc_result* res) {
         solver_own.reset(new Solver(lw));
         solver = solver_own.get();
         solver->run(roots, derived_nodes);
+        if (solver->dead) {                 // a false root: that root alone
+            births.resize(1);
+            probes.clear();
+        }
     }
     tp[3] = now_us();
     Memo probe_memo;
@@ -2952,6 +2968,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
         Memo memo_e;
         lw.birth = 0;
         for (auto& te : lw.arg_entries.items) {
+            if (solver->dead) break;
             std::vector<std::vector<int>> ks;
             for (auto& ent : te.second) {
                 std::vector<int> row;

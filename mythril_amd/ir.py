@@ -1224,6 +1224,8 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
         solver = Solver(lw)
         roots, derived_nodes = solver.run(roots)
         probe_memo: Dict[int, LNode] = {}
+        if solver.dead:                       # a false root: that root alone
+            births, probes = births[:1], ()
     sinks: List[LNode] = []
     for r, b in zip(roots, births):
         lw.birth = b
@@ -1253,7 +1255,7 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
             derived[li] = out(e)
         memo_e: Dict[int, LNode] = {}
         lw.birth = 0
-        for name, ents in lw.arg_entries.items():
+        for name, ents in (lw.arg_entries.items() if not solver.dead else ()):
             # keys under the constructed model (folded: an ABI offset the
             # model pins makes its reads' keys constants)
             entry_keys[name] = [[out(solver.rewrite(k, memo_e)) for k in key]

@@ -108,6 +108,7 @@ class Solver:
         # (a stand-in may be split again by a later ``or``, to BRANCH_DEPTH)
         self.depth: Dict[int, int] = {}
         self.unsat = False
+        self.dead = False                        # run: a root folded to false
 
     # -- rewriting -------------------------------------------------------------
     def _interval(self, n):
@@ -1009,6 +1010,13 @@ class Solver:
             every = []
             for r in order:
                 atoms = self._atoms(r, memo)
+                rr = self.rewrite(r, memo)
+                if rr.op == I.CONST and not rr.imm & 1:
+                    # a root folded to false under the construction: the
+                    # group needs no program beyond it (model._ground_value)
+                    self.dead = True
+                    self.lw.birth = saved_birth
+                    return [rr], {}
                 every += atoms
                 found += self._define(atoms)
             # intervals from the bounds of all conjuncts together: per
