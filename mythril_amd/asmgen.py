@@ -1746,29 +1746,59 @@ def h_cdwx(a, bank, root, mask, dc=False, w32=False, ip=False):
     wrap, back, done = a.uniq("cdxw"), a.uniq("cdxb"), a.uniq("cdxd")
     a("v_cmp_eq_u32 vcc, 0x7fffffff, %s" % v(Y[7]))
     a("s_cbranch_vccnz %s" % wrap)
-    _prefix(a, T[2], T[0], T[2])                                   # valid bytes
-    a.label(back)
-    a("v_cmp_ne_u32 vcc, -1, %s" % v(T[2]))
-    if not ip:
-        a.read_slot(R, fld(bank, F_A))
-    a("s_cbranch_vccz %s" % done)                                  # every byte valid
-    a("v_bfrev_b32 %s, %s" % (v(T[2]), v(T[2])))                   # bit 4j + k: limb j, byte k
-    a("s_mov_b32 %s, 0x1010101" % s(S_T))
-    for j in range(8):
-        a("v_bfe_u32 %s, %s, %d, 4" % (v(T[3]), v(T[2]), 4 * j))
-        a("v_mul_u32_u24 %s, 0x204081, %s" % (v(T[3]), v(T[3])))    # bit k -> bit 8k
-        a("v_and_b32 %s, %s, %s" % (v(T[3]), s(S_T), v(T[3])))
-        # x 255 (a 24-bit multiply would drop byte 3's bit): (t << 8) - t
-        a("v_lshlrev_b32 %s, 8, %s" % (v(X[j]), v(T[3])))
-        a("v_sub_u32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[3])))
-    if ip:
-        a.idx_on(fld(bank, F_D), "SRC1,DST")
+    if CDWX_PREFIX:
+        # no lane wraps: the valid bytes are the first n, so limb j keeps its
+        # top min(max(n - 4(7 - j), 0), 4) bytes — with x_j = 8 * that, the
+        # low word of (0xffffffff << 32) >> x_j (x_j <= 32: a 64-bit shift)
+        a("v_cmp_gt_u32 vcc, 32, %s" % v(T[0]))                    # lanes missing a byte
+        if not ip:
+            a.read_slot(R, fld(bank, F_A))
+        a("s_cbranch_vccz %s" % done)                              # every byte valid
+        a("v_lshlrev_b32 %s, 3, %s" % (v(T[1]), v(T[0])))          # 8n
+        a("s_mov_b32 %s, 0" % s(S_T))
+        a("s_mov_b32 %s, -1" % s(S_T + 1))
         for j in range(8):
-            a("v_and_b32 %s, %s, %s" % (v(F[j]), v(X[j]), v(F[j])))
-        a.idx_off()
-    else:
+            k = 32 * (7 - j)
+            if k:
+                a("v_subrev_u32 %s, %d, %s" % (v(T[4]), k, v(T[1])))
+                a("v_med3_i32 %s, %s, 0, 32" % (v(T[4]), v(T[4])))
+            else:
+                a("v_min_u32 %s, 32, %s" % (v(T[4]), v(T[1])))
+            a("v_lshrrev_b64 %s, %s, %s" % (vp(T[2]), v(T[4]), sp(S_T)))
+            if ip:
+                a.idx_on(fld(bank, F_D), "SRC1,DST")
+                a("v_and_b32 %s, %s, %s" % (v(F[j]), v(T[2]), v(F[j])))
+                a.idx_off()
+            else:
+                a("v_and_b32 %s, %s, %s" % (v(R[j]), v(T[2]), v(R[j])))
+
+    def spread_and():
+        # T[2] = the 32-bit valid-byte set (bit i: byte 31 - i)
+        a("v_cmp_ne_u32 vcc, -1, %s" % v(T[2]))
+        if not ip:
+            a.read_slot(R, fld(bank, F_A))
+        a("s_cbranch_vccz %s" % done)                              # every byte valid
+        a("v_bfrev_b32 %s, %s" % (v(T[2]), v(T[2])))               # bit 4j + k: limb j, byte k
+        a("s_mov_b32 %s, 0x1010101" % s(S_T))
         for j in range(8):
-            a("v_and_b32 %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j])))
+            a("v_bfe_u32 %s, %s, %d, 4" % (v(T[3]), v(T[2]), 4 * j))
+            a("v_mul_u32_u24 %s, 0x204081, %s" % (v(T[3]), v(T[3])))    # bit k -> bit 8k
+            a("v_and_b32 %s, %s, %s" % (v(T[3]), s(S_T), v(T[3])))
+            # x 255 (a 24-bit multiply would drop byte 3's bit): (t << 8) - t
+            a("v_lshlrev_b32 %s, 8, %s" % (v(X[j]), v(T[3])))
+            a("v_sub_u32 %s, %s, %s" % (v(X[j]), v(X[j]), v(T[3])))
+        if ip:
+            a.idx_on(fld(bank, F_D), "SRC1,DST")
+            for j in range(8):
+                a("v_and_b32 %s, %s, %s" % (v(F[j]), v(X[j]), v(F[j])))
+            a.idx_off()
+        else:
+            for j in range(8):
+                a("v_and_b32 %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j])))
+    if not CDWX_PREFIX:
+        _prefix(a, T[2], T[0], T[2])                               # valid bytes
+        a.label(back)
+        spread_and()
     a.label(done)
     if not ip:
         a.write_slot(R, fld(bank, F_D))
@@ -1804,7 +1834,11 @@ def h_cdwx(a, bank, root, mask, dc=False, w32=False, ip=False):
     _prefix(a, T[8], T[4], T[8])
     a("v_bfi_b32 %s, %s, 0, %s" % (v(T[6]), v(T[8]), v(T[6])))    # [K, end)
     a("v_or_b32 %s, %s, %s" % (v(T[2]), v(T[2]), v(T[6])))
-    a("s_branch %s" % back)
+    if CDWX_PREFIX:
+        spread_and()                                               # not a prefix here
+        a("s_branch %s" % done)
+    else:
+        a("s_branch %s" % back)
     a.hot()
     a.flush_cold()
 
@@ -2195,6 +2229,9 @@ DIV_ZERO_EXIT = os.environ.get("MYTHGPU_DIV_ZERO_EXIT", "1") != "0"
 # with the digit-0 jump, the reciprocal after the wave's digit-0 test (round
 # 5; A/B knob: MYTHGPU_DIV_J0_LATE=0 computes it first)
 DIV_J0_LATE = os.environ.get("MYTHGPU_DIV_J0_LATE", "1") != "0"
+# the calldata word's byte mask built per limb from the valid-byte count when
+# no lane wraps (round 5; A/B knob: MYTHGPU_CDWX_PREFIX=0 spreads the byte set)
+CDWX_PREFIX = os.environ.get("MYTHGPU_CDWX_PREFIX", "1") != "0"
 
 
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,

@@ -89,10 +89,14 @@ def pack(program: Program, assignments: Sequence[Assignment]) -> np.ndarray:
 
 
 def _limbs_int(row) -> int:
-    v = 0
-    for j in reversed(range(8)):
-        v = (v << 32) | int(row[j])
-    return v
+    return int.from_bytes(np.ascontiguousarray(row, dtype="<u4").tobytes(), "little")
+
+
+def _rows_int(rows: np.ndarray, n: int) -> list:
+    """The first n rows of an (.., 8) limb array as Python ints (one byte
+    string, sliced: no per-limb Python work)."""
+    b = np.ascontiguousarray(rows[:n], dtype="<u4").tobytes()
+    return [int.from_bytes(b[32 * i:32 * i + 32], "little") for i in range(n)]
 
 
 def unpack(program: Program, leaves: np.ndarray, probes: np.ndarray = None) -> Assignment:
@@ -100,12 +104,13 @@ def unpack(program: Program, leaves: np.ndarray, probes: np.ndarray = None) -> A
     solve-mode program (``Program.solved``) also needs the candidate's probe
     values ((n_probes, 8)): the leaves it defines by equalities and the keys
     of its argument-keyed table entries are computed, not generated."""
-    vals = [_limbs_int(leaves[i]) for i in range(len(program.leaves))]
+    vals = _rows_int(leaves, len(program.leaves))
+    pv = _rows_int(probes, len(probes)) if probes is not None else None
     if program.solved:
         if probes is None:
             raise ValueError("a solve-mode witness needs its probe values")
         for li, k in program.derived.items():
-            vals[li] = _limbs_int(probes[k])
+            vals[li] = pv[k]
     vars_: Dict[str, int] = {}
     tables: Dict[str, dict] = {}
     for leaf, v in zip(program.leaves, vals):
@@ -126,7 +131,7 @@ def unpack(program: Program, leaves: np.ndarray, probes: np.ndarray = None) -> A
     for name, ents in program.entry_keys.items():
         t = tables.setdefault(name, {"k": {}, "v": {}, "c": {}, "else": 0})
         for e, chunks in enumerate(ents):
-            t["k"][e] = sum(_limbs_int(probes[k]) << (CHUNK * c) for c, k in enumerate(chunks))
+            t["k"][e] = sum(pv[k] << (CHUNK * c) for c, k in enumerate(chunks))
     arrays, funcs = {}, {}
     for name, t in tables.items():
         n = program.table_sizes.get(name, 0)

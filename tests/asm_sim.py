@@ -604,6 +604,13 @@ class Wave:
     def i_v_min_u32(self, a, pc):
         self._vop2(a, lambda x, y: np.minimum(x, y))
 
+    def i_v_med3_i32(self, a, pc):
+        def med3(x, y, z):
+            sx, sy, sz = (t.astype(np.uint32).view(np.int32).astype(np.int64) for t in (x, y, z))
+            m = np.maximum(np.minimum(sx, sy), np.minimum(np.maximum(sx, sy), sz))
+            return (m & 0xFFFFFFFF).astype(np.uint64)
+        self._vop3(a, med3, 3)
+
     def i_s_movk_i32(self, a, pc):
         v = int(a[1], 0) & 0xFFFF
         self.swrite(a[0], (v - 0x10000 if v & 0x8000 else v) & M32)
