@@ -106,6 +106,7 @@ class SolverStatistics:
         self.gpu_candidates = 0
         self.gpu_time = 0.0
         self.kernel_time = 0.0          # device time of the search launches (HIP events)
+        self.witness_time = 0.0         # part of the search phase: witnesses read back and unpacked
         self.memo_misses = 0            # queries answered "miss" by the group-miss memo
         self.gated = 0                  # queries whose compile estimate exceeded the budget
         self.shape_skipped = 0          # queries of a shape the search keeps missing
@@ -530,8 +531,11 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
         with _Phase("search"):
             hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
             _count_kernel(eng)
-            return [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
-                    for lp, h in zip(loaded, hits)]
+            t0 = time.perf_counter()
+            out = [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
+                   for lp, h in zip(loaded, hits)]
+            stats.witness_time += time.perf_counter() - t0
+            return out
     parts = lpt_assign([float(p.n_ins) for p in progs], len(devices))
     out: List = [None] * len(progs)
 
