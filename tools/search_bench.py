@@ -139,6 +139,7 @@ def shape_lines(eng, n_queries, n_sample=48):
                     "memo_misses": M.stats.memo_misses, "shape_skipped": M.stats.shape_skipped,
                     "gated": M.stats.gated, "kernel_ms_per_query":
                         M.stats.kernel_time * 1000.0 / len(lat),
+                    "witness_ms_per_query": M.stats.witness_time * 1000.0 / len(lat),
                     "phase_ms_per_query": {k: v * 1000.0 / len(lat)
                                            for k, v in M.stats.phase.items()}}
         cold = run(True)
