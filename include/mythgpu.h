@@ -157,6 +157,15 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* batch, uint64_t seed, uint64_t firs
  * max_leaves must be >= the batch's largest leaf count. */
 int mg_batch_search(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_cand,
                     int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves);
+/* mg_batch_search plus, in the same regeneration launch, each solved
+ * program's probe values at its witness (witness_probes: [n_progs]
+ * [max_probes][8] u32, max_probes >= the batch's largest probe count;
+ * witness_leaves must be given too): a solve-mode program's derived leaves
+ * and argument-keyed table keys, so a batch of hits needs no per-hit
+ * mg_eval_gen (round 5). */
+int mg_batch_search_probes(mg_ctx* ctx, mg_batch* batch, const mg_gen* gen, uint64_t n_cand,
+                           int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves,
+                           uint32_t* witness_probes, uint32_t max_probes);
 
 /* Compiled programs (batch path without interpretive dispatch; built on the
  * host by mythril_amd/jit.py): ``image`` is a gfx950 code object holding the

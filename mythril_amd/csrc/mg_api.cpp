@@ -157,6 +157,7 @@ struct mg_batch {
     uint32_t n = 0;
     uint32_t max_lds = 0;
     uint32_t max_leaves = 0;
+    uint32_t max_probes = 0;
 };
 
 static int fail(mg_ctx* ctx, int code, const char* fmt, ...) {
@@ -682,18 +683,20 @@ int mg_batch_create(mg_ctx* ctx, const mg_prog* const* progs, uint32_t n_progs, 
     *out = nullptr;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     std::vector<mg_pdesc> descs(n_progs);
-    uint32_t max_lds = 0, max_leaves = 0;
+    uint32_t max_lds = 0, max_leaves = 0, max_probes = 0;
     for (uint32_t i = 0; i < n_progs; ++i) {
         if (!progs[i] || progs[i]->ctx != ctx) return fail(ctx, MG_E_ARG, "program %u", i);
         descs[i] = progs[i]->h_desc;
         if (progs[i]->n_lds > max_lds) max_lds = progs[i]->n_lds;
         if (progs[i]->n_leaves > max_leaves) max_leaves = progs[i]->n_leaves;
+        if (progs[i]->n_probes > max_probes) max_probes = progs[i]->n_probes;
     }
     mg_batch* b = new mg_batch();
     b->ctx = ctx;
     b->n = n_progs;
     b->max_lds = max_lds;
     b->max_leaves = max_leaves;
+    b->max_probes = max_probes;
     if (n_progs) {
         void* d = nullptr;
         hipError_t e = dev_alloc(ctx, sizeof(mg_pdesc) * n_progs, &d, &b->descs_cls);
@@ -746,18 +749,30 @@ int mg_batch_eval_gen(mg_ctx* ctx, mg_batch* b, uint64_t seed, uint64_t first_in
 
 int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand,
                     int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves) {
+    return mg_batch_search_probes(ctx, b, gen, n_cand, first_sat, witness_leaves, max_leaves,
+                                  nullptr, 0);
+}
+
+int mg_batch_search_probes(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand,
+                           int64_t* first_sat, uint32_t* witness_leaves, uint32_t max_leaves,
+                           uint32_t* witness_probes, uint32_t max_probes) {
     if (!ctx || !b || !gen || (b->n && !first_sat)) return fail(ctx, MG_E_ARG, "null argument");
     if (b->ctx != ctx) return fail(ctx, MG_E_ARG, "batch belongs to another context");
     if (witness_leaves && max_leaves < b->max_leaves)
         return fail(ctx, MG_E_ARG, "witness rows hold %u leaves, a program has %u", max_leaves,
                     b->max_leaves);
+    if (witness_probes && (!witness_leaves || max_probes < b->max_probes))
+        return fail(ctx, MG_E_ARG, "probe rows hold %u probes, a program has %u", max_probes,
+                    b->max_probes);
     for (uint32_t i = 0; i < b->n; ++i) first_sat[i] = -1;
     if (n_cand == 0 || b->n == 0) return MG_OK;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     const size_t first_b = ((size_t)b->n * 8 + 255) & ~(size_t)255;
     const size_t wit_b = witness_leaves ? (size_t)b->n * max_leaves * 8 * 4 : 0;
+    const size_t wit_b_al = (wit_b + 255) & ~(size_t)255;
+    const size_t prb_b = witness_probes ? (size_t)b->n * max_probes * 8 * 4 : 0;
     void* ws;
-    int rc = workspace(ctx, first_b + wit_b, &ws);
+    int rc = workspace(ctx, first_b + wit_b_al + prb_b, &ws);
     if (rc) return rc;
     unsigned long long* d_first = (unsigned long long*)ws;
     HIPCHECK(ctx, hipMemsetAsync(d_first, 0xFF, (size_t)b->n * 8, ctx->stream));
@@ -781,8 +796,12 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
     if (witness_leaves) {
         // one launch regenerates every program's winning candidate: lane 0
         // of program p evaluates candidate first_sat[p] (solved programs only)
+        // (and, when asked, its probe values: what a solve-mode witness
+        // computes besides the generated leaves)
         uint32_t* d_wit = (uint32_t*)((uint8_t*)ws + first_b);
+        uint32_t* d_prb = prb_b ? (uint32_t*)((uint8_t*)ws + first_b + wit_b_al) : nullptr;
         HIPCHECK(ctx, hipMemsetAsync(d_wit, 0, wit_b, ctx->stream));
+        if (prb_b) HIPCHECK(ctx, hipMemsetAsync(d_prb, 0, prb_b, ctx->stream));
         for (uint32_t p0 = 0; p0 < b->n; p0 += 65535) {
             const uint32_t np = b->n - p0 < 65535 ? b->n - p0 : 65535;
             mg_run run = empty_run();
@@ -792,10 +811,17 @@ int mg_batch_search(mg_ctx* ctx, mg_batch* b, const mg_gen* gen, uint64_t n_cand
             run.first_per_prog = (const uint64_t*)(d_first + p0);
             run.leaves_out = d_wit + (size_t)p0 * max_leaves * 8;
             run.lout_prog_words = (uint64_t)max_leaves * 8;
+            if (d_prb) {
+                run.probes = d_prb + (size_t)p0 * max_probes * 8;
+                run.probe_prog_words = (uint64_t)max_probes * 8;
+            }
             HIPCHECK(ctx, launch(ctx, 1, b->d_descs + p0, np, run, b->max_lds, ctx->stream));
         }
         HIPCHECK(ctx, hipMemcpyAsync(witness_leaves, d_wit, wit_b, hipMemcpyDeviceToHost,
                                      ctx->stream));
+        if (prb_b)
+            HIPCHECK(ctx, hipMemcpyAsync(witness_probes, d_prb, prb_b, hipMemcpyDeviceToHost,
+                                         ctx->stream));
     }
     std::vector<unsigned long long> h(b->n, ~0ull);
     HIPCHECK(ctx, hipMemcpyAsync(h.data(), d_first, (size_t)b->n * 8, hipMemcpyDeviceToHost,

@@ -80,6 +80,8 @@ struct mg_run {
                                   candidate index (first_index ignored);
                                   ~0 = unsolved, the program returns      */
     uint64_t lout_prog_words;  /* leaves_out stride between programs       */
+    uint64_t probe_prog_words; /* witness regeneration: probes stride
+                                  between programs (0: one program)        */
 };
 
 #endif

@@ -24,7 +24,7 @@ _LIB_PATH = os.environ.get("MYTHGPU_LIB") or \
 
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
-           "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_keccak256", "mg_version", "mg_config",
+           "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_batch_search_probes", "mg_keccak256", "mg_version", "mg_config",
            "mg_translate", "mg_asm_digest", "mg_last_kernel_ms", "mg_jit_attach", "mg_jit_detach",
            "mg_runtime_info")
 
@@ -89,6 +89,7 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_batch_free.restype = None
         lib.mg_batch_eval_gen.argtypes = [p, p, u64, u64, u64, p, p, p]
         lib.mg_batch_search.argtypes = [p, p, C.POINTER(Gen), u64, p, p, u32]
+        lib.mg_batch_search_probes.argtypes = [p, p, C.POINTER(Gen), u64, p, p, u32, p, u32]
         lib.mg_keccak256.argtypes = [p, p, p, p, u32, p]
         lib.mg_config.argtypes = [p, u32]
         lib.mg_asm_digest.restype = C.c_char_p
@@ -290,26 +291,40 @@ class Engine:
 
 
     def batch_search(self, loaded: Sequence[LoadedProgram], seed: int, n_cand: int,
-                     first_index: int = 0) -> List[Tuple[int, Optional[np.ndarray]]]:
+                     first_index: int = 0, want_probes: bool = False) -> List[tuple]:
         """Witness search over many programs in shared launches
         (mg_batch_search, witnesses regenerated in one launch); per program
-        (index, leaves) or (-1, None)."""
+        (index, leaves) or (-1, None) — with ``want_probes`` (index, leaves,
+        probes) or (-1, None, None), the probe values coming from the same
+        regeneration launch (mg_batch_search_probes)."""
         if not loaded:
             return []
         h = self.batch_create(loaded)
         max_leaves = max(1, max(len(lp.program.leaves) for lp in loaded))
+        max_probes = max(1, max(lp.program.n_probes for lp in loaded))
         try:
             first = np.full(len(loaded), -1, dtype=np.int64)
             wit = np.zeros((len(loaded), max_leaves, 8), dtype=np.uint32)
             g = Gen(seed & (2**64 - 1), first_index)
-            rc = self.lib.mg_batch_search(self._ctx, h, C.byref(g), n_cand, _ptr(first), _ptr(wit),
-                                          max_leaves)
-            self._check(rc, "mg_batch_search")
+            if want_probes:
+                prb = np.zeros((len(loaded), max_probes, 8), dtype=np.uint32)
+                rc = self.lib.mg_batch_search_probes(self._ctx, h, C.byref(g), n_cand, _ptr(first),
+                                                     _ptr(wit), max_leaves, _ptr(prb), max_probes)
+                self._check(rc, "mg_batch_search_probes")
+            else:
+                rc = self.lib.mg_batch_search(self._ctx, h, C.byref(g), n_cand, _ptr(first),
+                                              _ptr(wit), max_leaves)
+                self._check(rc, "mg_batch_search")
         finally:
             self.batch_free(h)
         out = []
         for k, (lp, f) in enumerate(zip(loaded, first.tolist())):
-            out.append((-1, None) if f < 0 else (f, wit[k, :len(lp.program.leaves)].copy()))
+            if not want_probes:
+                out.append((-1, None) if f < 0 else (f, wit[k, :len(lp.program.leaves)].copy()))
+            else:
+                out.append((-1, None, None) if f < 0 else
+                           (f, wit[k, :len(lp.program.leaves)].copy(),
+                            prb[k, :lp.program.n_probes].copy()))
         return out
 
 

@@ -345,11 +345,14 @@ def _compile_search_uncached(nodes: Sequence[N.Node], probes: Sequence[N.Node] =
 
 
 def _witness(eng, lp, hit) -> Assignment:
-    """The model of a search hit (index, leaves): a solve-mode program also
-    reports the values it computed (probes of one re-evaluated lane)."""
-    idx, leaves = hit
+    """The model of a search hit (index, leaves[, probes]): a solve-mode
+    program also reports the values it computed — the probes the batched
+    search regenerated with the leaves, or those of one re-evaluated lane."""
+    idx, leaves = hit[0], hit[1]
     prog = getattr(lp, "program", lp)
     if prog.solved:
+        if len(hit) > 2 and hit[2] is not None:
+            return unpack(prog, leaves, hit[2])
         leaves, probes = eng.witness(lp, SEARCH_SEED, idx)
         return unpack(prog, leaves, probes)
     return unpack(prog, leaves)
@@ -529,7 +532,7 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
         with _Phase("load"):
             loaded = [eng.load(p, search_leafgen(p), prog_seed=0) for p in progs]
         with _Phase("search"):
-            hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
+            hits = eng.batch_search(loaded, SEARCH_SEED, n_cand, want_probes=True)
             _count_kernel(eng)
             t0 = time.perf_counter()
             out = [(h[0], _witness(eng, lp, h) if h[0] >= 0 else None)
@@ -542,7 +545,7 @@ def batch_search_devices(progs: Sequence[Program], n_cand: int):
     def run(dev, idx):
         eng = get_engine(*dev)
         loaded = [eng.load(progs[i], search_leafgen(progs[i]), prog_seed=0) for i in idx]
-        hits = eng.batch_search(loaded, SEARCH_SEED, n_cand)
+        hits = eng.batch_search(loaded, SEARCH_SEED, n_cand, want_probes=True)
         _count_kernel(eng)
         for i, lp, h in zip(idx, loaded, hits):
             out[i] = (h[0], _witness(eng, lp, h) if h[0] >= 0 else None)

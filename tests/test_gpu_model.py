@@ -136,6 +136,34 @@ def test_batch_search_equals_per_program_search(engine):
     assert batch[3][0] == -1 and all(b[0] >= 0 for i, b in enumerate(batch) if i != 3)
 
 
+@pytest.mark.parametrize("stream", ["c1", "c4", "c5"])
+def test_batch_search_probes_equal_per_hit_evaluation(engine, stream):
+    """mg_batch_search_probes: the probe values a solve-mode program reports
+    for its witness come from the batched regeneration launch and equal the
+    per-hit re-evaluation (mg_eval_gen of that one lane, engine.witness) —
+    leaves and probes, for every hit of a stand-in stream's search groups."""
+    from mythril_amd import workloads as W
+    progs = []
+    for q in W.queries(stream, 8):
+        progs += [M._compile_search(b) for b in M.dependence_buckets(q)]
+    progs = [p for p in progs if M._ground_value(p) is None][:24]
+    loaded = [engine.load(p, M.search_leafgen(p), prog_seed=0) for p in progs]
+    plain = engine.batch_search(loaded, M.SEARCH_SEED, 1 << 20)
+    both = engine.batch_search(loaded, M.SEARCH_SEED, 1 << 20, want_probes=True)
+    hits = 0
+    for p, lp, (i0, w0), (i1, w1, pr) in zip(progs, loaded, plain, both):
+        assert i0 == i1
+        if i1 < 0:
+            assert w1 is None and pr is None
+            continue
+        hits += 1
+        leaves, probes = engine.witness(lp, M.SEARCH_SEED, i1)
+        assert (w1 == leaves).all() and (w0 == w1).all()
+        if p.solved:
+            assert (pr == probes).all()
+    assert hits
+
+
 def test_batch_is_possible_on_reference_sat_queries(engine):
     """The sat keccak / calldata / model_test queries as sibling states in
     one batch: all possible, all found by the single batched search."""

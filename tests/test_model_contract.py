@@ -100,13 +100,15 @@ class FakeEngine:
     def load(self, prog, leafgen, prog_seed=0):
         return prog
 
-    def batch_search(self, loaded, seed, n_cand, first_index=0):
+    def batch_search(self, loaded, seed, n_cand, first_index=0, want_probes=False):
         self.batches.append(len(loaded))
         import numpy as np
         out = []
         for prog in loaded:
             unsat = len(prog.leaves) == 0               # e.g. a constant-false query
-            out.append((-1, None) if unsat else (7, np.zeros((len(prog.leaves), 8), np.uint32)))
+            hit = (-1, None) if unsat else (7, np.zeros((len(prog.leaves), 8), np.uint32))
+            # (no batched probes here: the model asks witness() per hit)
+            out.append(hit + (None,) if want_probes else hit)
         return out
 
     def witness(self, prog, seed, index):
@@ -205,7 +207,7 @@ def test_bucketed_witness_joins_group_assignments(monkeypatch, fresh):
         def load(self, prog, leafgen, prog_seed=0):
             return prog
 
-        def batch_search(self, loaded, seed, n_cand, first_index=0):
+        def batch_search(self, loaded, seed, n_cand, first_index=0, want_probes=False):
             Eng.calls += 1
             out = []
             for p in loaded:
@@ -427,7 +429,7 @@ def test_batch_search_spreads_programs_over_devices(monkeypatch):
         def load(self, prog, leafgen, prog_seed=0):
             return prog
 
-        def batch_search(self, loaded, seed, n_cand, first_index=0):
+        def batch_search(self, loaded, seed, n_cand, first_index=0, want_probes=False):
             self.seen.extend(loaded)
             return [(self.dev * 1000 + p.n_ins, np.zeros((len(p.leaves), 8), np.uint32))
                     for p in loaded]
@@ -674,7 +676,7 @@ def test_repeated_devices_get_their_own_contexts(monkeypatch):
         def load(self, prog, leafgen, prog_seed=0):
             return prog
 
-        def batch_search(self, loaded, seed, n_cand, first_index=0):
+        def batch_search(self, loaded, seed, n_cand, first_index=0, want_probes=False):
             return [(-1, None) for _ in loaded]
 
     def ge(dev=0, slot=0):
