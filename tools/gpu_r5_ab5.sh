@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-5 check: C2 on the final library against the library built before
-# the calldata-word prefix mask and the batched-probe kernel shell
-# (mythril_amd/lib/ab/libmythgpu_cdwxoff.so) — neither should touch C2,
-# whose programs have no calldata word and no probes.
+# Round-5 check: C2 on the final library against the same sources built with
+# MYTHGPU_CDWX_PREFIX=0 (mythril_amd/lib/ab/libmythgpu_cdwxoff.so): C2's
+# programs have no calldata word, so only the interpreter image's layout
+# differs.
 cd $GRAFT_REPO_ROOT || exit 1
 D=gpurun_out/ab_r5e && mkdir -p $D
 ( while true; do date >> $D/heartbeat.txt; sleep 45; done ) &
