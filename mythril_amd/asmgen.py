@@ -2008,6 +2008,26 @@ def body_umulno(a: Asm):
     heavy_prologue(a)
     a.read_slot(X, cur(F_A))
     a.read_slot(Y, cur(F_B))
+    lab = a.uniq("unf")
+    if UMULNO_FAST:
+        # W = 256 and both operands >= 2^128 in every active lane (90 % of the
+        # C2 corpus's UMULNO waves): p + q >= 258, every product overflows —
+        # no bit lengths needed (round 5)
+        lab_gen = a.uniq("ung")
+        a("s_cmp_eq_u32 %s, 0x100" % s(cur(F_W)))
+        a("s_cbranch_scc0 %s" % lab_gen)
+        a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(X[4]), v(X[5]), v(X[6])))
+        a("v_or_b32 %s, %s, %s" % (v(T[0]), v(T[0]), v(X[7])))
+        a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(Y[4]), v(Y[5]), v(Y[6])))
+        a("v_or_b32 %s, %s, %s" % (v(T[1]), v(T[1]), v(Y[7])))
+        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_X + 4), v(T[0])))
+        a("v_cmp_ne_u32 vcc, 0, %s" % v(T[1]))
+        a("s_and_b64 vcc, vcc, %s" % sp(S_X + 4))
+        a("s_cmp_eq_u64 vcc, exec")
+        a("s_cbranch_scc0 %s" % lab_gen)
+        a("s_mov_b64 %s, 0" % sp(S_X + 4))                 # no lane is free of overflow
+        a("s_branch %s" % lab)
+        a.label(lab_gen)
     sz = T[8]                                   # clz(x) + clz(y) = 512 - (p + q)
     clz256(a, X, sz, [T[8], T[9], T[10], T[11], T[0], T[1], T[2], T[3]])
     clz256(a, Y, T[4], [T[4], T[5], T[6], T[7], T[0], T[1], T[2], T[3]])
@@ -2015,7 +2035,6 @@ def body_umulno(a: Asm):
     a("s_sub_u32 %s, 511, %s" % (s(S_X), s(cur(F_W))))                  # 511 - W
     a("v_cmp_eq_u32_e64 %s, %s, %s" % (sp(S_X + 2), s(S_X), v(sz)))     # p + q == W + 1
     a("v_cmp_lt_u32_e64 %s, %s, %s" % (sp(S_X + 4), s(S_X), v(sz)))     # p + q <= W
-    lab = a.uniq("unf")
     a("s_cmp_eq_u64 %s, 0" % sp(S_X + 2))
     a("s_cbranch_scc1 %s" % lab)
     a("s_waitcnt lgkmcnt(0)")                   # the width masks
@@ -2229,6 +2248,9 @@ DIV_ZERO_EXIT = os.environ.get("MYTHGPU_DIV_ZERO_EXIT", "1") != "0"
 # with the digit-0 jump, the reciprocal after the wave's digit-0 test (round
 # 5; A/B knob: MYTHGPU_DIV_J0_LATE=0 computes it first)
 DIV_J0_LATE = os.environ.get("MYTHGPU_DIV_J0_LATE", "1") != "0"
+# bvumul_noovfl at W = 256 with both operands >= 2^128 in every lane answers
+# "overflow" without bit lengths (round 5; A/B knob: MYTHGPU_UMULNO_FAST=0)
+UMULNO_FAST = os.environ.get("MYTHGPU_UMULNO_FAST", "1") != "0"
 # the calldata word's byte mask built per limb from the valid-byte count when
 # no lane wraps (round 5; A/B knob: MYTHGPU_CDWX_PREFIX=0 spreads the byte set)
 CDWX_PREFIX = os.environ.get("MYTHGPU_CDWX_PREFIX", "1") != "0"

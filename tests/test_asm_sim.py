@@ -193,6 +193,32 @@ def test_division_by_zero_waves(w):
         assert got == want, (w, a, hex(asg.vars["x"]))
 
 
+@pytest.mark.parametrize("mode", ["all_large", "one_small", "w160"])
+def test_umulno_overflow_waves(mode):
+    """bvumul_noovfl: a W = 256 wave whose operands are all >= 2^128 answers
+    "overflow" without bit lengths (asmgen.UMULNO_FAST); a lane with a small
+    operand, or a narrower width, takes the bit-length path."""
+    w = 160 if mode == "w160" else 256
+    x, y = N.bv_var("x", w), N.bv_var("y", w)
+    probes = [N.ite(N.bv_cmp("bvumul_noovfl", x, y), x, y),
+              N.ite(N.bv_cmp("bvumul_noovfl", y, x), y, x)]
+    prog = compile_constraints([], probes)
+    rng = random.Random(len(mode))
+    half = w // 2
+    asgs = []
+    for lane in range(64):
+        xv = rng.getrandbits(w - half) << half | rng.getrandbits(half) | 1 << (w - 1 - rng.randrange(w - half))
+        yv = rng.getrandbits(w - half) << half | 1 << half
+        if mode == "one_small" and lane == 37:
+            yv = rng.getrandbits(100)
+        asgs.append(PA(vars={"x": xv & ((1 << w) - 1), "y": yv & ((1 << w) - 1)}))
+    root, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs))
+    for a, asg in enumerate(asgs):
+        want = R.evaluate(probes, R.Assignment(asg.vars))
+        got = [limbs_to_int(pr[k, :, a]) for k in range(len(probes))]
+        assert got == want, (mode, a)
+
+
 def _div3by2_unlikely(rng):
     """(d, r, u0) with d normalised to 64 bits and r < d where the 3-by-2
     step needs its rare final correction (a restatement of Moller-Granlund's
