@@ -136,6 +136,33 @@ def batch_env(monkeypatch, fresh):
     return eng, z3_calls
 
 
+def test_witness_probes_from_the_batched_search_need_no_per_hit_launch(batch_env, monkeypatch):
+    """A solve-mode hit whose probe values came back with the batched search
+    (mg_batch_search_probes) is unpacked from them: no per-hit witness()."""
+    eng, _ = batch_env
+    import numpy as np
+    import ir_sim
+
+    def batch_search(loaded, seed, n_cand, first_index=0, want_probes=False):
+        assert want_probes
+        out = []
+        for prog in loaded:
+            lv = np.zeros((len(prog.leaves), 8), np.uint32)
+            _, probes = ir_sim.run(prog, [0] * len(prog.leaves))
+            pr = np.zeros((max(1, len(probes)), 8), np.uint32)
+            for k, v in enumerate(probes):
+                pr[k] = [(v >> (32 * j)) & 0xFFFFFFFF for j in range(8)]
+            out.append((7, lv, pr))
+        return out
+
+    def no_witness(*a, **k):
+        raise AssertionError("per-hit witness launch")
+    monkeypatch.setattr(eng, "batch_search", batch_search)
+    monkeypatch.setattr(eng, "witness", no_witness)
+    m = M.get_model((c_sat(),))
+    assert m.assignment.vars["x"] < 5           # a derived value, from the probes
+
+
 def test_batch_is_possible_matches_the_per_state_loop(batch_env, monkeypatch):
     eng, z3_calls = batch_env
     x = symbol_factory.BitVecSym("x", 256)
