@@ -8,7 +8,7 @@ and every returned witness is checked by the oracle."""
 import pytest
 
 import mythril_amd.model as M
-from keccak_mirror import KeccakManager
+from mythril_amd.workloads import KeccakFunctionManager as KeccakManager
 from mythril_amd.smt import And, Array, If, symbol_factory
 from oracle import smtlib_ref as R
 

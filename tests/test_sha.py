@@ -6,7 +6,7 @@ import random
 
 import pytest
 
-from keccak_mirror import KeccakManager
+from mythril_amd.workloads import KeccakFunctionManager as KeccakManager
 from mythril_amd.sha import HASH_MATCHER, replace_with_actual_sha
 from mythril_amd.smt import symbol_factory
 from oracle import keccak_ref

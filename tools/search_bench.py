@@ -41,7 +41,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def reference_sat_queries(engine):
-    from keccak_mirror import KeccakManager
+    from mythril_amd.workloads import KeccakFunctionManager as KeccakManager
     from mythril_amd.smt import And, Array, If, symbol_factory
     BVV, BVS = symbol_factory.BitVecVal, symbol_factory.BitVecSym
 
