@@ -38,7 +38,9 @@ import os
 import re
 from typing import Dict, List, Optional
 
-NREG = 16                  # register-file slots (MG_NREG)
+# register-file slots (MG_NREG); A/B knob MYTHGPU_NREG (a library built with
+# MG_NREG_OVERRIDE to match: fewer slots, fewer VGPRs, more waves per SIMD)
+NREG = int(os.environ.get("MYTHGPU_NREG", "16"))
 FB = 8                     # first VGPR of the file
 XB = 0                     # X temps v0..v7   (guard below the file)
 YB = FB + 8 * NREG         # Y temps v136..v143 (guard above the file)
@@ -209,11 +211,12 @@ IN = {k: "%%[%s]" % k for k in ("desc", "seed", "first", "leaves", "stride", "lo
 # Every operand lives in a FIXED register (physical-register constraints in
 # mg_interp_asm.hip, generated from this table): compiled programs (jit.py),
 # assembled apart from the kernel, address them by these names too.
-PINNED = {"root": "v164", "idx_lo": "v165", "idx_hi": "v166", "lds": "v167",
+PINNED = {"root": v(NVGPR_FIXED), "idx_lo": v(NVGPR_FIXED + 1), "idx_hi": v(NVGPR_FIXED + 2),
+          "lds": v(NVGPR_FIXED + 3),
           "desc": "s[16:17]", "seed": "s[18:19]", "first": "s[20:21]", "leaves": "s[22:23]",
           "stride": "s[24:25]", "lout": "s[26:27]", "probes": "s[28:29]", "mode": "s30",
           "scr": "s31", "active": "s[32:33]", "table": "s[34:35]"}
-NVGPR_KERNEL = 168         # the kernel's VGPR budget (3 waves / SIMD)
+NVGPR_KERNEL = NVGPR_FIXED + 4   # the kernel's VGPR budget (168: 3 waves / SIMD)
 # mg_pdesc byte offsets the assembly reads (mg_device.h)
 PDESC_CONSTS, PDESC_XCODE, PDESC_BTAB, PDESC_JIT = 0x8, 0x30, 0x38, 0x40
 

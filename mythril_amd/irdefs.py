@@ -20,7 +20,7 @@ def _parse():
 
 
 OPS, DEFINES = _parse()
-NREG = DEFINES["NREG"]
+NREG = int(os.environ.get("MYTHGPU_NREG", DEFINES["NREG"]))   # (A/B builds: asmgen.NREG)
 TRASH = NREG - 1
 MAX_WIDTH = DEFINES["MAX_WIDTH"]
 MAX_LDS = DEFINES["MAX_LDS"]
