@@ -40,8 +40,32 @@ SEED = 0x6D797468
 # stand-in query streams (mythril_amd/workloads.py): distinct queries per step
 STREAM_QUERIES = 256
 # LDS spill tier of the context (mg_api.cpp reads the same variable): the
-# compiled programs are translated for it
+# compiled programs are translated for it (apply_layout sets it per layout)
 LDS_SLOTS = int(os.environ.get("MYTHGPU_LDS_SLOTS", "6"))
+# Register layout per workload (profiles/r05/nreg/): the C2
+# corpus barely spills and runs 3.7 % faster with a fourth wave per SIMD in
+# an 11-slot register file (libmythgpu_w4.so); the query streams spill more
+# at 11 slots and lose 11 %, so they keep the 16-slot, three-wave default.
+# An explicit MYTHGPU_NREG wins.
+WORKLOAD_NREG = {"c2": 11}
+
+
+def apply_layout(workload) -> int:
+    """Set this process's register layout for ``workload`` — MYTHGPU_NREG
+    and the LDS regions that fit it (build.LAYOUT_LDS_SLOTS) — before
+    anything imports the compiler or the engine; returns the slot count."""
+    global LDS_SLOTS
+    from mythril_amd.build import LAYOUT_LDS_SLOTS
+    if "MYTHGPU_NREG" not in os.environ and workload in WORKLOAD_NREG:
+        if "mythril_amd.irdefs" in sys.modules:
+            raise RuntimeError("register layout chosen after mythril_amd.irdefs was imported")
+        os.environ["MYTHGPU_NREG"] = str(WORKLOAD_NREG[workload])
+    nreg = int(os.environ.get("MYTHGPU_NREG", "16"))
+    if nreg not in LAYOUT_LDS_SLOTS:
+        raise RuntimeError("no library for a %d-slot register layout" % nreg)
+    os.environ.setdefault("MYTHGPU_LDS_SLOTS", str(LAYOUT_LDS_SLOTS[nreg]))
+    LDS_SLOTS = int(os.environ["MYTHGPU_LDS_SLOTS"])
+    return nreg
 _STREAM = None
 
 
@@ -138,7 +162,9 @@ def node_image(workload, corpus, workers, world):
     import tempfile
     from mythril_amd import jit
     ids = [d for d, _, _, _ in corpus]
-    key = "%s_%d_%d_%d_%d_lds%d" % (workload, len(ids), ids[0], ids[-1], sum(ids), LDS_SLOTS)
+    from mythril_amd import irdefs
+    key = "%s_%d_%d_%d_%d_lds%d_r%d" % (workload, len(ids), ids[0], ids[-1], sum(ids), LDS_SLOTS,
+                                        irdefs.NREG)
     cache = os.environ.get("MYTHGPU_JIT_CACHE") or (
         os.path.join(tempfile.gettempdir(), "mythgpu_jit_%d" % os.getuid()) if world > 1 else None)
     nw = max(workers, min(os.cpu_count() or 1, 64)) if world > 1 else workers
@@ -302,6 +328,11 @@ def cpu_baseline(corpus, budget_s=20.0, workload="c2", check=None):
     return base, sc
 
 
+def engine_lib_path() -> str:
+    from mythril_amd import engine
+    return engine._LIB_PATH
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -330,6 +361,7 @@ def main():
     args.jit = not args.interp
     if args.dags is None:
         args.dags = default_units(args.workload)
+    nreg = apply_layout(args.workload)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -465,7 +497,9 @@ def main():
                         "each" % (workload_txt, args.assign_log2)),
                        "dags": args.dags * (world if args.shard == "corpus" else 1),
                        "assignments_per_gpu": n_assign, "nodes_total": int(nodes_all),
-                       "shard": args.shard, "parallelism": "dp%d" % world},
+                       "shard": args.shard, "parallelism": "dp%d" % world,
+                       "register_layout": "%d slots, %d waves/SIMD, %d LDS regions"
+                                          % (nreg, 4 if nreg <= 11 else 3, LDS_SLOTS)},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
                          "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kern_ms,
@@ -481,7 +515,8 @@ def main():
                                                       (nodes_per_lane * n_assign)
                                                       if sq and sq.get("valu_insts") else None)},
             "kernel_key": key,
-            "runtime": dict(eng.runtime_info(), torch_hip=getattr(torch.version, "hip", None),
+            "runtime": dict(eng.runtime_info(), library=os.path.basename(engine_lib_path()),
+                            torch_hip=getattr(torch.version, "hip", None),
                             note="the library's NEEDED libamdhip64.so.7 binds to the runtime "
                                  "torch loaded first (tests/test_gpu_torch_runtime.py checks "
                                  "parity in that configuration)"),

@@ -38,21 +38,14 @@ def up_to_date() -> bool:
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-structurizecfg-skip-uniform-regions=true"]
 
 
-def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(),
-          flags=None) -> str:
-    if not force and out == LIB and up_to_date():
-        return LIB
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    # the assembly interpreter's body and handler numbering are generated
-    from mythril_amd import asmgen
-    asmgen.write_outputs(CSRC)
+def _compile(csrc: str, out: str, defines=(), flags=None, verbose: bool = False) -> str:
     objs = []
     for src in SOURCES:
         obj = out + "." + src + ".o"
         cmd = [HIPCC, "--offload-arch=" + ARCH] + (HIP_FLAGS if flags is None else flags) + \
               ["-D" + d for d in defines] + [
-               "-I" + os.path.join(ROOT, "include"), "-I" + CSRC, "-c",
-               os.path.join(CSRC, src), "-o", obj]
+               "-I" + os.path.join(ROOT, "include"), "-I" + csrc, "-c",
+               os.path.join(csrc, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
@@ -63,8 +56,59 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     os.replace(tmp, out)
     for o in objs:
         os.remove(o)
+    return out
+
+
+def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(),
+          flags=None) -> str:
+    if not force and out == LIB and up_to_date():
+        return LIB
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    # the assembly interpreter's body and handler numbering are generated
+    from mythril_amd import asmgen
+    asmgen.write_outputs(CSRC)
+    _compile(CSRC, out, defines, flags, verbose)
     if out == LIB:
         build_jit_stub()
+    return out
+
+
+# Register layouts: 16 slots at three waves per SIMD (the
+# default library) and 11 slots at four (128 VGPRs, five LDS regions of
+# 40 KiB per block).  A layout other than 16 is generated under
+# MYTHGPU_NREG into a private copy of csrc/, so the tracked generated files
+# stay the default's.
+LIB_W4 = os.path.join(LIBDIR, "libmythgpu_w4.so")
+LAYOUTS = {16: (LIB, ()),
+           11: (LIB_W4, ("MG_NREG_OVERRIDE=11", "MG_ASM_WAVES_PER_SIMD=4",
+                         "MG_LDS_SLOTS_DEFAULT=5"))}
+LAYOUT_LDS_SLOTS = {16: 6, 11: 5}
+
+
+def lib_for_layout(nreg: int) -> str:
+    if nreg not in LAYOUTS:
+        raise ValueError("no library for a %d-slot register layout (have %s)"
+                         % (nreg, sorted(LAYOUTS)))
+    return LAYOUTS[nreg][0]
+
+
+def build_layout(nreg: int, force: bool = False, verbose: bool = False) -> str:
+    out, defines = LAYOUTS[nreg]
+    if nreg == 16:
+        return build(force, verbose)
+    if not force and _fresh(out, _deps()):
+        return out
+    import shutil
+    import tempfile
+    os.makedirs(LIBDIR, exist_ok=True)
+    with tempfile.TemporaryDirectory() as td:
+        src = os.path.join(td, "csrc")
+        shutil.copytree(CSRC, src)
+        code = ("import sys; sys.path.insert(0, %r); from mythril_amd import asmgen; "
+                "assert asmgen.NREG == %d; asmgen.write_outputs(%r)" % (ROOT, nreg, src))
+        subprocess.run([sys.executable, "-c", code], check=True,
+                       env=dict(os.environ, MYTHGPU_NREG=str(nreg)))
+        _compile(src, out, defines, None, verbose)
     return out
 
 
@@ -116,4 +160,5 @@ def build_compiler(force: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    print(build_layout(11, force="--force" in sys.argv))
     print(build_compiler(force="--force" in sys.argv))

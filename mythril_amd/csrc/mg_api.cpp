@@ -30,6 +30,13 @@ hipError_t mg_launch_keccak(const uint8_t* d_data, const uint64_t* d_off, const 
                             uint32_t n, uint8_t* d_out, hipStream_t stream);
 
 
+// LDS spill regions per lane when MYTHGPU_LDS_SLOTS is unset: 6 fill the
+// CU at three 256-lane blocks (13 halves, mg_lds_bytes); the four-wave
+// layout (MG_ASM_WAVES_PER_SIMD=4, four blocks per CU) is built with 5
+#ifndef MG_LDS_SLOTS_DEFAULT
+#define MG_LDS_SLOTS_DEFAULT 6
+#endif
+
 struct mg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -39,7 +46,7 @@ struct mg_ctx {
     // assembly interpreter: handler byte offsets (query launch at init) and
     // LDS spill slots per 256-lane block
     uint32_t hoff[MGA_NUM_HANDLERS] = {0};
-    uint32_t lds_slots = 6;
+    uint32_t lds_slots = MG_LDS_SLOTS_DEFAULT;
     // generator boundary-value table (device, 48 KiB; MG_BTAB_WORDS)
     uint32_t* d_btab = nullptr;
     // grow-only device workspace for synchronous calls

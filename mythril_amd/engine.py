@@ -17,10 +17,19 @@ import numpy as np
 
 from .ir import Program
 
+
+def _layout_lib() -> str:
+    """The in-tree library of this process's register layout
+    (``MYTHGPU_NREG``: 16 slots / three waves per SIMD by default, 11 / four
+    in ``libmythgpu_w4.so``; build.LAYOUTS)."""
+    from . import irdefs
+    from .build import lib_for_layout
+    return lib_for_layout(irdefs.NREG)
+
+
 # (MYTHGPU_LIB: an A/B build of the same ABI, with the asmgen knobs it was
 # built under set in the environment)
-_LIB_PATH = os.environ.get("MYTHGPU_LIB") or \
-    os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmythgpu.so")
+_LIB_PATH = os.environ.get("MYTHGPU_LIB") or _layout_lib()
 
 EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
            "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",

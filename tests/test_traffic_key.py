@@ -9,19 +9,58 @@ bench line with ``traffic: null``.  CPU-only: the key is computed from the
 generator and the compiled corpus, no GPU."""
 import json
 import os
-
-import bench
-from mythril_amd import asmgen
+import subprocess
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench_env():
+    """The environment a default bench run starts from (no layout knobs)."""
+    env = dict(os.environ)
+    for k in ("MYTHGPU_NREG", "MYTHGPU_LDS_SLOTS", "MYTHGPU_LIB"):
+        env.pop(k, None)
+    return env
+
+
+def _run_json(code: str):
+    out = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=_bench_env(), check=True,
+                         capture_output=True, text=True, timeout=600).stdout
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def kernel_key_as_bench(workload: str, dags: int):
+    """bench.kernel_key of a default ``bench.py --workload <workload>`` run,
+    computed in a fresh process under the register layout bench.py picks for
+    the workload (bench.apply_layout, before the compiler is imported)."""
+    return _run_json(
+        "import json, os, bench\n"
+        "bench.apply_layout(%r)\n"
+        "from mythril_amd import asmgen\n"
+        "corpus = bench.build_corpus(%d, min(8, os.cpu_count() or 1), workload=%r)\n"
+        "print(json.dumps(bench.kernel_key(asmgen.digest(), %r, %d, 20, True, corpus)))\n"
+        % (workload, dags, workload, workload, dags))
+
+
+def test_bench_register_layouts():
+    """C2 runs the 11-slot, four-wave layout with five LDS regions; the query
+    streams the 16-slot default with six."""
+    got = _run_json(
+        "import json, os, bench\n"
+        "out = {}\n"
+        "for w in ('c2', 'c3', 'c4', 'c5'):\n"
+        "    for k in ('MYTHGPU_NREG', 'MYTHGPU_LDS_SLOTS'):\n"
+        "        os.environ.pop(k, None)\n"
+        "    out[w] = [bench.apply_layout(w), bench.LDS_SLOTS]\n"
+        "print(json.dumps(out))\n")
+    assert got == {"c2": [11, 5], "c3": [16, 6], "c4": [16, 6], "c5": [16, 6]}
 
 
 def test_traffic_json_keyed_to_this_tree():
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as fh:
         tj = json.load(fh)
     entries = tj["entries"]
-    corpus = bench.build_corpus(4096, min(8, os.cpu_count() or 1))
-    key = bench.kernel_key(asmgen.digest(), "c2", 4096, 20, True, corpus)
+    key = kernel_key_as_bench("c2", 4096)
     c2 = [e for e in entries if e["kernel_key"].get("workload") == "c2"]
     assert c2, "profiles/traffic.json has no C2 entry"
     diff = sorted(k for k in key if c2[0]["kernel_key"].get(k) != key[k])
