@@ -22,7 +22,9 @@ ARGS="$@"
 ( while true; do date >> $P/heartbeat.txt; sleep 45; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-timeout -k 10 300 python3 bench.py --jit-build-only $ARGS > $P/prebuild.log 2>&1 || exit 1
+# (the prebuild runs outside the profiler: it may use a worker pool; the
+# C2 image of the 11-slot layout takes ~290 s on one worker)
+MYTHGPU_BENCH_WORKERS=16 timeout -k 10 600 python3 bench.py --jit-build-only $ARGS > $P/prebuild.log 2>&1 || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $P/kt -o kt -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $ARGS > $P/kt.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/fetch -o fetch -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > $P/fetch.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/write -o write -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline $ARGS > $P/write.log 2>&1 || exit 1
