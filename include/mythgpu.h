@@ -217,7 +217,10 @@ int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32
                  uint32_t max_record_words, uint32_t* n_record_words, uint32_t* masks,
                  uint32_t max_mask_words, uint32_t* n_mask_words);
 /* Build configuration (no GPU needed): out[0..3] = version, MG_NREG,
- * MG_MAX_LDS, MG_MAX_PSLOTS — programs must be compiled for these. */
+ * MG_MAX_LDS, MG_MAX_PSLOTS — programs must be compiled for these.  Two
+ * builds export this same ABI: libmythgpu.so (16 register slots, three
+ * waves per SIMD) and libmythgpu_w4.so (11 slots, four waves);
+ * a caller compiles for the MG_NREG of the library it loaded. */
 int mg_config(uint32_t* out, uint32_t n);
 
 #ifdef __cplusplus
