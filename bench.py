@@ -62,8 +62,11 @@ def apply_layout(workload) -> int:
         os.environ["MYTHGPU_NREG"] = str(WORKLOAD_NREG[workload])
     nreg = int(os.environ.get("MYTHGPU_NREG", "16"))
     if nreg not in LAYOUT_LDS_SLOTS:
-        raise RuntimeError("no library for a %d-slot register layout" % nreg)
-    os.environ.setdefault("MYTHGPU_LDS_SLOTS", str(LAYOUT_LDS_SLOTS[nreg]))
+        # an A/B build of another layout names its library and LDS regions
+        if not (os.environ.get("MYTHGPU_LIB") and os.environ.get("MYTHGPU_LDS_SLOTS")):
+            raise RuntimeError("no library for a %d-slot register layout" % nreg)
+    else:
+        os.environ.setdefault("MYTHGPU_LDS_SLOTS", str(LAYOUT_LDS_SLOTS[nreg]))
     LDS_SLOTS = int(os.environ["MYTHGPU_LDS_SLOTS"])
     return nreg
 _STREAM = None
@@ -328,6 +331,12 @@ def cpu_baseline(corpus, budget_s=20.0, workload="c2", check=None):
     return base, sc
 
 
+def waves_per_simd() -> int:
+    """Waves per SIMD the layout's VGPR budget allows (512 per lane)."""
+    from mythril_amd import asmgen
+    return 512 // asmgen.NVGPR_KERNEL
+
+
 def engine_lib_path() -> str:
     from mythril_amd import engine
     return engine._LIB_PATH
@@ -499,7 +508,7 @@ def main():
                        "assignments_per_gpu": n_assign, "nodes_total": int(nodes_all),
                        "shard": args.shard, "parallelism": "dp%d" % world,
                        "register_layout": "%d slots, %d waves/SIMD, %d LDS regions"
-                                          % (nreg, 4 if nreg <= 11 else 3, LDS_SLOTS)},
+                                          % (nreg, waves_per_simd(), LDS_SLOTS)},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
                          "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kern_ms,
