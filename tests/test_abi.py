@@ -32,6 +32,29 @@ def test_library_exports_every_declared_symbol():
     assert lib.mg_config(cfg, 4) == 0 and cfg[1] >= 8
 
 
+def test_four_wave_build_exports_the_same_abi():
+    """libmythgpu_w4.so (bench's C2 layout) exports every declared symbol,
+    reports 11 register slots, and was generated from the current generator
+    under that layout (its digest, computed in a fresh process)."""
+    import json
+    import subprocess
+    import sys
+    lib = ctypes.CDLL(build.LIB_W4)
+    for n in declared():
+        assert hasattr(lib, n), n
+    lib.mg_config.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]
+    cfg = (ctypes.c_uint32 * 4)()
+    assert lib.mg_config(cfg, 4) == 0 and cfg[1] == 11
+    lib.mg_asm_digest.restype = ctypes.c_char_p
+    env = dict(os.environ, MYTHGPU_NREG="11")
+    out = subprocess.run([sys.executable, "-c", "import json; from mythril_amd import asmgen; "
+                          "print(json.dumps([asmgen.digest(), asmgen.NVGPR_KERNEL]))"],
+                         cwd=build.ROOT, env=env, check=True, capture_output=True, text=True).stdout
+    digest, nvgpr = json.loads(out.strip().splitlines()[-1])
+    assert lib.mg_asm_digest().decode() == digest
+    assert nvgpr == 128          # 512 / 128 = four waves per SIMD
+
+
 def test_version_without_gpu():
     assert load_library().mg_version() == 3
 
