@@ -1095,6 +1095,21 @@ struct Solver {
     Lowerer& lw;
     std::vector<LN>& ln;
     OMap<int, int> repl;                   // LEAF id -> definition
+    // dense mirror of repl for the lookups (rewrite, depends, try_define):
+    // LEAF id -> definition, -1 when undefined
+    std::vector<int> repl_of_;
+    const int* repl_find(int x) const {
+        return (size_t)x < repl_of_.size() && repl_of_[x] >= 0 ? &repl_of_[x] : nullptr;
+    }
+    void repl_put(int k, int v) {
+        repl.put(k, v);
+        if ((size_t)k >= repl_of_.size()) repl_of_.resize(std::max<size_t>(k + 1, 2 * repl_of_.size()), -1);
+        repl_of_[k] = v;
+    }
+    void repl_truncate(size_t n) {
+        for (size_t i = n; i < repl.items.size(); i++) repl_of_[repl.items[i].first] = -1;
+        repl.truncate(n);
+    }
     int one, zero;
     int n_aux = 0, n_branch = 0;
     std::unordered_set<int> selectors, or_seen;
@@ -1347,7 +1362,7 @@ struct Solver {
                 if (r >= 0 && !depof(r).meets(dmask)) continue;
             }
             if (ln[x].op == MG_LEAF) {
-                const int* e = repl.find(x);
+                const int* e = repl_find(x);
                 if (!e) { memo.put(x, x); continue; }
                 int ev = *e;
                 int r = memo.get(ev);
@@ -1798,7 +1813,7 @@ struct Solver {
             if (x == leaf) return true;
             if (stamped(x, g)) continue;
             if (ln[x].op == MG_LEAF) {
-                const int* d = repl.find(x);
+                const int* d = repl_find(x);
                 if (d) stack.push_back(*d);
                 continue;
             }
@@ -1808,15 +1823,15 @@ struct Solver {
     }
 
     bool try_define(int leaf, int e) {
-        if (ln[leaf].op != MG_LEAF || repl.has(leaf)) return false;
+        if (ln[leaf].op != MG_LEAF || repl_find(leaf)) return false;
         if (selectors.count(leaf) && ln[e].op != MG_CONST) return false;
         if (ln[e].width > ln[leaf].width && !(ln[e].op == MG_CONST && shr(ln[e].imm, ln[leaf].width).zero()))
             return false;
         if (depends(e, leaf)) return false;
-        repl.put(leaf, e);
+        repl_put(leaf, e);
         leaf_imm[leaf] = (int)ln[leaf].imm.w[0];
         leaf_node[leaf] = leaf;
-        dm_valid = false;
+        if (dm_valid) dm.set(leaf_imm[leaf]);   // the mask only grows here
         return true;
     }
 
@@ -1977,7 +1992,7 @@ struct Solver {
             OMap<int, int> defs;
             for (size_t i = saved; i < repl.items.size(); i++) defs.put(repl.items[i].first, repl.items[i].second);
             per.push_back(std::move(defs));
-            repl.truncate(saved);
+            repl_truncate(saved);
             dm_valid = false;
         }
         unsat = unsat_saved;
