@@ -2568,7 +2568,8 @@ static std::vector<std::vector<U>> leaf_pools(const std::vector<LN>& ln, const s
 }
 
 // ir.scan_const_keys
-static OMap<std::string, std::vector<Big>> scan_const_keys(const std::vector<Src>& S, const std::vector<int>& roots,
+// (``order``: topo(S, roots), computed once by the caller)
+static OMap<std::string, std::vector<Big>> scan_const_keys(const std::vector<Src>& S, const std::vector<int>& order,
                                                            int cap, int max_links,
                                                            std::unordered_map<std::string, int>& sym_counts) {
     OMap<std::string, std::vector<Big>> out;
@@ -2586,7 +2587,7 @@ static OMap<std::string, std::vector<Big>> scan_const_keys(const std::vector<Src
             sym.setdefault(name, {}).insert(key);
         }
     };
-    for (int n : topo(S, roots)) {
+    for (int n : order) {
         if (S[n].op == S_SELECT) {
             std::vector<int> stack{S[n].args[0]};
             std::unordered_set<int> seen;
@@ -2621,9 +2622,9 @@ static OMap<std::string, std::vector<Big>> scan_const_keys(const std::vector<Src
 // search-mode inputs: candidate hints (model.harvest_hints) and ABI presets
 // (abi.plan / Plan.view)
 // ---------------------------------------------------------------------------
-static void harvest_hints(const std::vector<Src>& S, const std::vector<int>& cons, std::vector<U>& out) {
+static void harvest_hints(const std::vector<Src>& S, const std::vector<int>& order, std::vector<U>& out) {
     U M256 = mask(256), low6 = ~U::of(63);
-    for (int n : topo(S, cons)) {
+    for (int n : order) {                                 // topo(S, cons)
         if (S[n].op != S_BVNUM || S[n].width < 8) continue;
         U v = S[n].val.chunk(0);                         // (v + 63) & ~63, mod 2^256
         out.push_back((v + U::of(63)) & M256 & low6);
@@ -2698,8 +2699,8 @@ static bool word_of(const std::vector<Src>& S, int base, int arr, int64_t& first
     return true;
 }
 
-static bool abi_plan(const std::vector<Src>& S, const std::vector<int>& cons, Presets& out) {
-    std::vector<int> nodes = topo(S, cons);
+static bool abi_plan(const std::vector<Src>& S, const std::vector<int>& nodes, Presets& out) {
+    // nodes: topo(S, cons)
     struct Arr { int arr; std::vector<Big> consts; std::vector<int> sym; };
     OMap<int, Arr> by_arr;
     for (int n : nodes) {
@@ -2892,9 +2893,11 @@ static void compile(const mgc_input* in, mgc_result* res) {
     all.insert(all.end(), probes.begin(), probes.end());
 
     std::vector<U> hints;
-    if (in->search_hints) harvest_hints(S, cons, hints);
+    std::vector<int> cons_order;                         // one walk for both scans
+    if (in->search_hints || in->abi_presets) cons_order = topo(S, cons);
+    if (in->search_hints) harvest_hints(S, cons_order, hints);
     Presets presets;
-    bool have_presets = in->abi_presets && abi_plan(S, cons, presets);
+    bool have_presets = in->abi_presets && abi_plan(S, cons_order, presets);
     if (have_presets) {
         // the query under the presets (Plan.view): each pinned node becomes
         // the numeral, keeping its id
@@ -2919,10 +2922,11 @@ static void compile(const mgc_input* in, mgc_result* res) {
     lw.solve = in->solve != 0;
     if (in->const_keys || in->solve) {
         std::unordered_map<std::string, int> sym_counts;
-        auto ck = scan_const_keys(S, all, in->solve ? 256 : 128, in->solve ? 8192 : 2048, sym_counts);
+        const std::vector<int> all_order = topo(S, all);  // after the presets
+        auto ck = scan_const_keys(S, all_order, in->solve ? 256 : 128, in->solve ? 8192 : 2048, sym_counts);
         if (in->const_keys) lw.table_ckeys = ck;
         if (in->solve) {
-            for (int n : topo(S, all)) {
+            for (int n : all_order) {
                 if (S[n].op == S_ARRAY || S[n].op == S_APPLY) {
                     auto it = sym_counts.find(S[n].str);
                     if ((it == sym_counts.end() ? 0 : it->second) <= ARG_ENTRIES_CAP) lw.solve_tables.insert(S[n].str);
