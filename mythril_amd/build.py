@@ -64,9 +64,11 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     if not force and out == LIB and up_to_date():
         return LIB
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    # the assembly interpreter's body and handler numbering are generated
-    from mythril_amd import asmgen
-    asmgen.write_outputs(CSRC)
+    # the assembly interpreter's body and handler numbering are generated —
+    # for the default 16-slot layout whatever this process's MYTHGPU_NREG
+    # (an 11-slot generator would overwrite the tracked sources
+    # and pair 11-slot handlers with the C code's 16 slots)
+    _generate(16, CSRC)
     _compile(CSRC, out, defines, flags, verbose)
     if out == LIB:
         build_jit_stub()
@@ -92,6 +94,20 @@ def lib_for_layout(nreg: int) -> str:
     return LAYOUTS[nreg][0]
 
 
+def _generate(nreg: int, dst: str) -> None:
+    """asmgen's outputs for a ``nreg``-slot layout into ``dst`` (in this
+    process when its generator already has that layout, else in a child
+    with MYTHGPU_NREG set to it)."""
+    from mythril_amd import asmgen
+    if asmgen.NREG == nreg:
+        asmgen.write_outputs(dst)
+        return
+    code = ("import sys; sys.path.insert(0, %r); from mythril_amd import asmgen; "
+            "assert asmgen.NREG == %d; asmgen.write_outputs(%r)" % (ROOT, nreg, dst))
+    subprocess.run([sys.executable, "-c", code], check=True,
+                   env=dict(os.environ, MYTHGPU_NREG=str(nreg)))
+
+
 def build_layout(nreg: int, force: bool = False, verbose: bool = False) -> str:
     out, defines = LAYOUTS[nreg]
     if nreg == 16:
@@ -104,10 +120,7 @@ def build_layout(nreg: int, force: bool = False, verbose: bool = False) -> str:
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "csrc")
         shutil.copytree(CSRC, src)
-        code = ("import sys; sys.path.insert(0, %r); from mythril_amd import asmgen; "
-                "assert asmgen.NREG == %d; asmgen.write_outputs(%r)" % (ROOT, nreg, src))
-        subprocess.run([sys.executable, "-c", code], check=True,
-                       env=dict(os.environ, MYTHGPU_NREG=str(nreg)))
+        _generate(nreg, src)
         _compile(src, out, defines, None, verbose)
     return out
 

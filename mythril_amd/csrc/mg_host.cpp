@@ -365,6 +365,32 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             order[t] = moved;
         }
     }
+    // A store-chain link: t = (a == b) of wide values, consumed only by the
+    // next instruction, an ITE on t -> one EQSEL record.  Decided up front
+    // (it depends on the order only): the dirty one-limb scan below must know
+    // that such an ITE reads all eight limbs of its value operands (EQSEL
+    // copies them), not limb 0 as a w <= 32 ITE does.
+    std::vector<uint8_t> eqsel(n_ins + 1, 0), eqsel_ite(n_ins + 1, 0);
+    for (uint32_t pc = 0; pc + 1 < n_ins; ++pc) {
+        const uint32_t* in = code + 4 * order[pc];
+        const uint32_t op = in[0] & 0xFF, w = (in[0] >> 8) & 0x3FF, d = in[1] & 0xFF;
+        if (op != MG_EQ || w <= 32 || (in[0] & MG_ROOT_FLAG)) continue;
+        const uint32_t* nx = code + 4 * order[pc + 1];
+        const uint32_t na = (nx[1] >> 8) & 0xFF, nb = (nx[1] >> 16) & 0xFF, nc = (nx[1] >> 24) & 0xFF;
+        bool fuse = (nx[0] & 0xFF) == MG_ITE && !(nx[0] & MG_ROOT_FLAG) && nc == d && na != d && nb != d;
+        for (uint32_t q = pc + 2; fuse && q < n_ins; ++q) {     // is t dead after the ITE?
+            const uint32_t* f = code + 4 * order[q];
+            const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
+                           fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
+            if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) fuse = false;
+            else if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
+        }
+        if (fuse) {
+            eqsel[pc] = 1;
+            eqsel_ite[pc + 1] = 1;
+            ++pc;
+        }
+    }
     for (uint32_t pc = 0; pc <= n_ins; ++pc) {
         if (pc == n_ins) {          // HALT, then one zeroed record (prefetch pad)
             if (pending) wait_vm();
@@ -378,36 +404,23 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         if (op == MG_SPILL && (pl & PL_DEAD)) continue;     // never reloaded
         const uint32_t d = in[1] & 0xFF, a = (in[1] >> 8) & 0xFF, b = (in[1] >> 16) & 0xFF,
                        c = (in[1] >> 24) & 0xFF;
-        // a store-chain link: t = (a == b) of wide values, consumed only by
-        // the next instruction, an ITE on t -> one EQSEL record
-        if (op == MG_EQ && w > 32 && !(in[0] & MG_ROOT_FLAG) && pc + 1 < n_ins) {
+        if (eqsel[pc]) {
             const uint32_t* nx = code + 4 * order[pc + 1];
             const uint32_t nd = nx[1] & 0xFF, na = (nx[1] >> 8) & 0xFF, nb = (nx[1] >> 16) & 0xFF,
                            nc = (nx[1] >> 24) & 0xFF;
-            bool fuse = (nx[0] & 0xFF) == MG_ITE && !(nx[0] & MG_ROOT_FLAG) && nc == d &&
-                        na != d && nb != d;
-            for (uint32_t q = pc + 2; fuse && q < n_ins; ++q) {     // is t dead after the ITE?
-                const uint32_t* f = code + 4 * order[q];
-                const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
-                               fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
-                if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) fuse = false;
-                else if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
-            }
-            if (fuse) {
-                const uint32_t touch = slots_touched(op, d, a, b, c) | slots_touched(MG_ITE, nd, na, nb, nc);
-                if (pending & touch) wait_vm();
-                uint32_t* r = emit();
-                uint32_t var;
-                r[1] = 8 * nd; r[2] = 8 * a; r[3] = 8 * b;
-                if (nd == na) { var = MGA_V_NEG; r[4] = 8 * nb; }          // keep F[d] where equal
-                else if (nd == nb) { var = 0; r[4] = 8 * na; }             // take F[a] where equal
-                else { var = MGA_V_GEN; r[4] = 8 * na; r[5] = 8 * nb; }
-                r[0] = hoff[MGA_HID(MGA_EQSEL, var, bank)];
-                bank = 1 - bank;
-                clean[nd] = ((nx[0] >> 8) & 0x3FF) <= 32;     // canonical values
-                ++pc;
-                continue;
-            }
+            const uint32_t touch = slots_touched(op, d, a, b, c) | slots_touched(MG_ITE, nd, na, nb, nc);
+            if (pending & touch) wait_vm();
+            uint32_t* r = emit();
+            uint32_t var;
+            r[1] = 8 * nd; r[2] = 8 * a; r[3] = 8 * b;
+            if (nd == na) { var = MGA_V_NEG; r[4] = 8 * nb; }          // keep F[d] where equal
+            else if (nd == nb) { var = 0; r[4] = 8 * na; }             // take F[a] where equal
+            else { var = MGA_V_GEN; r[4] = 8 * na; r[5] = 8 * nb; }
+            r[0] = hoff[MGA_HID(MGA_EQSEL, var, bank)];
+            bank = 1 - bank;
+            clean[nd] = ((nx[0] >> 8) & 0x3FF) <= 32;     // canonical values
+            ++pc;
+            continue;
         }
         const bool leafd = op == MG_LEAF && w == 256;
         const bool reloadd = op == MG_RELOAD && !(pl & PL_LDS);
@@ -443,8 +456,8 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
                 if (rd & (1u << d)) {
                     read = true;
                     const bool limb0 =
-                        (has_w32(fop) && fw <= 32 && fop != MG_EXTRACT) ||
-                        (fop == MG_ITE && fc == d && fa != d && fb != d) ||
+                        (has_w32(fop) && fw <= 32 && fop != MG_EXTRACT && !eqsel_ite[q]) ||
+                        (fop == MG_ITE && fc == d && fa != d && fb != d && !eqsel_ite[q]) ||
                         fop == MG_ROOT ||
                         (fop == MG_SPILL && (place[order[q]] & PL_NARROW));
                     if (!limb0) dirty = false;

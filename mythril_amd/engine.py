@@ -120,6 +120,13 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
                                     "(digest %s, generator %s); rebuild with "
                                     "`python -m mythril_amd.build`" % (path, got, want))
         if check_digest:
+            # the compiler allocates irdefs.NREG slots: the library's
+            # translator and interpreter must hold as many
+            from . import irdefs
+            cfg = (C.c_uint32 * 4)()
+            if lib.mg_config(cfg, 4) != 0 or cfg[1] != irdefs.NREG:
+                raise EngineUnavailable("%s holds %d register slots, the compiler %d "
+                                        "(MYTHGPU_NREG)" % (path, cfg[1], irdefs.NREG))
             _libs[path] = lib
         return lib
 

@@ -243,7 +243,7 @@ class World:
     def query(self, extra: Sequence[S.Bool] = ()) -> List[N.Node]:
         q = Query(c.raw for c in list(self.constraints) + list(extra))
         if extra:                              # a module's check: "open" unless labelled
-            q.label = _CHECK_LABELS.pop(id(extra[-1]), "open")
+            q.label = getattr(extra[-1], "check_label", "open")
         return q
 
 
@@ -377,12 +377,14 @@ _BAL, _ALLOW, _OWNER_PAUSED, _TOTAL = 1, 2, 3, 0
 # tests/planted.py looks for a model).  The label belongs to the check as
 # created on its path (the wrapper object: hash-consing gives the same node to
 # the same check expression on different paths, e.g. BECToken's multiply
-# check after one or two receivers); the query streams do not depend on it.
-_CHECK_LABELS: Dict[int, str] = {}
+# check after one or two receivers), kept as an attribute of that object
+# (an id()-keyed map could hand a stale label to a later object at
+# the same address, and popping it made a second query of one check "open");
+# the query streams do not depend on it.
 
 
 def _label(chk: S.Bool, label: str) -> S.Bool:
-    _CHECK_LABELS[id(chk)] = label
+    chk.check_label = label
     return chk
 
 

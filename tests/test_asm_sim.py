@@ -481,3 +481,51 @@ def test_spill_placement_stand_in_units(workload, unit, n_lds, jit):
         asg = unpack(prog, lout[:, :, lane])
         want = R.eval_constraints(list(roots), R.Assignment(asg.vars, asg.arrays, asg.funcs))
         assert bool(root[lane]) == bool(want), lane
+
+
+@pytest.mark.parametrize("jit", [False, True])
+def test_dirty_one_limb_value_never_reaches_eqsel(jit):
+    """a one-limb result left dirty (limbs 1..7 stale,
+    the DC handler writes limb 0 only) is safe only for limb-0 readers.  A
+    w <= 32 ITE right after a wide EQ on its condition is fused into EQSEL,
+    which copies all eight limbs of its value operands and marks the result
+    clean — so a dirty value operand must not be left dirty.  Hand-written
+    IR: slot 4 holds a wide leaf, EXTRACT w=8 overwrites it, EQ(w=256) +
+    ITE(w=8) select it, and the ITE result is read at full width (OUT and a
+    256-bit ADD)."""
+    from mythril_amd import irdefs as I
+    x, y, k, z = (N.bv_var(n, 256) for n in ("x", "y", "k", "z"))
+    v = N.bv_var("v", 8)
+    base = compile_constraints([], [x, y, k, z, v, x])
+    li = {l.name: i for i, l in enumerate(base.leaves)}
+    code = [
+        (I.w0(I.LEAF, 256), I.w1(0), li["x"]),
+        (I.w0(I.LEAF, 256), I.w1(1), li["y"]),
+        (I.w0(I.LEAF, 256), I.w1(2), li["k"]),
+        (I.w0(I.LEAF, 8), I.w1(3), li["v"]),
+        (I.w0(I.LEAF, 256), I.w1(4), li["z"]),               # slot 4: a wide value
+        (I.w0(I.EXTRACT, 8), I.w1(4, 0), 0),                  # x[7:0] into slot 4
+        (I.w0(I.EQ, 256), I.w1(5, 1, 2), 0),
+        (I.w0(I.ITE, 8), I.w1(6, 4, 3, 5), 0),                # EQSEL candidate
+        (I.w0(I.OUT, 8), I.w1(0, 6), 0),
+        (I.w0(I.ADD, 256), I.w1(7, 6, 6), 0),
+        (I.w0(I.OUT, 256), I.w1(0, 7), 1),
+    ]
+    prog = base
+    prog.code = np.array([[a, b, c, 0] for a, b, c in code], dtype=np.uint32)
+    prog.n_probes = 2
+    fams = [f for f, _ in _record_handlers(prog)]
+    assert "EQSEL" in fams and "ITE" not in fams         # the fused shape is exercised
+    rng = random.Random(11)
+    asgs = []
+    for lane in range(64):
+        yy = rng.getrandbits(256)
+        asgs.append(PA(vars={"x": rng.getrandbits(256), "y": yy,
+                             "k": yy if lane % 2 else rng.getrandbits(256),
+                             "z": (1 << 256) - 1 - lane, "v": rng.getrandbits(8)}))
+    _, pr, _, _ = asm_sim.simulate(prog, pack(prog, asgs), jit=jit)
+    for a, asg in enumerate(asgs):
+        vv = asg.vars
+        sel = (vv["x"] & 0xFF) if vv["y"] == vv["k"] else vv["v"]
+        assert limbs_to_int(pr[0, :, a]) == sel, (a, hex(limbs_to_int(pr[0, :, a])))
+        assert limbs_to_int(pr[1, :, a]) == 2 * sel, a

@@ -12,6 +12,12 @@ static properties, so the test also asserts that every
 (family, variant) the bench configurations execute — reported by the
 translator itself (``engine.handler_variants``) — belongs to a program this
 test checked lane by lane.
+
+The module runs on the register layout of its process (``MYTHGPU_NREG``):
+the default 16 slots, and — from ``tests/test_gpu_layout.py``, in a fresh
+process with ``MYTHGPU_NREG=11 MYTHGPU_LDS_SLOTS=5`` — the four-wave 11-slot
+layout (``libmythgpu_w4.so``) that ``bench.py`` runs C2 on.  Programs are
+compiled for the layout's slots and translated for its LDS regions.
 """
 
 import ctypes as C
@@ -21,7 +27,8 @@ import numpy as np
 import pytest
 
 import bench
-from mythril_amd import shard
+from mythril_amd import irdefs, shard
+from mythril_amd.build import LAYOUT_LDS_SLOTS, lib_for_layout
 from mythril_amd.engine import default_leafgen, handler_variants, unpack_bits
 
 pytestmark = pytest.mark.gpu
@@ -31,6 +38,21 @@ SEED = bench.SEED
 FULL = {w: bench.default_units(w) for w in ("c2", "c3", "c4", "c5")}
 # (family, variant) handlers of the programs verified lane by lane below
 CHECKED = set()
+# the LDS spill regions of this process's layout (the context reads the same
+# variable; bench.apply_layout sets it per layout)
+LDS = int(os.environ.get("MYTHGPU_LDS_SLOTS", LAYOUT_LDS_SLOTS[irdefs.NREG]))
+
+
+def test_layout_of_this_process(engine):
+    """The library, its slot count and the compiler's agree on one layout."""
+    got = C.c_uint32 * 4
+    cfg = got()
+    assert engine.lib.mg_config(cfg, 4) == 0
+    assert cfg[1] == irdefs.NREG
+    assert os.path.basename(bench.engine_lib_path()) == os.path.basename(lib_for_layout(irdefs.NREG))
+    assert LDS == LAYOUT_LDS_SLOTS[irdefs.NREG]
+    print("layout: %d slots, %d LDS regions, %s" % (irdefs.NREG, LDS,
+                                                     os.path.basename(bench.engine_lib_path())))
 
 
 def _oracle_unit(item):
@@ -93,7 +115,7 @@ def images(units):
     built on spawned workers."""
     from mythril_amd import jit
     return {w: jit.compile_batch([(p, None, d) for d, p, _ in units[w]], workers=16,
-                                 start="spawn") for w in FULL}
+                                 start="spawn", lds_slots=LDS) for w in FULL}
 
 
 @pytest.mark.parametrize("path", ["interp", "jit"])
@@ -114,7 +136,7 @@ def test_every_bench_unit_every_lane(engine, units, images, workload, path):
         n_hit += bool(hit.size)
     if path == "interp":
         for d, p, _ in us:
-            CHECKED.update(handler_variants(p))
+            CHECKED.update(handler_variants(p, LDS))
     print("%s %s: %d units, %d with satisfying lanes, %d satisfying lanes"
           % (workload, path, len(us), n_hit, n_sat))
 
@@ -128,12 +150,12 @@ def test_bench_handler_variants_all_checked(units):
     bench_set = set()
     for w in FULL:                      # the programs bench.compile_unit builds
         for d, p, _ in units[w]:
-            bench_set |= handler_variants(p)
+            bench_set |= handler_variants(p, LDS)
     missing = sorted(bench_set - CHECKED)
     assert not missing, missing
     fams = sorted({f for f, _ in bench_set})
-    print("bench configurations execute %d (family, variant) handlers in %d families"
-          % (len(bench_set), len(fams)))
+    print("bench configurations execute %d (family, variant) handlers in %d families "
+          "(%d-slot layout)" % (len(bench_set), len(fams), irdefs.NREG))
 
 
 def test_jit_attach_refuses_code_compiled_for_other_records(engine):
