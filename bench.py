@@ -67,7 +67,8 @@ def apply_layout(workload) -> int:
             raise RuntimeError("no library for a %d-slot register layout" % nreg)
     else:
         os.environ.setdefault("MYTHGPU_LDS_SLOTS", str(LAYOUT_LDS_SLOTS[nreg]))
-    LDS_SLOTS = int(os.environ["MYTHGPU_LDS_SLOTS"])
+    from mythril_amd.irdefs import check_lds_slots
+    LDS_SLOTS = check_lds_slots(os.environ["MYTHGPU_LDS_SLOTS"])
     return nreg
 _STREAM = None
 

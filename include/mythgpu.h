@@ -90,7 +90,9 @@ typedef struct mg_gen {
  *     handle and serialise the devices inside a call.
  * A mask maps onto this by calling mg_init once per set bit.  Every entry
  * point makes the context's device current (hipSetDevice) before it touches
- * device memory, so one thread may drive contexts on different devices. */
+ * device memory, so one thread may drive contexts on different devices.
+ * MYTHGPU_LDS_SLOTS (LDS spill regions per lane, default 6; 5 in the
+ * four-wave build) must be an integer 0..MG_MAX_LDS_DS, else MG_E_ARG. */
 int mg_init(int device, mg_ctx** out);
 void mg_free(mg_ctx* ctx);
 const char* mg_last_error(const mg_ctx* ctx);

@@ -31,7 +31,7 @@
 #ifndef MYTHGPU_IR_H
 #define MYTHGPU_IR_H
 
-#ifdef MG_NREG_OVERRIDE      /* A/B builds only                               */
+#ifdef MG_NREG_OVERRIDE      /* the four-wave layout (11 slots, build.LAYOUTS) */
 #define MG_NREG MG_NREG_OVERRIDE
 #else
 #define MG_NREG 16           /* VGPR slots per lane (per-limb GPR-indexed vectors) */
@@ -43,6 +43,10 @@
                                 assembly kernel keeps the first 6 in LDS
                                 (6 x 8 KiB per 256-lane block, 3 blocks per
                                 CU) and the rest in per-lane scratch         */
+#define MG_MAX_LDS_DS 8      /* LDS regions a context may use: compiled
+                                programs address every half with a DS
+                                instruction's 16-bit offset (16 halves x
+                                4 KiB); more is refused when configured     */
 #ifndef MG_MAX_PSLOTS        /* (A/B builds may override)                    */
 #define MG_MAX_PSLOTS 240    /* further spill slots in per-lane scratch      */
 #endif

@@ -352,9 +352,6 @@ def prologue(a: Asm, bank: int):
     a("s_add_u32 %s, %s, 32" % (s(S_IP), s(S_IP)))
 
 
-_PROBE = os.environ.get("MYTHGPU_PROBE", "")     # sensitivity probes (A/B builds only)
-
-
 def dispatch(a: Asm, next_bank: int):
     if JIT:
         # end of the handler's straight-line part: the dispatch's wait stays
@@ -368,14 +365,6 @@ def dispatch(a: Asm, next_bank: int):
     nb = BANK[next_bank]
     if a.lines and a.lines[-1].strip() == "s_set_gpr_idx_off":
         a.lines.pop()                  # the next handler turns it off if it must
-    if _PROBE == "salu2":
-        a("s_mov_b32 s85, s85")
-        a("s_mov_b32 s85, s85")
-    elif _PROBE == "valu2":
-        a("v_mov_b32 %s, %s" % (v(TMP), v(TMP)))
-        a("v_mov_b32 %s, %s" % (v(TMP), v(TMP)))
-    elif _PROBE == "valu4c":
-        a("v_mov_b64 %s, %s" % (vp(T[8]), vp(T[8])))
     a("s_waitcnt lgkmcnt(0)")
     a("s_add_u32 %s, %s, %s" % (s(S_JMP), s(S_BASE), s(nb + F_OFF)))
     a("s_addc_u32 %s, %s, 0" % (s(S_JMP + 1), s(S_BASE + 1)))
@@ -1087,18 +1076,8 @@ def h_out(a, bank, root, mask, dc=False, w32=False, ip=False):
 
 GOLD = 0x9E3779B97F4A7C15
 MIX1 = 0xBF58476D1CE4E5B9                         # the one 64-bit multiplier (generator v9)
-MIX2 = 0x94D049BB133111EB                         # v8's second SplitMix64 multiplier
-# A/B knob only: MYTHGPU_GEN_MIX=8 renders v8's SplitMix64 finaliser (the
-# oracle restates v9 alone, so such a build fails parity by design)
-GEN_MIX = int(os.environ.get("MYTHGPU_GEN_MIX", "9"))
 PAIR_MUL = (0x85EBCA6B, 0xC2B2AE35, 0x27D4EB2F)   # uniform limb pairs 1-3 (generator v6)
 CLS_MUL = 0x2545F491                              # class remix (generator v7/v8)
-# the wave's class in SALU when its first active index starts a 64-group
-# (A/B knob: MYTHGPU_GEN_SALU_CLASS=0 draws per lane in every wave)
-GEN_SALU_CLASS = os.environ.get("MYTHGPU_GEN_SALU_CLASS", "1") != "0"
-# compiled programs: the aligned wave's class dispatch carries no waterfall
-# state (A/B knob: MYTHGPU_GEN_JIT_FLAT=0 keeps the interpreter's layout)
-GEN_JIT_FLAT = os.environ.get("MYTHGPU_GEN_JIT_FLAT", "1") != "0"
 # mixer constants live in SGPRs s[S_K:S_K+5], set once at entry
 K_GOLD_LO, K_GOLD_HI, K_M1_LO, K_M1_HI, K_M2_LO, K_M2_HI = range(S_K, S_K + 6)
 S_GROUP = K_GOLD_LO        # compiled programs: lo32(idx >> 6) of the wave (jit.program_asm)
@@ -1108,11 +1087,9 @@ S_PAIR = S_X + 2           # s[90:92] the uniform limb-pair multipliers during a
 def load_sm64_consts(a: Asm):
     # (GOLD goes in as literals; s[96:97] hold a compiled program's wave
     # group, S_GROUP, set at the program's entry)
-    consts = [(K_M1_LO, MIX1), (K_M1_HI, MIX1 >> 32)]
-    if GEN_MIX == 8:
-        consts += [(K_M2_LO, MIX2), (K_M2_HI, MIX2 >> 32)]
-    else:                       # v9 frees s[100:101]: two uniform-limb multipliers
-        consts += [(K_M2_LO, PAIR_MUL[0]), (K_M2_HI, PAIR_MUL[1])]
+    # (v9's single multiplier frees s[100:101]: two uniform-limb multipliers)
+    consts = [(K_M1_LO, MIX1), (K_M1_HI, MIX1 >> 32),
+              (K_M2_LO, PAIR_MUL[0]), (K_M2_HI, PAIR_MUL[1])]
     for reg, val in consts:
         a("s_mov_b32 %s, 0x%x" % (s(reg), val & 0xFFFFFFFF))
 
@@ -1130,9 +1107,6 @@ def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
     Uses vcc (also as the mads' junk carry-out)."""
     a("v_add_co_u32 %s, vcc, 0x%x, %s" % (v(st[0]), GOLD & 0xFFFFFFFF, v(st[0])))
     a("v_addc_co_u32 %s, vcc, %s, %s, vcc" % (v(st[1]), v(t[3]), v(st[1])))
-    if GEN_MIX == 8:
-        _splitmix_v8(a, st, z, t)
-        return
     a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(st[0]), v(st[1])))                    # u_lo
     # z = u * MIX1 with u = (z[0], st[1]): the two cross terms' low word
     # (lo * K_hi by v_mul_lo, hi * K_lo + it by the low half of a mad), the
@@ -1144,23 +1118,6 @@ def sm64(a: Asm, st: List[int], z: List[int], t: List[int]):
     a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(z[0]), v(z[1])))                       # r0_lo
 
 
-def _splitmix_v8(a: Asm, st: List[int], z: List[int], t: List[int]):
-    """v8's SplitMix64 finaliser on st (A/B knob MYTHGPU_GEN_MIX=8 only)."""
-    def mul64(klo, khi):
-        a("v_mul_lo_u32 %s, %s, %s" % (v(t[2]), v(z[0]), s(khi)))
-        a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(t[0]), v(z[1]), s(klo), vp(t[2])))
-        a("v_mad_u64_u32 %s, vcc, %s, %s, 0" % (vp(z[0]), v(z[0]), s(klo)))
-        a("v_add_u32 %s, %s, %s" % (v(z[1]), v(z[1]), v(t[0])))
-    src = st
-    for sh, k in ((30, (K_M1_LO, K_M1_HI)), (27, (K_M2_LO, K_M2_HI)), (31, None)):
-        a("v_lshrrev_b64 %s, %d, %s" % (vp(t[0]), sh, vp(src[0])))
-        a("v_xor_b32 %s, %s, %s" % (v(z[0]), v(src[0]), v(t[0])))
-        a("v_xor_b32 %s, %s, %s" % (v(z[1]), v(src[1]), v(t[1])))
-        if k:
-            mul64(*k)
-        src = z
-
-
 def _uniform_limbs(a: Asm, dst: List[int], z: List[int], x: int):
     """The uniform class's value: r0 in limbs 0-1, limb pair k = 1..3 is
     x * C_k + r0 (mod 2^64) with x = lo ^ hi of r0 — one v_mad_u64_u32 per
@@ -1170,11 +1127,8 @@ def _uniform_limbs(a: Asm, dst: List[int], z: List[int], x: int):
         a("v_mov_b64 %s, %s" % (vp(dst[0]), vp(z[0])))
     a("v_xor_b32 %s, %s, %s" % (v(x), v(z[0]), v(z[1])))
     # v9: the first two multipliers are resident in s[100:101] (set at entry)
-    regs = [K_M2_LO, K_M2_HI, S_PAIR + 2] if GEN_MIX != 8 else [S_PAIR + k for k in range(3)]
-    for k, c in enumerate(PAIR_MUL):
-        if regs[k] >= S_K + 4 and GEN_MIX != 8:
-            continue
-        a("s_mov_b32 %s, 0x%x" % (s(regs[k]), c))
+    regs = [K_M2_LO, K_M2_HI, S_PAIR + 2]
+    a("s_mov_b32 %s, 0x%x" % (s(regs[2]), PAIR_MUL[2]))
     for k in range(3):
         a("v_mad_u64_u32 %s, vcc, %s, %s, %s" % (vp(dst[2 + 2 * k]), v(x), s(regs[k]),
                                                  vp(z[0])))
@@ -1246,7 +1200,7 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     st, z, tt = [T[0], T[1]], [dst[0], dst[1]], [T[4], T[5], T[6], T[7]]
     cls, lo = T[8], z[0]
     g = S_CUR
-    flat = GEN_SALU_CLASS and JIT and GEN_JIT_FLAT
+    flat = JIT
 
     def record_fields():
         # width and class thresholds from the LEAFD record (in a compiled
@@ -1401,19 +1355,16 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
         else:
             a.hot()
         return
-    if GEN_SALU_CLASS:
-        a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
-        a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
-        a("s_and_b32 %s, %s, 63" % (s(rest), s(sc)))
-        a("s_cbranch_scc1 %s" % lab_slow)
-        a("s_lshr_b64 %s, %s, 6" % (sp(sc), sp(sc)))
-        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T)))
-        a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
-        a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
-        a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
-        a("s_mov_b64 %s, 0" % sp(rest))             # one pass: no lanes left after it
-    else:
-        lane_class()
+    a("v_readfirstlane_b32 %s, %s" % (s(sc), OP_IDX_LO))
+    a("v_readfirstlane_b32 %s, %s" % (s(sc + 1), OP_IDX_HI))
+    a("s_and_b32 %s, %s, 63" % (s(rest), s(sc)))
+    a("s_cbranch_scc1 %s" % lab_slow)
+    a("s_lshr_b64 %s, %s, 6" % (sp(sc), sp(sc)))
+    a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T)))
+    a("s_mul_i32 %s, %s, 0x%x" % (s(sc), s(sc), CLS_MUL))
+    a("s_xor_b32 %s, %s, %s" % (s(sc), s(sc), s(S_T + 1)))
+    a("s_mul_hi_u32 %s, %s, 100" % (s(sc), s(sc)))
+    a("s_mov_b64 %s, 0" % sp(rest))                 # one pass: no lanes left after it
     a.label(lab_join)
     sm64(a, st, z, tt)
     a("s_mov_b64 %s, exec" % sp(save))
@@ -1445,10 +1396,9 @@ def _gen_leaf(a: Asm, bank: int, dst: Optional[List[int]] = None, wait: bool = T
     if wait:
         a("s_waitcnt vmcnt(0)")                      # boundary and pool loads
     a.cold()
-    if GEN_SALU_CLASS:
-        a.label(lab_slow)
-        lane_class()
-        a("s_branch %s" % lab_join)
+    a.label(lab_slow)
+    lane_class()
+    a("s_branch %s" % lab_join)
     a.label(lab_loop)
     a("v_readfirstlane_b32 %s, %s" % (s(sc), v(cls)))
     a("v_cmp_eq_u32 vcc, %s, %s" % (s(sc), v(cls)))
@@ -1468,7 +1418,7 @@ def h_leaf(a, bank, root, mask, dc=False, w32=False, ip=False):
     if mask:
         load_masks(a, fld(bank, F_MOFF))
     lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
-    if JIT and GEN_SALU_CLASS and GEN_JIT_FLAT:
+    if JIT:
         # compiled programs: the common case (generator mode, no leaf store,
         # aligned wave) behind one flag test, as in h_leafd
         def masked():
@@ -1545,7 +1495,7 @@ def h_leafd(a: Asm, bank: int, var: int):
     fd = [FB + 8 * slot + j for j in range(8)]
     prologue(a, bank)
     lab_mem, lab_done = a.uniq("lmem"), a.uniq("ldone")
-    if JIT and GEN_SALU_CLASS and GEN_JIT_FLAT:
+    if JIT:
         # compiled programs: one flag test per leaf for the common case
         # (generator mode, no leaf store); the rest in a cold copy
         lab_gen = a.uniq("lgen")
@@ -1746,34 +1696,33 @@ def h_cdwx(a, bank, root, mask, dc=False, w32=False, ip=False):
     a("v_cmp_ne_u32 vcc, 0, %s" % v(T[1]))
     a("v_cndmask_b32_e64 %s, %s, 32, vcc" % (v(T[0]), v(T[0])))
     a("v_cndmask_b32_e64 %s, %s, 0, %s" % (v(T[0]), v(T[0]), sp(S_X)))   # n
-    wrap, back, done = a.uniq("cdxw"), a.uniq("cdxb"), a.uniq("cdxd")
+    wrap, done = a.uniq("cdxw"), a.uniq("cdxd")
     a("v_cmp_eq_u32 vcc, 0x7fffffff, %s" % v(Y[7]))
     a("s_cbranch_vccnz %s" % wrap)
-    if CDWX_PREFIX:
-        # no lane wraps: the valid bytes are the first n, so limb j keeps its
-        # top min(max(n - 4(7 - j), 0), 4) bytes — with x_j = 8 * that, the
-        # low word of (0xffffffff << 32) >> x_j (x_j <= 32: a 64-bit shift)
-        a("v_cmp_gt_u32 vcc, 32, %s" % v(T[0]))                    # lanes missing a byte
-        if not ip:
-            a.read_slot(R, fld(bank, F_A))
-        a("s_cbranch_vccz %s" % done)                              # every byte valid
-        a("v_lshlrev_b32 %s, 3, %s" % (v(T[1]), v(T[0])))          # 8n
-        a("s_mov_b32 %s, 0" % s(S_T))
-        a("s_mov_b32 %s, -1" % s(S_T + 1))
-        for j in range(8):
-            k = 32 * (7 - j)
-            if k:
-                a("v_subrev_u32 %s, %d, %s" % (v(T[4]), k, v(T[1])))
-                a("v_med3_i32 %s, %s, 0, 32" % (v(T[4]), v(T[4])))
-            else:
-                a("v_min_u32 %s, 32, %s" % (v(T[4]), v(T[1])))
-            a("v_lshrrev_b64 %s, %s, %s" % (vp(T[2]), v(T[4]), sp(S_T)))
-            if ip:
-                a.idx_on(fld(bank, F_D), "SRC1,DST")
-                a("v_and_b32 %s, %s, %s" % (v(F[j]), v(T[2]), v(F[j])))
-                a.idx_off()
-            else:
-                a("v_and_b32 %s, %s, %s" % (v(R[j]), v(T[2]), v(R[j])))
+    # no lane wraps: the valid bytes are the first n, so limb j keeps its
+    # top min(max(n - 4(7 - j), 0), 4) bytes — with x_j = 8 * that, the
+    # low word of (0xffffffff << 32) >> x_j (x_j <= 32: a 64-bit shift)
+    a("v_cmp_gt_u32 vcc, 32, %s" % v(T[0]))                    # lanes missing a byte
+    if not ip:
+        a.read_slot(R, fld(bank, F_A))
+    a("s_cbranch_vccz %s" % done)                              # every byte valid
+    a("v_lshlrev_b32 %s, 3, %s" % (v(T[1]), v(T[0])))          # 8n
+    a("s_mov_b32 %s, 0" % s(S_T))
+    a("s_mov_b32 %s, -1" % s(S_T + 1))
+    for j in range(8):
+        k = 32 * (7 - j)
+        if k:
+            a("v_subrev_u32 %s, %d, %s" % (v(T[4]), k, v(T[1])))
+            a("v_med3_i32 %s, %s, 0, 32" % (v(T[4]), v(T[4])))
+        else:
+            a("v_min_u32 %s, 32, %s" % (v(T[4]), v(T[1])))
+        a("v_lshrrev_b64 %s, %s, %s" % (vp(T[2]), v(T[4]), sp(S_T)))
+        if ip:
+            a.idx_on(fld(bank, F_D), "SRC1,DST")
+            a("v_and_b32 %s, %s, %s" % (v(F[j]), v(T[2]), v(F[j])))
+            a.idx_off()
+        else:
+            a("v_and_b32 %s, %s, %s" % (v(R[j]), v(T[2]), v(R[j])))
 
     def spread_and():
         # T[2] = the 32-bit valid-byte set (bit i: byte 31 - i)
@@ -1798,10 +1747,6 @@ def h_cdwx(a, bank, root, mask, dc=False, w32=False, ip=False):
         else:
             for j in range(8):
                 a("v_and_b32 %s, %s, %s" % (v(R[j]), v(X[j]), v(R[j])))
-    if not CDWX_PREFIX:
-        _prefix(a, T[2], T[0], T[2])                               # valid bytes
-        a.label(back)
-        spread_and()
     a.label(done)
     if not ip:
         a.write_slot(R, fld(bank, F_D))
@@ -1837,11 +1782,8 @@ def h_cdwx(a, bank, root, mask, dc=False, w32=False, ip=False):
     _prefix(a, T[8], T[4], T[8])
     a("v_bfi_b32 %s, %s, 0, %s" % (v(T[6]), v(T[8]), v(T[6])))    # [K, end)
     a("v_or_b32 %s, %s, %s" % (v(T[2]), v(T[2]), v(T[6])))
-    if CDWX_PREFIX:
-        spread_and()                                               # not a prefix here
-        a("s_branch %s" % done)
-    else:
-        a("s_branch %s" % back)
+    spread_and()                                                   # not a prefix here
+    a("s_branch %s" % done)
     a.hot()
     a.flush_cold()
 
@@ -2012,25 +1954,24 @@ def body_umulno(a: Asm):
     a.read_slot(X, cur(F_A))
     a.read_slot(Y, cur(F_B))
     lab = a.uniq("unf")
-    if UMULNO_FAST:
-        # W = 256 and both operands >= 2^128 in every active lane (90 % of the
-        # C2 corpus's UMULNO waves): p + q >= 258, every product overflows —
-        # no bit lengths needed (round 5)
-        lab_gen = a.uniq("ung")
-        a("s_cmp_eq_u32 %s, 0x100" % s(cur(F_W)))
-        a("s_cbranch_scc0 %s" % lab_gen)
-        a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(X[4]), v(X[5]), v(X[6])))
-        a("v_or_b32 %s, %s, %s" % (v(T[0]), v(T[0]), v(X[7])))
-        a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(Y[4]), v(Y[5]), v(Y[6])))
-        a("v_or_b32 %s, %s, %s" % (v(T[1]), v(T[1]), v(Y[7])))
-        a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_X + 4), v(T[0])))
-        a("v_cmp_ne_u32 vcc, 0, %s" % v(T[1]))
-        a("s_and_b64 vcc, vcc, %s" % sp(S_X + 4))
-        a("s_cmp_eq_u64 vcc, exec")
-        a("s_cbranch_scc0 %s" % lab_gen)
-        a("s_mov_b64 %s, 0" % sp(S_X + 4))                 # no lane is free of overflow
-        a("s_branch %s" % lab)
-        a.label(lab_gen)
+    # W = 256 and both operands >= 2^128 in every active lane (90 % of the
+    # C2 corpus's UMULNO waves): p + q >= 258, every product overflows —
+    # no bit lengths needed (round 5)
+    lab_gen = a.uniq("ung")
+    a("s_cmp_eq_u32 %s, 0x100" % s(cur(F_W)))
+    a("s_cbranch_scc0 %s" % lab_gen)
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[0]), v(X[4]), v(X[5]), v(X[6])))
+    a("v_or_b32 %s, %s, %s" % (v(T[0]), v(T[0]), v(X[7])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(T[1]), v(Y[4]), v(Y[5]), v(Y[6])))
+    a("v_or_b32 %s, %s, %s" % (v(T[1]), v(T[1]), v(Y[7])))
+    a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_X + 4), v(T[0])))
+    a("v_cmp_ne_u32 vcc, 0, %s" % v(T[1]))
+    a("s_and_b64 vcc, vcc, %s" % sp(S_X + 4))
+    a("s_cmp_eq_u64 vcc, exec")
+    a("s_cbranch_scc0 %s" % lab_gen)
+    a("s_mov_b64 %s, 0" % sp(S_X + 4))                 # no lane is free of overflow
+    a("s_branch %s" % lab)
+    a.label(lab_gen)
     sz = T[8]                                   # clz(x) + clz(y) = 512 - (p + q)
     clz256(a, X, sz, [T[8], T[9], T[10], T[11], T[0], T[1], T[2], T[3]])
     clz256(a, Y, T[4], [T[4], T[5], T[6], T[7], T[0], T[1], T[2], T[3]])
@@ -2225,38 +2166,19 @@ def shift_core(a: Asm, kind: str, fa: int, fb: int, fw: int, masked: bool):
 # Registers: u = X, v = Y on entry; un = X ++ R ++ [T0]; vn = Y;
 # b/c = T2/T3 (b kept for the remainder); digit temps T4..T11.
 
-# dividend normalisation order (A/B knob: MYTHGPU_DIV_BITS_FIRST=0 shifts
-# limbs first, then 17 limbs of bits — the round-2 order)
-DIV_BITS_FIRST = os.environ.get("MYTHGPU_DIV_BITS_FIRST", "1") != "0"
+# Division's wave-uniform exits and paths (rounds 3-5; each was an A/B knob,
+# retired in round 6 with its losing side): the dividend is shifted by bits
+# before limbs; limb-barrel stages of DIV_STAGE_SKIP or more limbs branch over
+# an empty lane mask; a wave whose divisors all keep their top limb jumps to
+# quotient digit 0 and computes the reciprocal only if some lane needs that
+# digit; the one-limb short division's second correction sits behind a
+# branch; waves whose divisors all fit 64 bits take Moller-Granlund 3-by-2
+# steps; a wave dividing by zero everywhere skips the division.
 DIV_M = {4: 48, 2: 50, 1: 52}   # limb-shift stage masks (bank B: free in heavy bodies)
 DIV_Z6 = 54                     # lanes with vn[0..5] == 0 (bank B)
-# limb-barrel stages this long get a branch over an empty lane mask (A/B
-# knob: MYTHGPU_DIV_STAGE_SKIP=99 never branches, the round-3 code)
-DIV_STAGE_SKIP = int(os.environ.get("MYTHGPU_DIV_STAGE_SKIP", "6"))
+DIV_STAGE_SKIP = 6
 DIV_Z4 = S_CUR + F_C            # lanes with vn[0..3] == 0 (record fields c, imm:
                                 # unused by division)
-# a wave whose divisors all have their top limb set jumps straight to quotient
-# digit 0 (round 5; A/B knob: MYTHGPU_DIV_J0=0 tests every digit)
-DIV_J0_JUMP = os.environ.get("MYTHGPU_DIV_J0", "1") != "0"
-# the one-limb short division's second ("unlikely") quotient correction behind
-# a branch (round 5; A/B knob: MYTHGPU_DIV_SHORT_BRANCH=0 is the round-4 step)
-DIV_SHORT_BRANCH = os.environ.get("MYTHGPU_DIV_SHORT_BRANCH", "1") != "0"
-# waves whose every divisor fits 64 bits (and not all 32) divide by Moller-
-# Granlund 3-by-2 steps out of line (round 5; A/B knob: MYTHGPU_DIV_SHORT2=0
-# sends them down the general path)
-DIV_SHORT2 = os.environ.get("MYTHGPU_DIV_SHORT2", "1") != "0"
-# a wave whose every divisor is zero skips the division (round 5; A/B knob:
-# MYTHGPU_DIV_ZERO_EXIT=0 divides 0 by 1 in the one-limb short division)
-DIV_ZERO_EXIT = os.environ.get("MYTHGPU_DIV_ZERO_EXIT", "1") != "0"
-# with the digit-0 jump, the reciprocal after the wave's digit-0 test (round
-# 5; A/B knob: MYTHGPU_DIV_J0_LATE=0 computes it first)
-DIV_J0_LATE = os.environ.get("MYTHGPU_DIV_J0_LATE", "1") != "0"
-# bvumul_noovfl at W = 256 with both operands >= 2^128 in every lane answers
-# "overflow" without bit lengths (round 5; A/B knob: MYTHGPU_UMULNO_FAST=0)
-UMULNO_FAST = os.environ.get("MYTHGPU_UMULNO_FAST", "1") != "0"
-# the calldata word's byte mask built per limb from the valid-byte count when
-# no lane wraps (round 5; A/B knob: MYTHGPU_CDWX_PREFIX=0 spreads the byte set)
-CDWX_PREFIX = os.environ.get("MYTHGPU_CDWX_PREFIX", "1") != "0"
 
 
 def _stage(a: Asm, t: List[int], st: int, nl: int, left: bool, mask: int,
@@ -2294,55 +2216,38 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     vn = Y
     b, c, dinv = T[2], T[3], T[10]
     bz = S_T + 4
-    # every active lane's divisor fits one limb: short division, out of line
-    lab_short, lab_done = a.uniq("dsh"), a.uniq("dsd")
+    # every active lane's divisor fits two limbs: out of line, where one limb
+    # (the one-limb short division) or two (3-by-2 steps) is decided
+    lab_done = a.uniq("dsd")
     t = T[4]
-    if DIV_SHORT2:
-        # every active lane's divisor fits two limbs: out of line, where
-        # one limb (the one-limb short division) or two (3-by-2 steps) is
-        # decided
-        lab_fit64, lab_two = a.uniq("d64"), a.uniq("d2l")
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[2]), v(Y[3]), v(Y[4])))
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[5]), v(Y[6])))
-        a("v_or_b32 %s, %s, %s" % (v(t), v(t), v(Y[7])))
-        a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
-        a("s_cmp_eq_u64 vcc, exec")
-        a("s_cbranch_scc1 %s" % lab_fit64)
-        a.cold()
-        a.label(lab_fit64)
-        a("v_cmp_eq_u32 vcc, 0, %s" % v(Y[1]))
-        a("s_cmp_eq_u64 vcc, exec")
-        a("s_cbranch_scc0 %s" % lab_two)
-        if DIV_ZERO_EXIT:
-            # every active lane divides by zero (11 % of the C2 corpus's
-            # division waves): quotient and remainder 0 as the contract says,
-            # the caller applies SMT-LIB's x/0 rules
-            lab_zero = a.uniq("dz")
-            a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(Y[0])))
-            a("s_cmp_eq_u64 %s, exec" % sp(z))
-            a("s_cbranch_scc1 %s" % lab_zero)
-        _udivrem_short(a, want_rem, z)
-        a("s_branch %s" % lab_done)
-        if DIV_ZERO_EXIT:
-            a.label(lab_zero)
-            moves(a, (X if want_rem else []) + R, [None] * (16 if want_rem else 8))
-            a("s_branch %s" % lab_done)
-        a.label(lab_two)
-        _udivrem_short2(a, want_rem, z)
-        a("s_branch %s" % lab_done)
-        a.hot()
-    else:
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[1]), v(Y[2]), v(Y[3])))
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[4]), v(Y[5])))
-        a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[6]), v(Y[7])))
-        a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
-        a("s_cmp_eq_u64 vcc, exec")
-        a("s_cbranch_scc1 %s" % lab_short)
-        a.cold()
-        a.label(lab_short)
-        _udivrem_short(a, want_rem, z)
-        a("s_branch %s" % lab_done)
-        a.hot()
+    lab_fit64, lab_two = a.uniq("d64"), a.uniq("d2l")
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(Y[2]), v(Y[3]), v(Y[4])))
+    a("v_or3_b32 %s, %s, %s, %s" % (v(t), v(t), v(Y[5]), v(Y[6])))
+    a("v_or_b32 %s, %s, %s" % (v(t), v(t), v(Y[7])))
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(t))
+    a("s_cmp_eq_u64 vcc, exec")
+    a("s_cbranch_scc1 %s" % lab_fit64)
+    a.cold()
+    a.label(lab_fit64)
+    a("v_cmp_eq_u32 vcc, 0, %s" % v(Y[1]))
+    a("s_cmp_eq_u64 vcc, exec")
+    a("s_cbranch_scc0 %s" % lab_two)
+    # every active lane divides by zero (11 % of the C2 corpus's
+    # division waves): quotient and remainder 0 as the contract says,
+    # the caller applies SMT-LIB's x/0 rules
+    lab_zero = a.uniq("dz")
+    a("v_cmp_eq_u32_e64 %s, 0, %s" % (sp(z), v(Y[0])))
+    a("s_cmp_eq_u64 %s, exec" % sp(z))
+    a("s_cbranch_scc1 %s" % lab_zero)
+    _udivrem_short(a, want_rem, z)
+    a("s_branch %s" % lab_done)
+    a.label(lab_zero)
+    moves(a, (X if want_rem else []) + R, [None] * (16 if want_rem else 8))
+    a("s_branch %s" % lab_done)
+    a.label(lab_two)
+    _udivrem_short2(a, want_rem, z)
+    a("s_branch %s" % lab_done)
+    a.hot()
     for j in range(0, 8, 2):
         a("v_mov_b64 %s, 0" % vp(R[j]))
     a("v_mov_b32 %s, 0" % v(T[0]))                                       # un[16]
@@ -2367,18 +2272,12 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     lab = exec_begin(a, z, S_T)
     moves(a, X, [None] * 8)
     exec_end(a, lab, S_T)
-    if DIV_BITS_FIRST:
-        # the dividend's bits first (9 limbs: u << b, the top limb un[8] = 0
-        # on entry), then its limbs: 9 funnels instead of 17 after the barrel
-        bitshift_left(a, un, c, bz, 9, S_T)
-        live = 9
-        for st in (4, 2, 1):
-            live = _stage(a, un, st, 17, True, DIV_M[st], live)
-    else:
-        live = 8
-        for st in (4, 2, 1):
-            live = _stage(a, un, st, 16, True, DIV_M[st], live)
-        bitshift_left(a, un, c, bz, 17, S_T)
+    # the dividend's bits first (9 limbs: u << b, the top limb un[8] = 0 on
+    # entry), then its limbs: 9 funnels instead of 17 after the barrel
+    bitshift_left(a, un, c, bz, 9, S_T)
+    live = 9
+    for st in (4, 2, 1):
+        live = _stage(a, un, st, 17, True, DIV_M[st], live)
     # lanes whose normalised divisor has its low 4 / 6 digits zero: a
     # quotient digit's multiply-subtract starts at digit 4 / 6 when every
     # lane with a nonzero digit is one of them (qh * 0 changes nothing)
@@ -2395,20 +2294,14 @@ def udivrem(a: Asm, want_rem: bool, z: int):
     # divisors; zero divisors excluded, they divide 0) only digit 0 can be
     # nonzero: one scalar test instead of seven per-digit VALU tests (round 5),
     # taken before the reciprocal, which such a wave then computes only when
-    # some lane needs digit 0 (DIV_J0_LATE)
+    # some lane needs digit 0
     lab_j0, lab_rem = a.uniq("dj0"), a.uniq("drm")
-    late = DIV_J0_JUMP and DIV_J0_LATE
-    if DIV_J0_JUMP:
-        if not late:
-            _reciprocal(a, d, dinv)
-            a("v_mov_b32 %s, 0" % v(T[9]))                          # RH of the digit loop
-        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(DIV_M[4]), sp(DIV_M[2])))
-        a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(DIV_M[1])))
-        a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(z)))
-        a("s_cbranch_scc0 %s" % lab_j0)
-    if late or not DIV_J0_JUMP:
-        _reciprocal(a, d, dinv)
-        a("v_mov_b32 %s, 0" % v(T[9]))                              # RH of the digit loop
+    a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(DIV_M[4]), sp(DIV_M[2])))
+    a("s_or_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(DIV_M[1])))
+    a("s_andn2_b64 %s, %s, %s" % (sp(S_T), sp(S_T), sp(z)))
+    a("s_cbranch_scc0 %s" % lab_j0)
+    _reciprocal(a, d, dinv)
+    a("v_mov_b32 %s, 0" % v(T[9]))                                  # RH of the digit loop
 
     def digit_test(j, skip):
         a("v_cmp_ne_u32_e64 %s, 0, %s" % (sp(S_T), v(un[j + 8])))
@@ -2417,20 +2310,17 @@ def udivrem(a: Asm, want_rem: bool, z: int):
         a("s_cbranch_vccz %s" % skip)
 
     for j in reversed(range(8)):
-        if j == 0 and DIV_J0_JUMP and not late:
-            a.label(lab_j0)
         skip = a.uniq("dvs")
         digit_test(j, skip)
         _div_digit(a, un, vn, j, d, dinv)
         a.label(skip)
-    if late:
-        a("s_branch %s" % lab_rem)
-        a.label(lab_j0)
-        digit_test(0, lab_rem)
-        _reciprocal(a, d, dinv)
-        a("v_mov_b32 %s, 0" % v(T[9]))
-        _div_digit(a, un, vn, 0, d, dinv)
-        a.label(lab_rem)
+    a("s_branch %s" % lab_rem)
+    a.label(lab_j0)
+    digit_test(0, lab_rem)
+    _reciprocal(a, d, dinv)
+    a("v_mov_b32 %s, 0" % v(T[9]))
+    _div_digit(a, un, vn, 0, d, dinv)
+    a.label(lab_rem)
     if want_rem:
         # remainder = un[0..8] >> sh; un[8] now holds a quotient digit: use 0
         a("v_mov_b32 %s, 0" % v(T[0]))
@@ -2465,8 +2355,6 @@ def _udivrem_short(a: Asm, want_rem: bool, z: int):
     a("v_mov_b32 %s, 0" % v(R[0]))
     bitshift_left(a, X + [R[0]], c, bz, 9, S_T)                       # u = X << b
     _reciprocal(a, d, dinv)
-    if not DIV_SHORT_BRANCH:
-        return _udivrem_short_r4(a, want_rem, z)
     a("v_mov_b32 %s, %s" % (v(r), v(R[0])))                           # r = u[8] < d
     lt = sp(S_T + 2)
     for j in reversed(range(8)):
@@ -2594,35 +2482,6 @@ def _udivrem_short2(a: Asm, want_rem: bool, z: int):
         moves(a, [X[0], X[1]], [X[1], None])
         exec_end(a, lab, S_T)
         moves(a, X[2:], [None] * 6)
-
-
-def _udivrem_short_r4(a: Asm, want_rem: bool, z: int):
-    """The round-4 digit loop of _udivrem_short (both corrections in line,
-    14 VALU per digit), kept for the A/B knob; entered after the common
-    normalisation and reciprocal."""
-    d, b, r, dinv = Y[0], T[2], T[3], T[10]
-    A0, A1, P0, CR, QH = T[4], T[5], T[6], T[8], T[11]
-    a("v_mov_b32 %s, %s" % (v(r), v(R[0])))
-    lt = sp(S_T + 2)
-    for j in reversed(range(8)):
-        a("v_mov_b32 %s, %s" % (v(A0), v(X[j])))
-        a("v_mov_b32 %s, %s" % (v(A1), v(r)))
-        a("v_mad_u64_u32 v[%d:%d], %s, %s, %s, v[%d:%d]" % (A0, A1, sp(S_T + 6), v(dinv), v(r),
-                                                           A0, A1))
-        a("v_add_u32 %s, 1, %s" % (v(QH), v(A1)))
-        a("v_mul_lo_u32 %s, %s, %s" % (v(P0), v(QH), v(d)))
-        a("v_sub_u32 %s, %s, %s" % (v(CR), v(X[j]), v(P0)))
-        a("v_cmp_gt_u32_e64 %s, %s, %s" % (lt, v(CR), v(A0)))
-        a("v_subb_co_u32_e64 %s, %s, %s, 0, %s" % (v(QH), sp(S_T + 4), v(QH), lt))
-        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), lt))
-        a("v_add_u32 %s, %s, %s" % (v(CR), v(CR), v(P0)))
-        a("v_cmp_ge_u32_e64 %s, %s, %s" % (lt, v(CR), v(d)))
-        a("v_addc_co_u32_e64 %s, %s, %s, 0, %s" % (v(R[j]), sp(S_T + 4), v(QH), lt))
-        a("v_cndmask_b32_e64 %s, 0, %s, %s" % (v(P0), v(d), lt))
-        a("v_sub_u32 %s, %s, %s" % (v(r), v(CR), v(P0)))
-    if want_rem:
-        a("v_lshrrev_b32 %s, %s, %s" % (v(X[0]), v(b), v(r)))
-        moves(a, X[1:], [None] * 7)
 
 
 def _reciprocal(a: Asm, d: int, dinv: int):

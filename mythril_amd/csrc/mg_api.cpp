@@ -347,8 +347,15 @@ int mg_init(int device, mg_ctx** out) {
         return MG_E_HIP;
     }
     if (const char* l = getenv("MYTHGPU_LDS_SLOTS")) {
-        const long v = strtol(l, nullptr, 10);
-        if (v >= 0 && v <= MG_MAX_LDS) ctx->lds_slots = (uint32_t)v;
+        // a region count whose halves a DS offset cannot reach is refused
+        // here, not found later by the assembler
+        char* end = nullptr;
+        const long v = strtol(l, &end, 10);
+        if (end == l || *end || v < 0 || v > MG_MAX_LDS_DS) {
+            mg_free(ctx);
+            return MG_E_ARG;
+        }
+        ctx->lds_slots = (uint32_t)v;
     }
     if (query_handlers(ctx) != MG_OK) {
         mg_free(ctx);

@@ -19,6 +19,9 @@ static inline uint32_t mg_lds_halves(uint32_t n_lds) {
 static inline uint32_t mg_lds_half_offset(uint32_t h) {   /* byte offset of lane 0 */
     return h * MG_BLOCK_LANES * 16u;
 }
+/* the last dword of the last half a context can use fits a DS offset */
+static_assert((2u * MG_MAX_LDS_DS - 1u) * MG_BLOCK_LANES * 16u + 12u <= 0xFFFFu,
+              "LDS halves beyond a DS instruction's 16-bit offset");
 static inline uint32_t mg_lds_bytes(uint32_t n_lds) {
     return mg_lds_halves(n_lds) * MG_BLOCK_LANES * 16u;
 }

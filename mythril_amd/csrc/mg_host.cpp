@@ -143,11 +143,7 @@ static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, 
         if (op == MG_SPILL) {
             if (imm >= open.size()) open.resize(imm + 1, -1);
             open[imm] = (int)ivs.size();
-#ifdef MG_NO_NARROW_SPILL                   /* A/B builds: every spill eight dwords */
-            ivs.push_back({i, i, 0, false, 0, 0});
-#else
             ivs.push_back({i, i, 0, a < MG_NREG && narrow_reg[a], 0, 0});
-#endif
             owner[i] = open[imm];
             continue;
         }
@@ -163,27 +159,6 @@ static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, 
         }
         const bool writes = op != MG_NOP && op != MG_OUT && op != MG_ROOT;
         if (writes && d < MG_NREG) narrow_reg[d] = is_compare(op) || w <= 32;
-    }
-    // A/B knob (MYTHGPU_SPILL_PLACE=0): the round-4 rule — a spill slot
-    // below n_lds is one whole LDS region, the rest scratch at its own slot
-    static const bool legacy = [] {
-        const char* e = getenv("MYTHGPU_SPILL_PLACE");
-        return e && e[0] == '0';
-    }();
-    if (legacy) {
-        for (uint32_t i = 0; i < n_ins; ++i) {
-            if (owner[i] < 0) continue;
-            const Iv& v = ivs[owner[i]];
-            const uint32_t slot = code[4 * i + 2];
-            uint32_t loc = slot < n_lds ? PL_LDS | mg_lds_half_offset(2 * slot)
-                                        : (v.narrow ? PL_NARROW : 0u) | (slot - n_lds) * 32u;
-            place[i] = PL_SPILLREL | loc;
-            if (slot < n_lds) place[i] &= ~PL_NARROW;
-        }
-        place2.assign(n_ins, 0);
-        for (uint32_t i = 0; i < n_ins; ++i)
-            if (owner[i] >= 0 && code[4 * i + 2] < n_lds) place2[i] = mg_lds_half_offset(2 * code[4 * i + 2] + 1);
-        return place;
     }
     // LDS: 4-dword HALVES (half h: region h / 2, part h % 2, 4 KiB = 256
     // lanes x 16 B).  A 256-bit value takes two free halves (any two: the
@@ -440,12 +415,8 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         // ROOT, a one-dword spill — need not zero limbs 1..7 either: the DC
         // handler (limb 0 only) serves, and the slot is then marked dirty
         // (round 5; the Bool results of compares are the common case)
-        static const bool dirty_dc = [] {          // A/B knob MYTHGPU_DIRTY_DC=0: off
-            const char* e = getenv("MYTHGPU_DIRTY_DC");
-            return !(e && e[0] == '0');
-        }();
         bool dirty = false;
-        if (dirty_dc && writes && narrow && !clean[d] && d < MG_NREG) {
+        if (writes && narrow && !clean[d] && d < MG_NREG) {
             dirty = true;
             bool read = false;
             for (uint32_t q = pc + 1; q < n_ins && dirty; ++q) {

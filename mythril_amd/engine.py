@@ -165,6 +165,12 @@ class Engine:
         # an A/B build elsewhere may carry another assembly interpreter
         self.lib = load_library(lib_path, check_digest=lib_path == _LIB_PATH)
         ctx = C.c_void_p()
+        from . import irdefs
+        if "MYTHGPU_LDS_SLOTS" in os.environ:       # (mg_init refuses it too)
+            try:
+                irdefs.check_lds_slots(os.environ["MYTHGPU_LDS_SLOTS"])
+            except ValueError as e:
+                raise EngineUnavailable("MYTHGPU_LDS_SLOTS: %s" % e) from e
         rc = self.lib.mg_init(device, C.byref(ctx))
         if rc != 0:
             raise EngineUnavailable("mg_init(%d) failed with %d (no usable GPU?)" % (device, rc))

@@ -918,8 +918,9 @@ def _allocate(order: List[LNode], const_index: Dict[int, int], fused: set = froz
 
 
 _CMP_OPS = (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE)
-# wide results avoid clean registers (A/B knob: MYTHRIL_GPU_KEEP_CLEAN=0)
-KEEP_CLEAN = _os.environ.get("MYTHRIL_GPU_KEEP_CLEAN", "1") != "0"
+# wide results avoid clean registers (a round-2 A/B; the compilers' C ABI
+# keeps the flag, mythcc.h keep_clean)
+KEEP_CLEAN = True
 POOL_CAP = 128          # candidate values per leaf pool
 
 

@@ -24,6 +24,22 @@ NREG = int(os.environ.get("MYTHGPU_NREG", DEFINES["NREG"]))   # (A/B builds: asm
 TRASH = NREG - 1
 MAX_WIDTH = DEFINES["MAX_WIDTH"]
 MAX_LDS = DEFINES["MAX_LDS"]
+MAX_LDS_DS = DEFINES["MAX_LDS_DS"]
+
+
+def check_lds_slots(n) -> int:
+    """LDS spill regions a context / compiled program may use: 0 ..
+    MG_MAX_LDS_DS (compiled programs address every LDS half with a DS
+    instruction's 16-bit offset; more regions would assemble to an image
+    the assembler refuses).  Raises ValueError."""
+    try:
+        v = int(n)
+    except (TypeError, ValueError):
+        raise ValueError("LDS spill regions %r: not an integer" % (n,)) from None
+    if not 0 <= v <= MAX_LDS_DS:
+        raise ValueError("LDS spill regions %d: the DS offsets of compiled programs reach "
+                         "%d regions at most (MG_MAX_LDS_DS)" % (v, MAX_LDS_DS))
+    return v
 ROOT_FLAG = 1 << 18          # MG_ROOT_FLAG: w0 bit 18, ROOT fused into the producer
 MAX_PSLOTS = DEFINES["MAX_PSLOTS"]
 NUM_OPS = OPS["NUM_OPS"]

@@ -43,6 +43,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import asmgen as G
+from . import irdefs as I
 
 LLVM_BIN = os.environ.get("MYTHGPU_LLVM_BIN", "/opt/rocm/lib/llvm/bin")
 ARCH = os.environ.get("MYTHGPU_ARCH", "gfx950")
@@ -677,7 +678,6 @@ def specialize(lines: Sequence[str], rec: Sequence[int], tag: str):
 
 SLOTS = range(G.FB, G.FB + 8 * G.NREG)                 # v8..v135
 TEMPS = frozenset(list(range(G.XB, G.XB + 8)) + list(range(G.YB, G.TB + G.NT)))
-COALESCE = os.environ.get("MYTHGPU_JIT_COALESCE", "1") != "0"
 
 
 @functools.lru_cache(maxsize=1 << 16)
@@ -871,8 +871,6 @@ def coalesce(lines: List[str], final: bool = True) -> List[str]:
     end at labels and branches (the analysis never crosses them);
     ``final``: the record's temporaries are dead at its end (true for every
     record: handlers never pass values in temporaries)."""
-    if not COALESCE:
-        return lines
     out: List[str] = []
     seg: List[Optional[_Ins]] = []
     masked = False
@@ -1050,7 +1048,7 @@ def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6, full: boo
     word 0; LEAFD records patched with their leaf's generator parameters
     exactly as mg_load_program does), and the translator's mask count."""
     from .engine import translate_records
-    rec, n_masks = translate_records(prog, lds_slots)
+    rec, n_masks = translate_records(prog, I.check_lds_slots(lds_slots))
     rec = rec.reshape(-1, 8).copy()
     n_consts = prog.consts.shape[0]
     n_leaves = len(prog.leaves)
@@ -1127,20 +1125,19 @@ def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
         fps.append(records_fingerprint(full))
     tag = tag or entry.lstrip(".L")
     out = [entry + ":"]
-    if G.GEN_SALU_CLASS and G.GEN_JIT_FLAT:
-        # s[S_FAST] bit 0: generator mode, no leaf store and a wave whose
-        # first active index starts a group of 64 (every active lane in one
-        # group) — the one test a compiled LEAFD makes on its common path
-        # (asmgen.h_leafd); s[S_GROUP] = lo32(that index >> 6), the group
-        # the leaves' classes are drawn for
-        g = G.S_GROUP
-        out.append("    s_cmp_eq_u64 %s, 0" % G.PINNED["lout"])
-        out.append("    s_cselect_b32 s%d, %s, 0" % (G.S_FAST, G.PINNED["mode"]))
-        out.append("    v_readfirstlane_b32 s%d, %s" % (g, G.PINNED["idx_lo"]))
-        out.append("    v_readfirstlane_b32 s%d, %s" % (g + 1, G.PINNED["idx_hi"]))
-        out.append("    s_and_b32 s%d, s%d, 63" % (G.S_T, g))
-        out.append("    s_cselect_b32 s%d, 0, s%d" % (G.S_FAST, G.S_FAST))
-        out.append("    s_lshr_b64 s[%d:%d], s[%d:%d], 6" % (g, g + 1, g, g + 1))
+    # s[S_FAST] bit 0: generator mode, no leaf store and a wave whose
+    # first active index starts a group of 64 (every active lane in one
+    # group) — the one test a compiled LEAFD makes on its common path
+    # (asmgen.h_leafd); s[S_GROUP] = lo32(that index >> 6), the group
+    # the leaves' classes are drawn for
+    g = G.S_GROUP
+    out.append("    s_cmp_eq_u64 %s, 0" % G.PINNED["lout"])
+    out.append("    s_cselect_b32 s%d, %s, 0" % (G.S_FAST, G.PINNED["mode"]))
+    out.append("    v_readfirstlane_b32 s%d, %s" % (g, G.PINNED["idx_lo"]))
+    out.append("    v_readfirstlane_b32 s%d, %s" % (g + 1, G.PINNED["idx_hi"]))
+    out.append("    s_and_b32 s%d, s%d, 63" % (G.S_T, g))
+    out.append("    s_cselect_b32 s%d, 0, s%d" % (G.S_FAST, G.S_FAST))
+    out.append("    s_lshr_b64 s[%d:%d], s[%d:%d], 6" % (g, g + 1, g, g + 1))
     pending_cold: List[str] = []
     flush_no = 0
     for i, r in enumerate(recs):
@@ -1273,12 +1270,8 @@ def source_digest() -> str:
                 with open(os.path.join(d, f), "rb") as fh:
                     h.update(f.encode() + fh.read())
     from . import ir
-    knobs = {"coalesce": COALESCE, "flush": COLD_FLUSH, "asm": G.digest(),
-             "div_bits_first": G.DIV_BITS_FIRST, "div_stage_skip": G.DIV_STAGE_SKIP,
-             "gen_salu_class": G.GEN_SALU_CLASS, "gen_mix": G.GEN_MIX,
-             "gen_jit_flat": G.GEN_JIT_FLAT,
-             "probe": G._PROBE,
-             "leaf_remat": ir.LEAF_REMAT, "keep_clean": ir.KEEP_CLEAN}
+    knobs = {"flush": COLD_FLUSH, "asm": G.digest(), "nreg": G.NREG,
+             "leaf_remat": ir.LEAF_REMAT}
     h.update(repr(sorted(knobs.items())).encode())
     return h.hexdigest()[:16]
 

@@ -5,8 +5,12 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from mythril_amd import build
 from mythril_amd.engine import EXPORTS, load_library
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 HDR = os.path.join(build.ROOT, "include", "mythgpu.h")
 
@@ -87,3 +91,33 @@ def test_every_device_entry_point_sets_its_device():
     assert missing == []
     # mg_init selects the device it is given
     assert "hipSetDevice(device)" in bodies["mg_init"]
+
+
+def test_lds_regions_beyond_ds_offsets_are_refused_when_configured():
+    """MYTHGPU_LDS_SLOTS=10 used to yield compiled code the
+    assembler rejected (LDS halves past a DS instruction's 16-bit offset).
+    Such a region count is refused where it is configured — the compiled-
+    program renderer, bench.apply_layout and (header) mg_init — and the
+    largest accepted count, MG_MAX_LDS_DS, renders DS offsets that fit."""
+    import re
+    import subprocess
+    import sys
+    import bench
+    from mythril_amd import irdefs, jit
+    from mythril_amd.engine import default_leafgen
+    assert irdefs.MAX_LDS_DS == 8
+    assert irdefs.check_lds_slots("8") == 8 and irdefs.check_lds_slots(0) == 0
+    for bad in (9, 10, -1, "x", None):
+        with pytest.raises(ValueError):
+            irdefs.check_lds_slots(bad)
+    _, prog, _, _ = bench.compile_unit(("c3", 16))           # a spill-heavy unit
+    with pytest.raises(ValueError, match="MG_MAX_LDS_DS"):
+        jit.program_asm(prog, default_leafgen(prog), 16, ".Ljp0", 10)
+    text = "\n".join(jit.program_asm(prog, default_leafgen(prog), 16, ".Ljp0", 8))
+    offs = [int(m) for m in re.findall(r"\bds_\w+ .*offset:(\d+)", text)]
+    assert offs and max(offs) <= 0xFFFF
+    env = dict(os.environ, MYTHGPU_LDS_SLOTS="10")
+    env.pop("MYTHGPU_NREG", None)
+    r = subprocess.run([sys.executable, "-c", "import bench; bench.apply_layout('c3')"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "MG_MAX_LDS_DS" in r.stderr

@@ -196,7 +196,7 @@ def test_division_by_zero_waves(w):
 @pytest.mark.parametrize("mode", ["all_large", "one_small", "w160"])
 def test_umulno_overflow_waves(mode):
     """bvumul_noovfl: a W = 256 wave whose operands are all >= 2^128 answers
-    "overflow" without bit lengths (asmgen.UMULNO_FAST); a lane with a small
+    "overflow" without bit lengths (asmgen.h_umulno's wave exit); a lane with a small
     operand, or a narrower width, takes the bit-length path."""
     w = 160 if mode == "w160" else 256
     x, y = N.bv_var("x", w), N.bv_var("y", w)
