@@ -84,7 +84,7 @@ args = Args()
 time_handler = TimeHandler()
 
 
-PHASES = ("flatten", "compile", "load", "search", "verify")
+PHASES = ("flatten", "refute", "compile", "load", "search", "verify")
 
 
 class SolverStatistics:
@@ -116,14 +116,17 @@ class SolverStatistics:
         self.rejected = 0
         self.ground_true = 0            # groups folded to true: answered without a launch
         self.ground_false = 0           # queries with a group folded to false: not searched
+        self.refuted = 0                # queries refuted on the host (refute.py): not compiled
         self.phase = {k: 0.0 for k in PHASES}
 
     def gpu_report(self) -> str:
         return ("GPU pre-filter: queries: {} hits: {} fallbacks: {} unsupported: {} errors: {} "
-                "rejected by z3: {} memo misses: {} compile-gated: {} shape-skipped: {}\n"
+                "rejected by z3: {} memo misses: {} compile-gated: {} shape-skipped: {} "
+                "refuted: {}\n"
                 "GPU candidates: {} time: {:.3f}s (kernel {:.3f}s; {})").format(
             self.gpu_queries, self.gpu_hits, self.fallbacks, self.unsupported, self.errors,
-            self.rejected, self.memo_misses, self.gated, self.shape_skipped, self.gpu_candidates,
+            self.rejected, self.memo_misses, self.gated, self.shape_skipped, self.refuted,
+            self.gpu_candidates,
             self.gpu_time,
             self.kernel_time, ", ".join("%s %.3fs" % (k, self.phase[k]) for k in PHASES))
 
@@ -177,6 +180,7 @@ GPU_ENABLED = True
 # shape with a hit rate below SHAPE_FLOOR, only every SHAPE_PROBE-th query of
 # that shape is searched
 SHAPE_GATE = True
+REFUTE = True              # host refutation before compiling (refute.py)
 SHAPE_MIN, SHAPE_FLOOR, SHAPE_PROBE = 4, 1.0 / 16, 8
 
 
@@ -186,8 +190,9 @@ def configure_from_env(env=None) -> None:
     ``MYTHRIL_GPU_DEVICES=0,1,...`` the devices batched searches use,
     ``MYTHRIL_GPU_CANDIDATES`` the candidates per query (a power of two),
     ``MYTHRIL_GPU_BUDGET_MS`` the share of a query's timeout the search may
-    take, ``MYTHRIL_GPU_ADAPTIVE=0`` turns the per-shape gate off."""
-    global GPU_ENABLED, DEVICES, SEARCH_CANDIDATES, SEARCH_BUDGET_MS, SHAPE_GATE
+    take, ``MYTHRIL_GPU_ADAPTIVE=0`` turns the per-shape gate off,
+    ``MYTHRIL_GPU_REFUTE=0`` the host refutation (refute.py)."""
+    global GPU_ENABLED, DEVICES, SEARCH_CANDIDATES, SEARCH_BUDGET_MS, SHAPE_GATE, REFUTE
     import os
     env = os.environ if env is None else env
     GPU_ENABLED = env.get("MYTHRIL_GPU", "1").strip().lower() not in ("0", "off", "false", "no")
@@ -201,6 +206,7 @@ def configure_from_env(env=None) -> None:
         SEARCH_BUDGET_MS = max(0.0, float(env["MYTHRIL_GPU_BUDGET_MS"]))
     SHAPE_GATE = env.get("MYTHRIL_GPU_ADAPTIVE", "1").strip().lower() not in ("0", "off", "false",
                                                                              "no")
+    REFUTE = env.get("MYTHRIL_GPU_REFUTE", "1").strip().lower() not in ("0", "off", "false", "no")
 
 
 configure_from_env()
@@ -720,6 +726,19 @@ def _compile_estimate_ms(buckets, sizes) -> float:
     return n * (COMPILE_MS_PER_NODE_PY if ir.COMPILER == "py" else COMPILE_MS_PER_NODE)
 
 
+def _refuted_group(buckets, keys) -> Optional[frozenset]:
+    """Key of the first group the host refutes (refute.refuted), or None.
+    One-constraint groups are skipped: the compiler folds a ground one, and
+    a single atom has no partner to contradict."""
+    if not REFUTE:
+        return None
+    from .refute import refuted
+    for b, k in zip(buckets, keys):
+        if len(b) > 1 and refuted(b):
+            return k
+    return None
+
+
 def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     """(assignment, programs) of a satisfying candidate, or None.  Queries
     that split into independent groups (dependence_buckets) search every
@@ -733,6 +752,15 @@ def gpu_search(nodes: Sequence[N.Node], budget_ms: float):
     keys = [_group_key(b) for b in buckets]
     if any(_known_miss(k, SEARCH_CANDIDATES) for k in keys):
         stats.memo_misses += 1
+        return None
+    # a group whose atoms contradict each other (refute.py: SafeMath's
+    # require against the module's check on the same terms) is not compiled
+    # or searched; z3 still decides the query, so UNSAT stays z3's
+    with _Phase("refute"):
+        dead = _refuted_group(buckets, keys)
+    if dead is not None:
+        stats.refuted += 1
+        _note_miss(dead, GROUND_MISS)
         return None
     shape = query_shape(nodes[-1]) if nodes else ""
     if not _shape_gate(shape):
@@ -1011,8 +1039,18 @@ def batch_is_possible(constraint_sets, enforce_execution_time=True) -> List[bool
             try:
                 with _Phase("flatten"):
                     nodes = _raw_nodes([c for c in cs if type(c) != bool])
+                buckets = dependence_buckets(nodes)
+                with _Phase("refute"):
+                    dead = _refuted_group(buckets, [_group_key(b) for b in buckets])
+                if dead is not None:
+                    # refuted on the host: get_model below sends it to z3
+                    # without a search (the memo answers it)
+                    stats.refuted += 1
+                    _note_miss(dead, GROUND_MISS)
+                    _remember(_gpu_missed, cs, True)
+                    continue
                 with _Phase("compile"):
-                    progs = [_compile_search(b) for b in dependence_buckets(nodes)]
+                    progs = [_compile_search(b) for b in buckets]
             except Unsupported as e:
                 stats.unsupported += 1
                 log.debug("GPU pre-filter: unsupported (%s)", e)

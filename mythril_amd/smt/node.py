@@ -85,6 +85,13 @@ def mk(op: str, sort: str, width: int, args: Tuple[Node, ...] = (), params: tupl
     return n
 
 
+def find(op: str, sort: str, width: int, args: Tuple[Node, ...] = (), params: tuple = (),
+         dom: int = 0):
+    """The node of this structure if it exists, else None (never creates
+    one: mythril_amd/refute.py looks up terms other atoms may share)."""
+    return _table.get((op, sort, width, dom, tuple(a.id for a in args), params))
+
+
 @contextlib.contextmanager
 def fresh_scope():
     """Build inside an empty hash-consing table (the previous one is restored
