@@ -39,37 +39,31 @@ sys.path.insert(0, ROOT)
 SEED = 0x6D797468
 # stand-in query streams (mythril_amd/workloads.py): distinct queries per step
 STREAM_QUERIES = 256
-# LDS spill tier of the context (mg_api.cpp reads the same variable): the
-# compiled programs are translated for it (apply_layout sets it per layout)
-LDS_SLOTS = int(os.environ.get("MYTHGPU_LDS_SLOTS", "6"))
-# Register layout per workload (profiles/r05/nreg/): the C2
-# corpus barely spills and runs 3.7 % faster with a fourth wave per SIMD in
-# an 11-slot register file (libmythgpu_w4.so); the query streams spill more
-# at 11 slots and lose 11 %, so they keep the 16-slot, three-wave default.
-# An explicit MYTHGPU_NREG wins.
-WORKLOAD_NREG = {"c2": 11}
+# LDS spill regions of the batch's context: its register layout's
+# (engine.lds_slots_for; MYTHGPU_LDS_SLOTS overrides), set in main() once the
+# layout is chosen — the compiled programs are translated for the same
+LDS_SLOTS = 6
 
 
-def apply_layout(workload) -> int:
-    """Set this process's register layout for ``workload`` — MYTHGPU_NREG
-    and the LDS regions that fit it (build.LAYOUT_LDS_SLOTS) — before
-    anything imports the compiler or the engine; returns the slot count."""
-    global LDS_SLOTS
-    from mythril_amd.build import LAYOUT_LDS_SLOTS
-    if "MYTHGPU_NREG" not in os.environ and workload in WORKLOAD_NREG:
-        if "mythril_amd.irdefs" in sys.modules:
-            raise RuntimeError("register layout chosen after mythril_amd.irdefs was imported")
-        os.environ["MYTHGPU_NREG"] = str(WORKLOAD_NREG[workload])
-    nreg = int(os.environ.get("MYTHGPU_NREG", "16"))
-    if nreg not in LAYOUT_LDS_SLOTS:
-        # an A/B build of another layout names its library and LDS regions
-        if not (os.environ.get("MYTHGPU_LIB") and os.environ.get("MYTHGPU_LDS_SLOTS")):
-            raise RuntimeError("no library for a %d-slot register layout" % nreg)
-    else:
-        os.environ.setdefault("MYTHGPU_LDS_SLOTS", str(LAYOUT_LDS_SLOTS[nreg]))
-    from mythril_amd.irdefs import check_lds_slots
-    LDS_SLOTS = check_lds_slots(os.environ["MYTHGPU_LDS_SLOTS"])
-    return nreg
+def explicit_layout():
+    """MYTHGPU_NREG, when set: a fixed register layout for every batch of the
+    process (A/B runs, the 11-slot parity suite); else None (per-batch rule)."""
+    v = os.environ.get("MYTHGPU_NREG")
+    return int(v) if v else None
+
+
+def choose_layout(corpus16, workers, dag_ids, workload, start="fork"):
+    """(register slots, corpus compiled for them): the per-batch rule of
+    mythril_amd/layout.py over the 16-slot programs (the C2 corpus, whose
+    programs barely spill, runs the four-wave layout; the query streams stay
+    on 16 slots), recompiled when it picks the four-wave layout."""
+    from mythril_amd import layout
+    nreg = explicit_layout() or layout.choose([p for _, p, _, _ in corpus16])
+    if nreg == 16 and explicit_layout() is None:
+        return nreg, corpus16
+    return nreg, build_corpus(len(corpus16), workers, dag_ids, workload, start, nreg=nreg)
+
+
 _STREAM = None
 
 
@@ -107,22 +101,27 @@ BENCH_REMAT = os.environ.get("MYTHRIL_GPU_LEAF_REMAT", "auto")
 
 
 def compile_unit(item):
-    """(workload, dag_id) -> (dag_id, Program, node count, int32-op weight)."""
+    """(workload, dag_id[, nreg]) -> (dag_id, Program, node count, int32-op
+    weight), compiled for ``nreg`` register slots (default: the process's
+    layout, irdefs.NREG)."""
+    from mythril_amd import irdefs
     from mythril_amd.ir import compile_constraints
     from mythril_amd.roofline import dag_work
-    workload, dag_id = item
+    workload, dag_id = item[:2]
+    nreg = item[2] if len(item) > 2 else irdefs.NREG
     roots = workload_roots(workload, dag_id)
-    prog = compile_constraints(roots, leaf_remat=BENCH_REMAT)
+    prog = compile_constraints(roots, leaf_remat=BENCH_REMAT, nreg=nreg)
     nodes, weight = dag_work(roots, prog.table_sizes)
     return dag_id, prog, nodes, weight
 
 
-def build_corpus(n_dags, workers, dag_ids=None, workload="c2", start="fork"):
+def build_corpus(n_dags, workers, dag_ids=None, workload="c2", start="fork", nreg=None):
     """Compile the step's DAGs on ``workers`` host processes (fork before
     any GPU initialisation; ``start="spawn"`` from a process that already
-    uses the GPU)."""
+    uses the GPU) for ``nreg`` register slots (default: the process's)."""
+    from mythril_amd import irdefs
     ids = list(range(n_dags)) if dag_ids is None else list(dag_ids)
-    items = [(workload, d) for d in ids]
+    items = [(workload, d, irdefs.NREG if nreg is None else nreg) for d in ids]
     from mythril_amd.procmap import process_map
     return sorted(process_map(compile_unit, items, workers, start, chunksize=16),
                   key=lambda t: t[0])
@@ -139,7 +138,7 @@ def programs_digest(corpus) -> str:
     return h.hexdigest()[:16]
 
 
-def kernel_key(lib_digest, workload, dags, assign_log2, jit, corpus=None):
+def kernel_key(lib_digest, workload, dags, assign_log2, jit, corpus=None, nreg=None):
     """What a traffic measurement (profiles/traffic.json) is valid for: the
     generated assembly, the allocator's leaf policy, the code path (and for
     compiled programs the digest of the sources that specialise them), the
@@ -148,6 +147,8 @@ def kernel_key(lib_digest, workload, dags, assign_log2, jit, corpus=None):
     from mythril_amd import ir
     key = {"asm_digest": lib_digest, "leaf_remat": BENCH_REMAT, "jit": bool(jit),
            "workload": workload, "dags": dags, "assign_log2": assign_log2}
+    if nreg is not None:
+        key["nreg"] = nreg
     if corpus is not None:
         key["programs"] = programs_digest(corpus)
     if jit:                           # the compiled programs' own code
@@ -166,9 +167,8 @@ def node_image(workload, corpus, workers, world):
     import tempfile
     from mythril_amd import jit
     ids = [d for d, _, _, _ in corpus]
-    from mythril_amd import irdefs
     key = "%s_%d_%d_%d_%d_lds%d_r%d" % (workload, len(ids), ids[0], ids[-1], sum(ids), LDS_SLOTS,
-                                        irdefs.NREG)
+                                        corpus[0][1].nreg)
     cache = os.environ.get("MYTHGPU_JIT_CACHE") or (
         os.path.join(tempfile.gettempdir(), "mythgpu_jit_%d" % os.getuid()) if world > 1 else None)
     nw = max(workers, min(os.cpu_count() or 1, 64)) if world > 1 else workers
@@ -332,10 +332,11 @@ def cpu_baseline(corpus, budget_s=20.0, workload="c2", check=None):
     return base, sc
 
 
-def waves_per_simd() -> int:
+def waves_per_simd(nreg: int) -> int:
     """Waves per SIMD the layout's VGPR budget allows (512 per lane)."""
     from mythril_amd import asmgen
-    return 512 // asmgen.NVGPR_KERNEL
+    with asmgen.layout(nreg):
+        return 512 // asmgen.NVGPR_KERNEL
 
 
 def engine_lib_path() -> str:
@@ -371,7 +372,6 @@ def main():
     args.jit = not args.interp
     if args.dags is None:
         args.dags = default_units(args.workload)
-    nreg = apply_layout(args.workload)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -384,8 +384,22 @@ def main():
     workers = int(os.environ.get("MYTHGPU_BENCH_WORKERS", "0")) or \
         max(1, min(16, ncpu // max(1, world)))
     t0 = time.time()
-    corpus = build_corpus(args.dags, workers, my_dags(args.shard, args.dags, rank, world, args.workload),
-                          args.workload)
+    mine = my_dags(args.shard, args.dags, rank, world, args.workload)
+    corpus16 = build_corpus(args.dags, workers, mine, args.workload, nreg=16)
+    # the batch's register layout (mythril_amd/layout.py): chosen from the
+    # 16-slot programs, recompiled for it when it is the four-wave one
+    nreg, corpus = choose_layout(corpus16, workers, mine, args.workload)
+    from mythril_amd import layout as LAY
+    layout_rule = {"nreg": nreg, "rule": "four waves when the 16-slot programs hold <= %.1f "
+                   "scratch spill slots each on average (mythril_amd/layout.py)"
+                   % LAY.W4_MAX_SCRATCH_SLOTS,
+                   "mean_scratch_slots_16": round(LAY.mean_scratch_slots(
+                       [p for _, p, _, _ in corpus16]), 3),
+                   "explicit": explicit_layout() is not None}
+    del corpus16
+    global LDS_SLOTS
+    from mythril_amd.engine import lds_slots_for
+    LDS_SLOTS = lds_slots_for(nreg)
     t_compile = time.time() - t0
     image, t_jit, jit_cached = None, 0.0, False
     if args.jit:                      # code generation + assembly, still before the GPU
@@ -409,7 +423,7 @@ def main():
     image_digest = None
     if image is not None:                     # assignment axis: every rank runs the same code
         image_digest = same_image(image, world if args.shard == "assign" else 1, "cuda")
-    eng = Engine(local)
+    eng = Engine(local, nreg=nreg)
     loaded = [eng.load(p, default_leafgen(p), prog_seed=d) for d, p, _, _ in corpus]
     if image is not None:
         jit_handle = eng.jit_attach(loaded, image)     # noqa: F841 (kept attached)
@@ -456,8 +470,8 @@ def main():
         evals = nodes_all * n_assign * args.steps
         ops_launch = weight_per_lane * n_assign
         achieved = ops_launch / (kern_ms / 1000.0)
-        key = kernel_key(eng.lib.mg_asm_digest().decode(), args.workload, args.dags,
-                         args.assign_log2, args.jit, corpus)
+        key = kernel_key(eng.lib.mg_asm_digest_layout(nreg).decode(), args.workload, args.dags,
+                         args.assign_log2, args.jit, corpus, nreg)
         traffic, traffic_note, sq = None, "no profiles/traffic.json", None
         if os.path.exists(args.traffic_json):
             try:
@@ -509,7 +523,8 @@ def main():
                        "assignments_per_gpu": n_assign, "nodes_total": int(nodes_all),
                        "shard": args.shard, "parallelism": "dp%d" % world,
                        "register_layout": "%d slots, %d waves/SIMD, %d LDS regions"
-                                          % (nreg, waves_per_simd(), LDS_SLOTS)},
+                                          % (nreg, waves_per_simd(nreg), LDS_SLOTS),
+                       "layout_rule": layout_rule},
             "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": VALU_PEAK_OPS / 1e12,
                          "unit": "Tops/s (int32 VALU)", "frac": achieved / VALU_PEAK_OPS,
                          "traffic": traffic, "traffic_note": traffic_note, "kernel_ms": kern_ms,

@@ -91,9 +91,22 @@ typedef struct mg_gen {
  * A mask maps onto this by calling mg_init once per set bit.  Every entry
  * point makes the context's device current (hipSetDevice) before it touches
  * device memory, so one thread may drive contexts on different devices.
- * MYTHGPU_LDS_SLOTS (LDS spill regions per lane, default 6; 5 in the
- * four-wave build) must be an integer 0..MG_MAX_LDS_DS, else MG_E_ARG. */
+ * MYTHGPU_LDS_SLOTS (LDS spill regions per lane; default: the layout's,
+ * mg_layouts) must be an integer 0..MG_MAX_LDS_DS, else MG_E_ARG.
+ *
+ * Register layouts: the library holds one assembly
+ * interpreter per layout — 16 slots at three waves per SIMD and 11 slots
+ * (MG_NREG_W4) in 128 VGPRs at four — and a context runs ONE of them:
+ * mg_init_layout(device, nreg) picks it (mg_init = the 16-slot layout).
+ * Programs loaded into a context must be compiled for its slot count
+ * (mg_load_program refuses a slot index >= nreg), so a caller chooses the
+ * layout per batch by choosing the context it loads the batch into. */
 int mg_init(int device, mg_ctx** out);
+int mg_init_layout(int device, uint32_t nreg, mg_ctx** out);
+/* The layouts this library holds (no GPU needed): out[3i..3i+2] = (slots,
+ * waves per SIMD, default LDS spill regions) of layout i, for as many as n
+ * words hold; returns the number of layouts. */
+int mg_layouts(uint32_t* out, uint32_t n);
 void mg_free(mg_ctx* ctx);
 const char* mg_last_error(const mg_ctx* ctx);
 /* Device time (ms, HIP events on the context stream) of the last synchronous
@@ -205,24 +218,25 @@ int mg_runtime_info(int* hip_version, char* path, size_t path_len);
 /* Library/ABI version (no GPU needed). */
 int mg_version(void);
 /* Digest of the generated gfx950 assembly the library was built from (no
- * GPU needed; mythril_amd/asmgen.py digest()). */
+ * GPU needed; mythril_amd/asmgen.py digest()): of the 16-slot interpreter,
+ * and of the interpreter of any layout (NULL for a slot count it lacks). */
 const char* mg_asm_digest(void);
-/* Host-only (no GPU): translate a validated IR program into the 8-word
- * records of the assembly interpreter, given its handler offset table
- * (mg_load_program does this with the table queried from the device).
+const char* mg_asm_digest_layout(uint32_t nreg);
+/* Host-only (no GPU): translate a validated IR program compiled for the
+ * nreg-slot layout into the 8-word records of that layout's assembly
+ * interpreter, given its handler offset table (mg_load_program does this
+ * with the table queried from the device).
  *   records: up to (2 * n_ins + 3) x 8 words (a WAITVM record may precede
  *   an instruction); masks: mask entries appended after the
  *   program's n_consts constants (8 words each).  Sizes are returned in
  *   *n_record_words / *n_mask_words; MG_E_ARG when a buffer is too small. */
 int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32_t n_lds,
-                 const uint32_t* handler_off, uint32_t n_handlers, uint32_t* records,
-                 uint32_t max_record_words, uint32_t* n_record_words, uint32_t* masks,
-                 uint32_t max_mask_words, uint32_t* n_mask_words);
-/* Build configuration (no GPU needed): out[0..3] = version, MG_NREG,
- * MG_MAX_LDS, MG_MAX_PSLOTS — programs must be compiled for these.  Two
- * builds export this same ABI: libmythgpu.so (16 register slots, three
- * waves per SIMD) and libmythgpu_w4.so (11 slots, four waves);
- * a caller compiles for the MG_NREG of the library it loaded. */
+                 uint32_t nreg, const uint32_t* handler_off, uint32_t n_handlers,
+                 uint32_t* records, uint32_t max_record_words, uint32_t* n_record_words,
+                 uint32_t* masks, uint32_t max_mask_words, uint32_t* n_mask_words);
+/* Build configuration (no GPU needed): out[0..3] = version, MG_NREG (the
+ * most slots any layout has; mg_layouts lists them), MG_MAX_LDS,
+ * MG_MAX_PSLOTS. */
 int mg_config(uint32_t* out, uint32_t n);
 
 #ifdef __cplusplus

@@ -17,8 +17,9 @@
  *   w1 = dst | a << 8 | b << 16 | c << 24 (register slots)
  *   w2 = imm0, w3 = imm1                 (per-op immediates, below)
  *
- * Register slots 0..MG_NREG-2 live in VGPRs (per-limb GPR-indexed vectors);
- * slot MG_TRASH receives results nobody reads.  Values that do not fit are
+ * Register slots 0..nreg-1 of the context's register layout (16 slots:
+ * MG_NREG, or 11: MG_NREG_W4; mg_layouts) live in VGPRs (per-limb
+ * GPR-indexed vectors); slot nreg-1 also receives results nobody reads.  Values that do not fit are
  * spilled with SPILL/RELOAD: the first n_lds spill slots live in LDS, the
  * rest in per-lane scratch.  Every instruction writes `dst`.  The code array
  * is followed by 8 NOPs so the interpreter can prefetch ahead.
@@ -31,12 +32,13 @@
 #ifndef MYTHGPU_IR_H
 #define MYTHGPU_IR_H
 
-#ifdef MG_NREG_OVERRIDE      /* the four-wave layout (11 slots, build.LAYOUTS) */
-#define MG_NREG MG_NREG_OVERRIDE
-#else
-#define MG_NREG 16           /* VGPR slots per lane (per-limb GPR-indexed vectors) */
-#endif
-#define MG_TRASH (MG_NREG - 1) /* result sink                                 */
+#define MG_NREG 16           /* VGPR slots per lane (per-limb GPR-indexed
+                                vectors) of the default register layout, and
+                                the most any layout has: a context of the
+                                four-wave layout holds MG_NREG_W4 (mg_layouts)
+                                and its programs use slots 0..MG_NREG_W4-1   */
+#define MG_NREG_W4 11        /* the four-wave layout (128 VGPRs)             */
+#define MG_TRASH (MG_NREG - 1) /* result sink of the default layout           */
 #define MG_LIMBS 8           /* 8 x 32-bit limbs = 256 bits                   */
 #define MG_MAX_WIDTH 256
 #define MG_MAX_LDS 10        /* LDS spill slots addressable by the IR; the

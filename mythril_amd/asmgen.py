@@ -38,8 +38,9 @@ import os
 import re
 from typing import Dict, List, Optional
 
-# register-file slots (MG_NREG); A/B knob MYTHGPU_NREG (a library built with
-# MG_NREG_OVERRIDE to match: fewer slots, fewer VGPRs, more waves per SIMD)
+# register-file slots of the layout being generated (MG_NREG = 16, or 11:
+# the four-wave layout; ``layout()`` switches, the library holds both);
+# MYTHGPU_NREG sets the process's default layout
 NREG = int(os.environ.get("MYTHGPU_NREG", "16"))
 FB = 8                     # first VGPR of the file
 XB = 0                     # X temps v0..v7   (guard below the file)
@@ -217,6 +218,53 @@ PINNED = {"root": v(NVGPR_FIXED), "idx_lo": v(NVGPR_FIXED + 1), "idx_hi": v(NVGP
           "stride": "s[24:25]", "lout": "s[26:27]", "probes": "s[28:29]", "mode": "s30",
           "scr": "s31", "active": "s[32:33]", "table": "s[34:35]"}
 NVGPR_KERNEL = NVGPR_FIXED + 4   # the kernel's VGPR budget (168: 3 waves / SIMD)
+
+
+# Layout switching: every name below derives from NREG; functions read them
+# as module globals at call time, so rebinding them switches what generate(),
+# digest(), canonical() and the compiled-program renderer (jit.py, which
+# registers a hook for its own derived tables and caches) produce.
+_layout_hooks = []
+
+
+def _set_layout(nreg: int) -> None:
+    global NREG, YB, RB, TB, NVGPR_FIXED, Y, R, T, TMP, PINNED, NVGPR_KERNEL
+    NREG = nreg
+    YB = FB + 8 * NREG
+    RB = YB + 8
+    TB = RB + 8
+    NVGPR_FIXED = TB + NT
+    Y = [YB + j for j in range(8)]
+    R = [RB + j for j in range(8)]
+    T = [TB + j for j in range(NT)]
+    TMP = T[11]
+    PINNED = dict(PINNED, root=v(NVGPR_FIXED), idx_lo=v(NVGPR_FIXED + 1),
+                  idx_hi=v(NVGPR_FIXED + 2), lds=v(NVGPR_FIXED + 3))
+    NVGPR_KERNEL = NVGPR_FIXED + 4
+    for hook in _layout_hooks:
+        hook()
+
+
+class layout:
+    """``with asmgen.layout(11): ...`` generates for the 11-slot layout and
+    restores the previous one on exit (not thread-safe: renderers switch it
+    in one thread, worker processes have their own)."""
+
+    def __init__(self, nreg: int):
+        if nreg not in (16, 11):
+            raise ValueError("no %d-slot register layout (16, 11)" % nreg)
+        self.nreg = nreg
+
+    def __enter__(self):
+        self.prev = NREG
+        if self.nreg != NREG:
+            _set_layout(self.nreg)
+        return self
+
+    def __exit__(self, *exc):
+        if NREG != self.prev:
+            _set_layout(self.prev)
+        return False
 # mg_pdesc byte offsets the assembly reads (mg_device.h)
 PDESC_CONSTS, PDESC_XCODE, PDESC_BTAB, PDESC_JIT = 0x8, 0x30, 0x38, 0x40
 

@@ -1,5 +1,7 @@
-"""Build libmythgpu.so in-tree (hipcc, gfx950).  The .so travels to the GPU
-box with the repo snapshot; nothing is JIT-compiled at run time."""
+"""Build libmythgpu.so in-tree (hipcc, gfx950): the interpreter of every
+register layout, the Keccak kernel and the host code in one library.  The
+.so travels to the GPU box with the repo snapshot; nothing is JIT-compiled at
+run time."""
 
 import os
 import subprocess
@@ -37,26 +39,32 @@ def up_to_date() -> bool:
 # of structurizer "Flow" blocks on every join (fewer SALU per instruction).
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mllvm", "-structurizecfg-skip-uniform-regions=true"]
 
+# Register layouts (mg_layouts in mg_host.cpp): slots ->
+# (waves per SIMD, default LDS spill regions).  ONE library holds the
+# interpreter of each: mg_interp_asm.hip is compiled once per layout, the
+# 16-slot body from the tracked generated sources, the others from a private
+# copy of csrc/ that asmgen fills for their slot count; a context runs one
+# layout (mg_init_layout), chosen per batch (mythril_amd/layout.py).
+LAYOUTS = {16: (3, 6), 11: (4, 5)}
+LAYOUT_LDS_SLOTS = {n: lds for n, (_, lds) in LAYOUTS.items()}
 
-def _compile(csrc: str, out: str, defines=(), flags=None, verbose: bool = False) -> str:
-    objs = []
-    for src in SOURCES:
-        obj = out + "." + src + ".o"
-        cmd = [HIPCC, "--offload-arch=" + ARCH] + (HIP_FLAGS if flags is None else flags) + \
-              ["-D" + d for d in defines] + [
-               "-I" + os.path.join(ROOT, "include"), "-I" + csrc, "-c",
-               os.path.join(csrc, src), "-o", obj]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
-        objs.append(obj)
-    tmp = out + ".tmp"
-    subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs,
-                   check=True)
-    os.replace(tmp, out)
-    for o in objs:
-        os.remove(o)
-    return out
+
+def _hipcc(csrc: str, src: str, obj: str, defines=(), flags=None, verbose: bool = False):
+    cmd = [HIPCC, "--offload-arch=" + ARCH] + (HIP_FLAGS if flags is None else flags) + \
+          ["-D" + d for d in defines] + [
+           "-I" + csrc, "-I" + os.path.join(ROOT, "include"), "-c", os.path.join(csrc, src),
+           "-o", obj]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return obj
+
+
+def _generate(nreg: int, dst: str) -> None:
+    """asmgen's outputs for a ``nreg``-slot layout into ``dst``."""
+    from mythril_amd import asmgen
+    with asmgen.layout(nreg):
+        asmgen.write_outputs(dst)
 
 
 def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=(),
@@ -64,64 +72,31 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB, defines=()
     if not force and out == LIB and up_to_date():
         return LIB
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    # the assembly interpreter's body and handler numbering are generated —
-    # for the default 16-slot layout whatever this process's MYTHGPU_NREG
-    # (an 11-slot generator would overwrite the tracked sources
-    # and pair 11-slot handlers with the C code's 16 slots)
-    _generate(16, CSRC)
-    _compile(CSRC, out, defines, flags, verbose)
-    if out == LIB:
-        build_jit_stub()
-    return out
-
-
-# Register layouts: 16 slots at three waves per SIMD (the
-# default library) and 11 slots at four (128 VGPRs, five LDS regions of
-# 40 KiB per block).  A layout other than 16 is generated under
-# MYTHGPU_NREG into a private copy of csrc/, so the tracked generated files
-# stay the default's.
-LIB_W4 = os.path.join(LIBDIR, "libmythgpu_w4.so")
-LAYOUTS = {16: (LIB, ()),
-           11: (LIB_W4, ("MG_NREG_OVERRIDE=11", "MG_ASM_WAVES_PER_SIMD=4",
-                         "MG_LDS_SLOTS_DEFAULT=5"))}
-LAYOUT_LDS_SLOTS = {16: 6, 11: 5}
-
-
-def lib_for_layout(nreg: int) -> str:
-    if nreg not in LAYOUTS:
-        raise ValueError("no library for a %d-slot register layout (have %s)"
-                         % (nreg, sorted(LAYOUTS)))
-    return LAYOUTS[nreg][0]
-
-
-def _generate(nreg: int, dst: str) -> None:
-    """asmgen's outputs for a ``nreg``-slot layout into ``dst`` (in this
-    process when its generator already has that layout, else in a child
-    with MYTHGPU_NREG set to it)."""
-    from mythril_amd import asmgen
-    if asmgen.NREG == nreg:
-        asmgen.write_outputs(dst)
-        return
-    code = ("import sys; sys.path.insert(0, %r); from mythril_amd import asmgen; "
-            "assert asmgen.NREG == %d; asmgen.write_outputs(%r)" % (ROOT, nreg, dst))
-    subprocess.run([sys.executable, "-c", code], check=True,
-                   env=dict(os.environ, MYTHGPU_NREG=str(nreg)))
-
-
-def build_layout(nreg: int, force: bool = False, verbose: bool = False) -> str:
-    out, defines = LAYOUTS[nreg]
-    if nreg == 16:
-        return build(force, verbose)
-    if not force and _fresh(out, _deps()):
-        return out
     import shutil
     import tempfile
-    os.makedirs(LIBDIR, exist_ok=True)
+    # the 16-slot interpreter's body and handler numbering are generated into
+    # the tracked sources (whatever this process's MYTHGPU_NREG)
+    _generate(16, CSRC)
+    objs = []
     with tempfile.TemporaryDirectory() as td:
-        src = os.path.join(td, "csrc")
-        shutil.copytree(CSRC, src)
-        _generate(nreg, src)
-        _compile(src, out, defines, None, verbose)
+        for src in SOURCES:
+            objs.append(_hipcc(CSRC, src, os.path.join(td, src + ".o"), defines, flags, verbose))
+        for nreg, (waves, _) in sorted(LAYOUTS.items()):
+            if nreg == 16:
+                continue
+            lay = os.path.join(td, "csrc_r%d" % nreg)
+            shutil.copytree(CSRC, lay)
+            _generate(nreg, lay)
+            objs.append(_hipcc(lay, "mg_interp_asm.hip", os.path.join(td, "interp_r%d.o" % nreg),
+                               list(defines) + ["MG_LAYOUT_NREG=%d" % nreg,
+                                                "MG_ASM_WAVES_PER_SIMD=%d" % waves],
+                               flags, verbose))
+        tmp = out + ".tmp"
+        subprocess.run([HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs,
+                       check=True)
+        os.replace(tmp, out)
+    if out == LIB:
+        build_jit_stub()
     return out
 
 
@@ -173,5 +148,4 @@ def build_compiler(force: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
-    print(build_layout(11, force="--force" in sys.argv))
     print(build_compiler(force="--force" in sys.argv))

@@ -134,8 +134,10 @@ def compile_native(constraints: Sequence, probes: Sequence = (),
         if rc == MGC_UNSUPPORTED:
             raise ir.Unsupported(err)
         raise RuntimeError("native compiler: " + err)
-    return _program(np.frombuffer(code_b, dtype=np.uint32).reshape(-1, 4).copy(), raw, ncv,
+    prog = _program(np.frombuffer(code_b, dtype=np.uint32).reshape(-1, 4).copy(), raw, ncv,
                     json.loads(meta))
+    prog.nreg = nreg
+    return prog
 
 
 def buckets(constraints: Sequence):
@@ -257,7 +259,9 @@ def compile_native_ctypes(constraints: Sequence, probes: Sequence = (),
         meta = json.loads(lib.mgc_meta(res))
     finally:
         lib.mgc_free(res)
-    return _program(code, raw, ncv.value, meta)
+    prog = _program(code, raw, ncv.value, meta)
+    prog.nreg = nreg
+    return prog
 
 
 class LeafRecords(_abc.Sequence):

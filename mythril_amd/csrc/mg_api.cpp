@@ -24,21 +24,35 @@
 #include "mg_asm_handlers.h"
 #include "mg_host.h"
 
-hipError_t mg_launch_asm(const mg_pdesc* d_descs, uint32_t n_progs, const mg_run& run,
-                         uint32_t mode, uint32_t lds_slots, uint32_t* table, hipStream_t stream);
+// the interpreter of each register layout (mg_interp_asm.hip, one
+// translation unit per layout; mg_find_layout lists them)
+typedef hipError_t (*mg_launch_fn)(const mg_pdesc* d_descs, uint32_t n_progs, const mg_run& run,
+                                   uint32_t mode, uint32_t lds_slots, uint32_t* table,
+                                   hipStream_t stream);
+hipError_t mg_launch_asm_r16(const mg_pdesc*, uint32_t, const mg_run&, uint32_t, uint32_t, uint32_t*,
+                             hipStream_t);
+hipError_t mg_launch_asm_r11(const mg_pdesc*, uint32_t, const mg_run&, uint32_t, uint32_t, uint32_t*,
+                             hipStream_t);
+const char* mg_asm_digest_r16(void);
+const char* mg_asm_digest_r11(void);
+static_assert(MG_NREG == 16 && MG_NREG_W4 == 11, "one interpreter per layout: _r16, _r11");
+
+static mg_launch_fn layout_launch(uint32_t nreg) {
+    return nreg == MG_NREG_W4 ? mg_launch_asm_r11 : mg_launch_asm_r16;
+}
+
 hipError_t mg_launch_keccak(const uint8_t* d_data, const uint64_t* d_off, const uint32_t* d_len,
                             uint32_t n, uint8_t* d_out, hipStream_t stream);
 
 
-// LDS spill regions per lane when MYTHGPU_LDS_SLOTS is unset: 6 fill the
-// CU at three 256-lane blocks (13 halves, mg_lds_bytes); the four-wave
-// layout (MG_ASM_WAVES_PER_SIMD=4, four blocks per CU) is built with 5
-#ifndef MG_LDS_SLOTS_DEFAULT
-#define MG_LDS_SLOTS_DEFAULT 6
-#endif
-
 struct mg_ctx {
     int device = 0;
+    // register layout of this context's interpreter (mg_init_layout): its
+    // slot count, kernel and LDS spill regions per lane (the layout's default
+    // — 6 fill the CU at three 256-lane blocks, 13 halves; 5 at four blocks —
+    // unless MYTHGPU_LDS_SLOTS sets it)
+    uint32_t nreg = MG_NREG;
+    mg_launch_fn launch_asm = mg_launch_asm_r16;
     hipStream_t stream = nullptr;
     std::string err;
     char name[256] = {0};
@@ -46,7 +60,7 @@ struct mg_ctx {
     // assembly interpreter: handler byte offsets (query launch at init) and
     // LDS spill slots per 256-lane block
     uint32_t hoff[MGA_NUM_HANDLERS] = {0};
-    uint32_t lds_slots = MG_LDS_SLOTS_DEFAULT;
+    uint32_t lds_slots = 6;
     // generator boundary-value table (device, 48 KiB; MG_BTAB_WORDS)
     uint32_t* d_btab = nullptr;
     // grow-only device workspace for synchronous calls
@@ -145,8 +159,8 @@ static uint32_t kernel_lds_slots(const mg_ctx* ctx, uint32_t n_lds) {
 
 static hipError_t launch(const mg_ctx* ctx, int gen, const mg_pdesc* d_descs, uint32_t n_progs,
                          const mg_run& run, uint32_t n_lds, hipStream_t stream) {
-    return mg_launch_asm(d_descs, n_progs, run, gen ? 1u : 0u, kernel_lds_slots(ctx, n_lds),
-                         nullptr, stream);
+    return ctx->launch_asm(d_descs, n_progs, run, gen ? 1u : 0u, kernel_lds_slots(ctx, n_lds),
+                           nullptr, stream);
 }
 
 // A loaded compiled-program code object (mythril_amd/jit.py) and the
@@ -284,7 +298,7 @@ static int query_handlers(mg_ctx* ctx) {
     memset(&run, 0, sizeof run);
     run.n_assign = 1;
     run.stride = 1;
-    if (e == hipSuccess) e = mg_launch_asm(d_desc, 1, run, 2u, 0, (uint32_t*)d, ctx->stream);
+    if (e == hipSuccess) e = ctx->launch_asm(d_desc, 1, run, 2u, 0, (uint32_t*)d, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(ctx->hoff, d, tab_b, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     (void)hipFree(d);
@@ -321,14 +335,29 @@ static void mg_boundary_table(uint32_t* t) {
     }
 }
 
-int mg_init(int device, mg_ctx** out) {
+int mg_init(int device, mg_ctx** out) { return mg_init_layout(device, MG_NREG, out); }
+
+const char* mg_asm_digest(void) { return mg_asm_digest_r16(); }
+
+const char* mg_asm_digest_layout(uint32_t nreg) {
+    if (nreg == MG_NREG) return mg_asm_digest_r16();
+    if (nreg == MG_NREG_W4) return mg_asm_digest_r11();
+    return nullptr;
+}
+
+int mg_init_layout(int device, uint32_t nreg, mg_ctx** out) {
     if (!out) return MG_E_ARG;
     *out = nullptr;
+    const mg_layout_info* lay = mg_find_layout(nreg);
+    if (!lay) return MG_E_ARG;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return MG_E_NODEV;
     if (device < 0 || device >= n) return MG_E_NODEV;
     mg_ctx* ctx = new mg_ctx();
     ctx->device = device;
+    ctx->nreg = nreg;
+    ctx->launch_asm = layout_launch(nreg);
+    ctx->lds_slots = lay->lds_slots;
     if (hipSetDevice(device) != hipSuccess) {
         delete ctx;
         return MG_E_NODEV;
@@ -428,7 +457,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     *out = nullptr;
     const uint32_t n_lds_slots = n_spill_slots < MG_MAX_LDS ? n_spill_slots : MG_MAX_LDS;
     int rc = mg_validate(ctx ? &ctx->err : nullptr, code, n_ins, n_consts, leaves, n_leaves, n_lds_slots, n_spill_slots,
-                      n_probes);
+                         n_probes, ctx->nreg);
     if (rc) return rc;
     HIPCHECK(ctx, hipSetDevice(ctx->device));
     // assembly records + translator masks (appended to the constant table);
@@ -436,7 +465,7 @@ int mg_load_program(mg_ctx* ctx, const uint32_t* code, uint32_t n_ins, const uin
     std::vector<uint32_t> rec;
     MaskPool pool;
     mg_translate_records(identity_handlers(), code, n_ins, n_consts,
-                         kernel_lds_slots(ctx, n_spill_slots), rec, pool);
+                         kernel_lds_slots(ctx, n_spill_slots), ctx->nreg, rec, pool);
     const uint32_t n_masks = (uint32_t)(pool.words.size() / 8);
     const uint32_t n_const_all = n_consts + n_masks + n_consts * 3;
     // device leaf descriptors: byte pool offsets and the per-leaf stream salt
@@ -925,7 +954,7 @@ int mg_jit_attach(mg_ctx* ctx, mg_prog* const* progs, uint32_t n_progs, const vo
         return fail(ctx, MG_E_HIP, "JIT image: %s (table %zu bytes for %u programs)",
                     hipGetErrorString(e), table_b, n_progs);
     }
-    const uint64_t want_digest = strtoull(mg_asm_digest(), nullptr, 16);
+    const uint64_t want_digest = strtoull(mg_asm_digest_layout(ctx->nreg), nullptr, 16);
     if ((uint64_t)row[0] != MG_JIT_MAGIC || (uint64_t)row[1] != want_digest) {
         (void)hipModuleUnload(mod);
         return fail(ctx, MG_E_ARG, "JIT image: built for another interpreter (header %016llx, "

@@ -70,7 +70,8 @@ static bool has_w32(uint32_t op) {
 }
 
 // register slots an IR instruction reads or writes (bit mask)
-static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
+static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c,
+                              uint32_t nreg) {
     switch (op) {
     case MG_NOP: return 0;
     case MG_CONST: case MG_LEAF: case MG_RELOAD: return 1u << d;
@@ -80,7 +81,7 @@ static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, u
     // the funnel shifts read one slot beyond their operand (masked off, but
     // the registers are read): the next slot for EXTRACT, the previous one
     // for CONCAT's high part
-    case MG_EXTRACT: return ((1u << d) | (3u << a)) & ((1u << MG_NREG) - 1);
+    case MG_EXTRACT: return ((1u << d) | (3u << a)) & ((1u << nreg) - 1);
     case MG_CONCAT: return (1u << d) | (1u << a) | (a ? 1u << (a - 1) : 0u) | (1u << b);
     case MG_ITE: case MG_CDWE: case MG_CDWX: return (1u << d) | (1u << a) | (1u << b) | (1u << c);
     case MG_BCAST: return (1u << d) | (1u << a);
@@ -89,8 +90,9 @@ static uint32_t slots_touched(uint32_t op, uint32_t d, uint32_t a, uint32_t b, u
 }
 
 // slots an instruction reads (its destination only when it is also an operand)
-static uint32_t slots_read(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t m = slots_touched(op, d, a, b, c);
+static uint32_t slots_read(uint32_t op, uint32_t d, uint32_t a, uint32_t b, uint32_t c,
+                           uint32_t nreg) {
+    uint32_t m = slots_touched(op, d, a, b, c, nreg);
     switch (op) {
     case MG_NOP: case MG_CONST: case MG_LEAF: case MG_RELOAD: return 0;
     case MG_SPILL: case MG_OUT: case MG_ROOT: return m;
@@ -128,7 +130,7 @@ enum : uint32_t {
 };
 
 static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, uint32_t n_lds,
-                                          std::vector<uint32_t>& place2) {
+                                          uint32_t nreg, std::vector<uint32_t>& place2) {
     struct Iv { uint32_t start, end, reloads; bool narrow; uint32_t loc, loc2; };
     std::vector<uint32_t> place(n_ins, 0);
     std::vector<Iv> ivs;
@@ -143,7 +145,7 @@ static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, 
         if (op == MG_SPILL) {
             if (imm >= open.size()) open.resize(imm + 1, -1);
             open[imm] = (int)ivs.size();
-            ivs.push_back({i, i, 0, a < MG_NREG && narrow_reg[a], 0, 0});
+            ivs.push_back({i, i, 0, a < nreg && narrow_reg[a], 0, 0});
             owner[i] = open[imm];
             continue;
         }
@@ -154,11 +156,11 @@ static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, 
                 ivs[k].reloads++;
             }
             owner[i] = k;
-            if (d < MG_NREG) narrow_reg[d] = k >= 0 ? ivs[k].narrow : w <= 32;
+            if (d < nreg) narrow_reg[d] = k >= 0 ? ivs[k].narrow : w <= 32;
             continue;
         }
         const bool writes = op != MG_NOP && op != MG_OUT && op != MG_ROOT;
-        if (writes && d < MG_NREG) narrow_reg[d] = is_compare(op) || w <= 32;
+        if (writes && d < nreg) narrow_reg[d] = is_compare(op) || w <= 32;
     }
     // LDS: 4-dword HALVES (half h: region h / 2, part h % 2, 4 KiB = 256
     // lanes x 16 B).  A 256-bit value takes two free halves (any two: the
@@ -274,7 +276,7 @@ static std::vector<uint32_t> place_spills(const uint32_t* code, uint32_t n_ins, 
 }
 
 void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
-                      uint32_t n_lds, std::vector<uint32_t>& rec, MaskPool& pool) {
+                          uint32_t n_lds, uint32_t nreg, std::vector<uint32_t>& rec, MaskPool& pool) {
     pool.base = n_consts;
     const uint32_t ones = pool.add(mask_lt(256));
     rec.clear();
@@ -286,7 +288,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
     // where every spilled value lives (LDS region / dword, or scratch), per
     // SPILL / RELOAD instruction (place_spills)
     std::vector<uint32_t> place2;           // a 256-bit LDS value's second half
-    const std::vector<uint32_t> place = place_spills(code, n_ins, n_lds, place2);
+    const std::vector<uint32_t> place = place_spills(code, n_ins, n_lds, nreg, place2);
     auto scratch_reload = [&](uint32_t i) {
         return (code[4 * i] & 0xFF) == MG_RELOAD && !(place[i] & PL_LDS);
     };
@@ -329,7 +331,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             const uint32_t* p = code + 4 * order[t - 1];
             const uint32_t pop = p[0] & 0xFF;
             if (slots_touched(pop, p[1] & 0xFF, (p[1] >> 8) & 0xFF, (p[1] >> 16) & 0xFF,
-                              (p[1] >> 24) & 0xFF) & (1u << rd))
+                              (p[1] >> 24) & 0xFF, nreg) & (1u << rd))
                 break;
             if (pop == MG_SPILL && p[2] == slot) break;
             --t;
@@ -357,8 +359,8 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             const uint32_t* f = code + 4 * order[q];
             const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
                            fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
-            if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) fuse = false;
-            else if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
+            if (slots_read(fop, fd, fa, fb, fc, nreg) & (1u << d)) fuse = false;
+            else if (slots_touched(fop, fd, fa, fb, fc, nreg) & (1u << d)) break;   // rewritten
         }
         if (fuse) {
             eqsel[pc] = 1;
@@ -383,7 +385,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
             const uint32_t* nx = code + 4 * order[pc + 1];
             const uint32_t nd = nx[1] & 0xFF, na = (nx[1] >> 8) & 0xFF, nb = (nx[1] >> 16) & 0xFF,
                            nc = (nx[1] >> 24) & 0xFF;
-            const uint32_t touch = slots_touched(op, d, a, b, c) | slots_touched(MG_ITE, nd, na, nb, nc);
+            const uint32_t touch = slots_touched(op, d, a, b, c, nreg) | slots_touched(MG_ITE, nd, na, nb, nc, nreg);
             if (pending & touch) wait_vm();
             uint32_t* r = emit();
             uint32_t var;
@@ -399,7 +401,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         }
         const bool leafd = op == MG_LEAF && w == 256;
         const bool reloadd = op == MG_RELOAD && !(pl & PL_LDS);
-        if (pending && (slots_touched(op, d, a, b, c) & pending)) wait_vm();
+        if (pending && (slots_touched(op, d, a, b, c, nreg) & pending)) wait_vm();
         if (leafd || reloadd) pending |= 1u << d;
         uint32_t* r = emit();
         uint32_t var = (in[0] & MG_ROOT_FLAG) ? MGA_V_ROOT : 0;
@@ -416,14 +418,14 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
         // handler (limb 0 only) serves, and the slot is then marked dirty
         // (round 5; the Bool results of compares are the common case)
         bool dirty = false;
-        if (writes && narrow && !clean[d] && d < MG_NREG) {
+        if (writes && narrow && !clean[d] && d < nreg) {
             dirty = true;
             bool read = false;
             for (uint32_t q = pc + 1; q < n_ins && dirty; ++q) {
                 const uint32_t* f = code + 4 * order[q];
                 const uint32_t fop = f[0] & 0xFF, fw = (f[0] >> 8) & 0x3FF, fd = f[1] & 0xFF,
                                fa = (f[1] >> 8) & 0xFF, fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
-                const uint32_t rd = slots_read(fop, fd, fa, fb, fc);
+                const uint32_t rd = slots_read(fop, fd, fa, fb, fc, nreg);
                 if (rd & (1u << d)) {
                     read = true;
                     const bool limb0 =
@@ -433,7 +435,7 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
                         (fop == MG_SPILL && (place[order[q]] & PL_NARROW));
                     if (!limb0) dirty = false;
                 }
-                if (slots_touched(fop, fd, fa, fb, fc) & ~rd & (1u << d)) break;   // rewritten
+                if (slots_touched(fop, fd, fa, fb, fc, nreg) & ~rd & (1u << d)) break;   // rewritten
             }
             (void)read;
         }
@@ -548,8 +550,8 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
                 const uint32_t* f = code + 4 * order[q];
                 const uint32_t fop = f[0] & 0xFF, fd = f[1] & 0xFF, fa = (f[1] >> 8) & 0xFF,
                                fb = (f[1] >> 16) & 0xFF, fc = (f[1] >> 24) & 0xFF;
-                if (slots_read(fop, fd, fa, fb, fc) & (1u << d)) { nw = false; break; }
-                if (slots_touched(fop, fd, fa, fb, fc) & (1u << d)) break;   // rewritten
+                if (slots_read(fop, fd, fa, fb, fc, nreg) & (1u << d)) { nw = false; break; }
+                if (slots_touched(fop, fd, fa, fb, fc, nreg) & (1u << d)) break;   // rewritten
             }
             if (nw) var = (var | MGA_V_NW) & ~MGA_V_DC;
         }
@@ -565,8 +567,9 @@ void mg_translate_records(const uint32_t* hoff, const uint32_t* code, uint32_t n
 }
 
 int mg_validate(std::string* err, const uint32_t* code, uint32_t n_ins, uint32_t n_consts,
-                    const mg_leafgen* leaves, uint32_t n_leaves, uint32_t n_lds,
-                    uint32_t n_spill, uint32_t n_probes) {
+                const mg_leafgen* leaves, uint32_t n_leaves, uint32_t n_lds,
+                uint32_t n_spill, uint32_t n_probes, uint32_t nreg) {
+    if (!mg_find_layout(nreg)) return fail(err, MG_E_ARG, "no %u-slot register layout", nreg);
     if (n_lds > MG_MAX_LDS) return fail(err, MG_E_ARG, "too many LDS slots (%u)", n_lds);
     if (n_spill < n_lds || n_spill - n_lds > MG_MAX_PSLOTS)
         return fail(err, MG_E_ARG, "spill slots %u (LDS %u)", n_spill, n_lds);
@@ -587,7 +590,7 @@ int mg_validate(std::string* err, const uint32_t* code, uint32_t n_ins, uint32_t
         if ((in[0] & ~(0x3FFFFu | MG_ROOT_FLAG)) != 0)
             return fail(err, MG_E_ARG, "ins %u: reserved bits set", pc);
         for (int k = 0; k < 4; ++k)
-            if (((in[1] >> (8 * k)) & 0xFF) >= MG_NREG)
+            if (((in[1] >> (8 * k)) & 0xFF) >= nreg)
                 return fail(err, MG_E_ARG, "ins %u: slot out of range", pc);
         const bool needs_w = op != MG_NOP && op != MG_SPILL && op != MG_OUT && op != MG_ROOT;
         if (needs_w && (w < 1 || w > MG_MAX_WIDTH))
@@ -628,23 +631,46 @@ int mg_validate(std::string* err, const uint32_t* code, uint32_t n_ins, uint32_t
     return MG_OK;
 }
 
+// The register layouts this library holds an interpreter for (one kernel
+// each, mg_interp_asm.hip): 16 slots at three waves per SIMD with six LDS
+// spill regions (13 halves fill the CU), 11 slots in 128 VGPRs at four waves
+// with five (40 KiB per block, four blocks per CU).
+static const mg_layout_info kLayouts[] = {{MG_NREG, 3, 6}, {MG_NREG_W4, 4, 5}};
+
+const mg_layout_info* mg_find_layout(uint32_t nreg) {
+    for (const auto& l : kLayouts)
+        if (l.nreg == nreg) return &l;
+    return nullptr;
+}
+
 extern "C" {
 
+int mg_layouts(uint32_t* out, uint32_t n) {
+    if (!out && n) return MG_E_ARG;
+    const uint32_t k = (uint32_t)(sizeof kLayouts / sizeof kLayouts[0]);
+    for (uint32_t i = 0; i < k && 3 * i + 2 < n; ++i) {
+        out[3 * i] = kLayouts[i].nreg;
+        out[3 * i + 1] = kLayouts[i].waves;
+        out[3 * i + 2] = kLayouts[i].lds_slots;
+    }
+    return (int)k;
+}
+
 int mg_translate(const uint32_t* code, uint32_t n_ins, uint32_t n_consts, uint32_t n_lds,
-                 const uint32_t* handler_off, uint32_t n_handlers, uint32_t* records,
-                 uint32_t max_record_words, uint32_t* n_record_words, uint32_t* masks,
-                 uint32_t max_mask_words, uint32_t* n_mask_words) {
+                 uint32_t nreg, const uint32_t* handler_off, uint32_t n_handlers,
+                 uint32_t* records, uint32_t max_record_words, uint32_t* n_record_words,
+                 uint32_t* masks, uint32_t max_mask_words, uint32_t* n_mask_words) {
     if ((n_ins && !code) || !handler_off || n_handlers != MGA_NUM_HANDLERS || !n_record_words ||
         !n_mask_words)
         return MG_E_ARG;
     // leaf and probe tables are not known here: only their indices' shape
     int rc = mg_validate(nullptr, code, n_ins, n_consts, nullptr, 0xFFFFFFFFu, MG_MAX_LDS,
-                      MG_MAX_LDS + MG_MAX_PSLOTS, 0xFFFFFFFFu);
+                         MG_MAX_LDS + MG_MAX_PSLOTS, 0xFFFFFFFFu, nreg);
     if (rc) return rc;
     if (n_lds > MG_MAX_LDS) return MG_E_ARG;
     std::vector<uint32_t> rec;
     MaskPool pool;
-    mg_translate_records(handler_off, code, n_ins, n_consts, n_lds, rec, pool);
+    mg_translate_records(handler_off, code, n_ins, n_consts, n_lds, nreg, rec, pool);
     *n_record_words = (uint32_t)rec.size();
     *n_mask_words = (uint32_t)pool.words.size();
     if (rec.size() > max_record_words || pool.words.size() > max_mask_words) return MG_E_ARG;

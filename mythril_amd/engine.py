@@ -18,24 +18,42 @@ import numpy as np
 from .ir import Program
 
 
-def _layout_lib() -> str:
-    """The in-tree library of this process's register layout
-    (``MYTHGPU_NREG``: 16 slots / three waves per SIMD by default, 11 / four
-    in ``libmythgpu_w4.so``; build.LAYOUTS)."""
+def _default_lib() -> str:
+    from .build import LIB
+    return LIB
+
+
+# One library holds the interpreter of every register layout (build.LAYOUTS;
+# a context runs one, Engine(nreg=...)).  MYTHGPU_LIB: an A/B build of the
+# same ABI.
+_LIB_PATH = os.environ.get("MYTHGPU_LIB") or _default_lib()
+
+EXPORTS = ("mg_init", "mg_init_layout", "mg_layouts", "mg_free", "mg_last_error",
+           "mg_device_info", "mg_load_program", "mg_free_program", "mg_eval", "mg_eval_gen",
+           "mg_search", "mg_batch_create", "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search",
+           "mg_batch_search_probes", "mg_keccak256", "mg_version", "mg_config", "mg_translate",
+           "mg_asm_digest", "mg_asm_digest_layout", "mg_last_kernel_ms", "mg_jit_attach",
+           "mg_jit_detach", "mg_runtime_info")
+
+
+def layouts() -> Dict[int, Tuple[int, int]]:
+    """slots -> (waves per SIMD, default LDS spill regions) of every register
+    layout the library holds (mg_layouts; build.LAYOUTS)."""
+    lib = load_library(check_digest=False)
+    buf = (C.c_uint32 * 24)()
+    n = lib.mg_layouts(buf, 24)
+    return {int(buf[3 * i]): (int(buf[3 * i + 1]), int(buf[3 * i + 2])) for i in range(n)}
+
+
+def lds_slots_for(nreg: int) -> int:
+    """LDS spill regions a context of the ``nreg``-slot layout uses (the
+    compiled programs of a batch are rendered for the same): the layout's
+    default, or ``MYTHGPU_LDS_SLOTS``."""
     from . import irdefs
-    from .build import lib_for_layout
-    return lib_for_layout(irdefs.NREG)
-
-
-# (MYTHGPU_LIB: an A/B build of the same ABI, with the asmgen knobs it was
-# built under set in the environment)
-_LIB_PATH = os.environ.get("MYTHGPU_LIB") or _layout_lib()
-
-EXPORTS = ("mg_init", "mg_free", "mg_last_error", "mg_device_info", "mg_load_program",
-           "mg_free_program", "mg_eval", "mg_eval_gen", "mg_search", "mg_batch_create",
-           "mg_batch_free", "mg_batch_eval_gen", "mg_batch_search", "mg_batch_search_probes", "mg_keccak256", "mg_version", "mg_config",
-           "mg_translate", "mg_asm_digest", "mg_last_kernel_ms", "mg_jit_attach", "mg_jit_detach",
-           "mg_runtime_info")
+    if "MYTHGPU_LDS_SLOTS" in os.environ:
+        return irdefs.check_lds_slots(os.environ["MYTHGPU_LDS_SLOTS"])
+    from .build import LAYOUT_LDS_SLOTS
+    return LAYOUT_LDS_SLOTS[nreg]
 
 
 class EngineUnavailable(RuntimeError):
@@ -82,6 +100,10 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         p, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
         lib.mg_version.restype = C.c_int
         lib.mg_init.argtypes = [C.c_int, C.POINTER(p)]
+        lib.mg_init_layout.argtypes = [C.c_int, u32, C.POINTER(p)]
+        lib.mg_layouts.argtypes = [p, u32]
+        lib.mg_asm_digest_layout.argtypes = [u32]
+        lib.mg_asm_digest_layout.restype = C.c_char_p
         lib.mg_free.argtypes = [p]
         lib.mg_free.restype = None
         lib.mg_last_error.argtypes = [p]
@@ -109,24 +131,25 @@ def load_library(path: str = _LIB_PATH, check_digest: bool = True):
         lib.mg_jit_detach.restype = None
         lib.mg_runtime_info.argtypes = [C.POINTER(C.c_int), C.c_char_p, C.c_size_t]
         pu32 = C.POINTER(u32)
-        lib.mg_translate.argtypes = [p, u32, u32, u32, p, u32, p, u32, pu32, p, u32, pu32]
+        lib.mg_translate.argtypes = [p, u32, u32, u32, u32, p, u32, p, u32, pu32, p, u32, pu32]
         for name in EXPORTS:
             getattr(lib, name)
-        from . import asmgen
-        want = asmgen.digest() if check_digest else None
-        got = lib.mg_asm_digest().decode()
-        if check_digest and got != want:
-            raise EngineUnavailable("%s was built from a different assembly interpreter "
-                                    "(digest %s, generator %s); rebuild with "
-                                    "`python -m mythril_amd.build`" % (path, got, want))
         if check_digest:
-            # the compiler allocates irdefs.NREG slots: the library's
-            # translator and interpreter must hold as many
-            from . import irdefs
-            cfg = (C.c_uint32 * 4)()
-            if lib.mg_config(cfg, 4) != 0 or cfg[1] != irdefs.NREG:
-                raise EngineUnavailable("%s holds %d register slots, the compiler %d "
-                                        "(MYTHGPU_NREG)" % (path, cfg[1], irdefs.NREG))
+            # every layout's interpreter must be the one this generator
+            # makes (a stale build is refused; ADVICE r5: and the slot count
+            # the compiler allocates must be a layout the library holds)
+            from . import asmgen
+            from .build import LAYOUTS
+            for nreg in sorted(LAYOUTS):
+                with asmgen.layout(nreg):
+                    want = asmgen.digest()
+                got = lib.mg_asm_digest_layout(nreg)
+                got = got.decode() if got else None
+                if got != want:
+                    raise EngineUnavailable(
+                        "%s was built from a different assembly interpreter for %d slots "
+                        "(digest %s, generator %s); rebuild with `python -m mythril_amd.build`"
+                        % (path, nreg, got, want))
             _libs[path] = lib
         return lib
 
@@ -161,23 +184,25 @@ class LoadedProgram:
 class Engine:
     """One HIP device context (one per host thread)."""
 
-    def __init__(self, device: int = 0, lib_path: str = _LIB_PATH):
+    def __init__(self, device: int = 0, lib_path: str = _LIB_PATH, nreg: Optional[int] = None):
+        """A context on ``device`` running the ``nreg``-slot register layout
+        (default: the process's, ``irdefs.NREG``; 16, or 11 for four waves
+        per SIMD): programs compiled for that many slots load into it."""
         # an A/B build elsewhere may carry another assembly interpreter
         self.lib = load_library(lib_path, check_digest=lib_path == _LIB_PATH)
         ctx = C.c_void_p()
         from . import irdefs
-        if "MYTHGPU_LDS_SLOTS" in os.environ:       # (mg_init refuses it too)
-            try:
-                irdefs.check_lds_slots(os.environ["MYTHGPU_LDS_SLOTS"])
-            except ValueError as e:
-                raise EngineUnavailable("MYTHGPU_LDS_SLOTS: %s" % e) from e
-        rc = self.lib.mg_init(device, C.byref(ctx))
+        self.nreg = irdefs.NREG if nreg is None else int(nreg)
+        try:
+            self.lds_slots = lds_slots_for(self.nreg)     # (mg_init refuses a bad one too)
+        except (KeyError, ValueError) as e:
+            raise EngineUnavailable("register layout %d / MYTHGPU_LDS_SLOTS: %s"
+                                    % (self.nreg, e)) from e
+        rc = self.lib.mg_init_layout(device, self.nreg, C.byref(ctx))
         if rc != 0:
-            raise EngineUnavailable("mg_init(%d) failed with %d (no usable GPU?)" % (device, rc))
+            raise EngineUnavailable("mg_init_layout(%d, %d) failed with %d (no usable GPU?)"
+                                    % (device, self.nreg, rc))
         self._ctx = ctx
-        cfg = (C.c_uint32 * 4)()
-        self.lib.mg_config(cfg, 4)
-        self.nreg = int(cfg[1])
         name = C.create_string_buffer(256)
         cus = C.c_int()
         self.lib.mg_device_info(ctx, name, 256, C.byref(cus))
@@ -208,6 +233,9 @@ class Engine:
 
     def load(self, program: Program, leafgen: Optional[Sequence[LeafGen]] = None,
              prog_seed: int = 0) -> LoadedProgram:
+        if program.nreg != self.nreg:
+            raise EngineError("program compiled for %d register slots, this context runs the "
+                              "%d-slot layout" % (program.nreg, self.nreg))
         code = np.ascontiguousarray(program.code, dtype=np.uint32)
         consts = np.ascontiguousarray(program.consts, dtype=np.uint32)
         gens = list(leafgen) if leafgen is not None else default_leafgen(program)
@@ -350,14 +378,17 @@ class Engine:
         return out
 
 
-def translate_records(program: Program, lds_slots: int = 6):
+def translate_records(program: Program, lds_slots: Optional[int] = None):
     """Host-only (no GPU): the records ``mg_load_program`` would upload for
     ``program`` with handler IDS in word 0 (the translator run with an
     identity offset table; the last record is the zeroed prefetch pad), and
     the number of mask entries the translator appended to the constant
-    table.  ``lds_slots`` is the context's LDS spill tier
-    (``MYTHGPU_LDS_SLOTS``, default 6)."""
+    table.  ``lds_slots`` is the context's LDS spill tier (``lds_slots_for``
+    the program's layout).  The translator is the one of the program's
+    register layout (``Program.nreg``)."""
     from . import asmgen
+    if lds_slots is None:
+        lds_slots = lds_slots_for(program.nreg)
     lib = load_library()
     code = np.ascontiguousarray(program.code, dtype=np.uint32)
     n_ins = code.shape[0]
@@ -368,7 +399,8 @@ def translate_records(program: Program, lds_slots: int = 6):
     masks = np.zeros(max_mask, dtype=np.uint32)
     nrw, nmw = C.c_uint32(), C.c_uint32()
     rc = lib.mg_translate(_ptr(code), n_ins, program.consts.shape[0],
-                          min(program.n_lds, lds_slots), _ptr(ident), asmgen.NUM_HANDLERS,
+                          min(program.n_lds, lds_slots), program.nreg, _ptr(ident),
+                          asmgen.NUM_HANDLERS,
                           C.cast(rec.ctypes.data, C.POINTER(C.c_uint32)), max_rec, C.byref(nrw),
                           _ptr(masks), max_mask, C.byref(nmw))
     if rc != 0:
@@ -376,21 +408,23 @@ def translate_records(program: Program, lds_slots: int = 6):
     return rec[:nrw.value], nmw.value // 8
 
 
-def record_handlers(program: Program, lds_slots: int = 6) -> List[int]:
+def record_handlers(program: Program, lds_slots: Optional[int] = None) -> List[int]:
     """The assembly-interpreter handler id of every record, in order."""
     rec, _ = translate_records(program, lds_slots)
     return [int(h) for h in rec[::8][:-1]]       # the last record is a zeroed pad
 
 
-def handler_variants(program: Program, lds_slots: int = 6):
+def handler_variants(program: Program, lds_slots: Optional[int] = None):
     """The set of (family, canonical variant) the program executes (every
     record runs on every lane: programs are straight-line)."""
     from . import asmgen
     out = set()
-    for h in record_handlers(program, lds_slots):
-        c = asmgen.canonical(h)
-        aop, var = c // (2 * asmgen.NVAR), (c // 2) % asmgen.NVAR
-        out.add((asmgen.AOPS[aop], var))
+    hs = record_handlers(program, lds_slots)
+    with asmgen.layout(program.nreg):
+        for h in hs:
+            c = asmgen.canonical(h)
+            aop, var = c // (2 * asmgen.NVAR), (c // 2) % asmgen.NVAR
+            out.add((asmgen.AOPS[aop], var))
     return out
 
 
@@ -410,13 +444,14 @@ def limbs_to_int(limbs) -> int:
     return v
 
 
-_engines: Dict[Tuple[int, int], Engine] = {}
+_engines: Dict[Tuple[int, int, int], Engine] = {}
 _failed: Dict[Tuple[int, int], str] = {}
 _engines_lock = threading.Lock()
 
 
-def get_engine(device: int = 0, slot: int = 0) -> Engine:
-    """The engine (one HIP context) of ``device``; ``slot`` > 0 gives further
+def get_engine(device: int = 0, slot: int = 0, nreg: Optional[int] = None) -> Engine:
+    """The engine (one HIP context) of ``device`` running the ``nreg``-slot
+    register layout (default: the process's); ``slot`` > 0 gives further
     independent contexts on the same device (a device listed twice in
     ``MYTHRIL_GPU_DEVICES`` is searched from two host threads, and a context
     serves one thread at a time).  An initialisation failure is remembered
@@ -424,21 +459,23 @@ def get_engine(device: int = 0, slot: int = 0) -> Engine:
     instead of retrying mg_init; a failed extra slot (e.g. out of memory for
     one more context) does not mark the device's first context failed, and
     the exception carries ``slot`` so callers can tell the two apart."""
+    from . import irdefs
+    nreg = irdefs.NREG if nreg is None else int(nreg)
     with _engines_lock:
-        e = _engines.get((device, slot))
+        e = _engines.get((device, slot, nreg))
         if e is None:
             for key in ((device, 0), (device, slot)):
                 if key in _failed:
                     raise EngineUnavailable(_failed[key], slot=key[1], device=device)
             try:
-                e = Engine(device)
+                e = Engine(device, nreg=nreg)
             except EngineUnavailable as x:
                 _failed[(device, slot)] = str(x)
                 raise EngineUnavailable(str(x), slot=slot, device=device) from x
             except Exception as x:  # noqa: BLE001 - any init failure means no engine
                 _failed[(device, slot)] = "%s: %s" % (type(x).__name__, x)
                 raise EngineUnavailable(_failed[(device, slot)], slot=slot, device=device) from x
-            _engines[(device, slot)] = e
+            _engines[(device, slot, nreg)] = e
         return e
 
 

@@ -121,6 +121,9 @@ class Program:
     # search mode: the independent group's constraint node ids (model.py's
     # group-miss memo)
     group_key: object = None
+    # register slots of the layout it was compiled for (16, or 11: the
+    # four-wave layout); a context of that layout loads it (Engine.load)
+    nreg: int = 16
 
     @property
     def solved(self) -> bool:
@@ -1302,6 +1305,7 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
     prog = Program(code, consts, const_values, lw.leaves, n_lds, probe_chunks,
                    len(constraints), tsizes, lw.table_kinds, ckeys, stats, pool_ranges,
                    derived, entry_keys, n_user_probes)
+    prog.nreg = nreg
     if plan is not None:
         prog.presets = plan
     return prog

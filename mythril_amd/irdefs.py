@@ -12,7 +12,10 @@ def _parse():
     ops, defs = {}, {}
     with open(_HDR) as fh:
         text = fh.read()
-    for m in re.finditer(r"\bMG_([A-Z0-9_]+)\s*=\s*(\d+)\s*[,\n]", text):
+    # opcodes: the enum mg_op body only (comments elsewhere may read "MG_X = n")
+    body = text[text.index("enum mg_op"):]
+    body = body[:body.index("};")]
+    for m in re.finditer(r"\bMG_([A-Z0-9_]+)\s*=\s*(\d+)\s*[,\n]", body):
         ops[m.group(1)] = int(m.group(2))
     for m in re.finditer(r"#define\s+MG_([A-Z_]+)\s+(\d+)", text):
         defs[m.group(1)] = int(m.group(2))

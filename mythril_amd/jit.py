@@ -974,6 +974,21 @@ _SPEC: Dict[tuple, tuple] = {}
 _TAG = "@T@"
 
 
+def _on_layout() -> None:
+    """asmgen switched register layouts (asmgen.layout): the register-file
+    and temporary ranges move, and every memo of rendered or specialised
+    text belongs to the previous layout."""
+    global SLOTS, TEMPS, FILE_LO, FILE_HI
+    SLOTS = range(G.FB, G.FB + 8 * G.NREG)
+    TEMPS = frozenset(list(range(G.XB, G.XB + 8)) + list(range(G.YB, G.TB + G.NT)))
+    FILE_LO, FILE_HI = G.FB, G.FB + 8 * G.NREG
+    for memo in (_TEMPLATES, _FIELDS, _SPEC, _COAL):
+        memo.clear()
+
+
+G._layout_hooks.append(_on_layout)
+
+
 def fields_read(lines: Sequence[str]) -> Tuple[int, ...]:
     """Record words a template reads (its s40..s47 operands)."""
     key = id(lines)
@@ -1043,11 +1058,14 @@ def records_fingerprint(rec) -> int:
     return (h + len(w) // 8) & ((1 << 64) - 1)
 
 
-def program_records(prog, leafgen, prog_seed: int, lds_slots: int = 6, full: bool = False):
+def program_records(prog, leafgen, prog_seed: int, lds_slots: Optional[int] = None,
+                    full: bool = False):
     """The records ``mg_load_program`` uploads for ``prog`` (handler ids in
     word 0; LEAFD records patched with their leaf's generator parameters
     exactly as mg_load_program does), and the translator's mask count."""
-    from .engine import translate_records
+    from .engine import lds_slots_for, translate_records
+    if lds_slots is None:
+        lds_slots = lds_slots_for(prog.nreg)
     rec, n_masks = translate_records(prog, I.check_lds_slots(lds_slots))
     rec = rec.reshape(-1, 8).copy()
     n_consts = prog.consts.shape[0]
@@ -1111,14 +1129,20 @@ def const_code(var: int, rec, prog) -> List[str]:
     return out
 
 
-def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: int = 6,
+def program_asm(prog, leafgen, prog_seed: int, entry: str, lds_slots: Optional[int] = None,
                 tag: Optional[str] = None, marks: bool = False,
                 fps: Optional[List[int]] = None) -> List[str]:
     """Straight-line gfx950 code of one program, entered at label
     ``entry`` (a local ``.L`` label, or a symbol the caller declares).
     ``marks``: a label ``.Lmark_<record>_<family>_<variant>`` ahead of each
     record's code (profiling in the simulator, tools/jit_profile.py).
-    ``fps``: the records' fingerprint is appended to it."""
+    ``fps``: the records' fingerprint is appended to it.  Rendered for the
+    program's register layout (``Program.nreg``)."""
+    with G.layout(prog.nreg):
+        return _program_asm(prog, leafgen, prog_seed, entry, lds_slots, tag, marks, fps)
+
+
+def _program_asm(prog, leafgen, prog_seed, entry, lds_slots, tag, marks, fps) -> List[str]:
     full, _ = program_records(prog, leafgen, prog_seed, lds_slots, full=True)
     recs = full[:-1]                             # the last record is the zeroed pad
     if fps is not None:
@@ -1194,11 +1218,28 @@ def peephole(lines: List[str]) -> List[str]:
 HEADER = '\t.amdgcn_target "amdgcn-amd-amdhsa--%s"\n' % ARCH
 
 
-def chunk_asm(items, first: int, lds_slots: int = 6, fps: Optional[List[int]] = None) -> str:
+def chunk_asm(items, first: int, lds_slots: Optional[int] = None,
+              fps: Optional[List[int]] = None) -> str:
     """One object's worth of programs: program ``first + i`` is entered at
     the (hidden) symbol ``mg_jp<first+i>``; the shared heavy bodies are
     copied into every chunk (local labels, a few KiB).  The programs' record
-    fingerprints are appended to ``fps``."""
+    fingerprints are appended to ``fps``.  The programs share one register
+    layout (the bodies are rendered for it)."""
+    nreg = _batch_layout(p for p, _, _ in items)
+    with G.layout(nreg):
+        return _chunk_asm(items, first, lds_slots, fps)
+
+
+def _batch_layout(progs) -> int:
+    """The one register layout of a batch's programs (a batch runs on one
+    context, Engine(nreg))."""
+    ns = {p.nreg for p in progs}
+    if len(ns) > 1:
+        raise ValueError("a batch mixes register layouts %s" % sorted(ns))
+    return ns.pop() if ns else G.NREG
+
+
+def _chunk_asm(items, first: int, lds_slots: int, fps: Optional[List[int]]) -> str:
     parts = [HEADER, "\t.text\n\t.p2align 8\n"]
     for i, (p, g, s) in enumerate(items):
         sym = "mg_jp%d" % (first + i)
@@ -1219,16 +1260,18 @@ def chunk_asm(items, first: int, lds_slots: int = 6, fps: Optional[List[int]] = 
     return "".join(parts)
 
 
-def table_asm(fps: Sequence[Optional[int]]) -> str:
+def table_asm(fps: Sequence[Optional[int]], nreg: Optional[int] = None) -> str:
     """The stub kernel and ``mg_jit_table``: a header row (JIT_MAGIC, the
     interpreter's asm digest: the code is generated from its handlers and
     assumes its pinned registers and descriptor layout), then row i + 1 =
     (mg_jp<i> - table, fingerprint of program i's records), or (0, 0) for a
     program that was not compiled (JitUnsupported: mg_jit_attach leaves it on
-    the interpreter)."""
+    the interpreter).  ``nreg``: the programs' register layout."""
     stub = open(STUB).read()
     cut = stub.index("\t.ident")
-    head = "\t.quad 0x%x\n\t.quad 0x%s\n" % (JIT_MAGIC, G.digest()[:16])
+    with G.layout(G.NREG if nreg is None else nreg):
+        dg = G.digest()
+    head = "\t.quad 0x%x\n\t.quad 0x%s\n" % (JIT_MAGIC, dg[:16])
     rows = "".join(("\t.quad mg_jp%d - . + %d\n\t.quad 0x%x\n" % (i, 16 * (i + 1), fp))
                    if fp is not None else "\t.quad 0\n\t.quad 0\n" for i, fp in enumerate(fps))
     return (stub[:cut] + "\t.data\n\t.globl mg_jit_table\n\t.protected mg_jit_table\n"
@@ -1270,8 +1313,11 @@ def source_digest() -> str:
                 with open(os.path.join(d, f), "rb") as fh:
                     h.update(f.encode() + fh.read())
     from . import ir
-    knobs = {"flush": COLD_FLUSH, "asm": G.digest(), "nreg": G.NREG,
-             "leaf_remat": ir.LEAF_REMAT}
+    asm = {}
+    for n in (16, 11):
+        with G.layout(n):
+            asm[n] = G.digest()
+    knobs = {"flush": COLD_FLUSH, "asm": sorted(asm.items()), "leaf_remat": ir.LEAF_REMAT}
     h.update(repr(sorted(knobs.items())).encode())
     return h.hexdigest()[:16]
 
@@ -1327,14 +1373,19 @@ def cached_image(key: str, build, cache_dir: Optional[str] = None) -> Tuple[byte
             fcntl.flock(lk, fcntl.LOCK_UN)
 
 
-def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
+def compile_batch(items, lds_slots: Optional[int] = None, workers: int = 1, chunk: int = 64,
                   start: str = "fork") -> bytes:
     """gfx950 code object of [(program, leafgen or None (= the C2 default),
     prog_seed)], entries in order (``Engine.jit_attach`` takes the same
     programs in the same order).  Chunks of programs are rendered and
     assembled on ``workers`` host processes (``start="fork"`` before the
     process touches the GPU, ``"spawn"`` after), then linked with the table
-    into one shared object."""
+    into one shared object.  ``lds_slots``: the LDS spill regions of the
+    context the programs will run on (default: their layout's,
+    engine.lds_slots_for)."""
+    if lds_slots is None:
+        from .engine import lds_slots_for
+        lds_slots = lds_slots_for(_batch_layout(p for p, _, _ in items))
     if workers > 1:                   # enough chunks to keep every worker busy
         chunk = max(1, min(chunk, -(-len(items) // (4 * workers))))
     with tempfile.TemporaryDirectory() as d:
@@ -1345,7 +1396,7 @@ def compile_batch(items, lds_slots: int = 6, workers: int = 1, chunk: int = 64,
         fps = [fp for _, f in objs for fp in f]
         objs = [o for o, _ in objs]
         tab = os.path.join(d, "table.o")
-        _as(table_asm(fps), tab)
+        _as(table_asm(fps, _batch_layout(p for p, _, _ in items)), tab)
         out = os.path.join(d, "jit.hsaco")
         subprocess.run([os.path.join(LLVM_BIN, "ld.lld"), "-shared", tab] + objs + ["-o", out],
                        check=True)

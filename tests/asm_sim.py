@@ -979,8 +979,12 @@ def translate(prog, n_lds: int):
     rec = np.zeros((2 * prog.n_ins + 3) * 8, dtype=np.uint32)
     masks = np.zeros(8 * 4096, dtype=np.uint32)
     nr, nm = C.c_uint32(0), C.c_uint32(0)
+    from mythril_amd import asmgen
+    if prog.nreg != asmgen.NREG:
+        raise SimError("a %d-slot program; this process simulates the %d-slot interpreter "
+                       "(MYTHGPU_NREG)" % (prog.nreg, asmgen.NREG))
     rc = lib.mg_translate(code.ctypes.data_as(C.c_void_p), prog.n_ins, prog.consts.shape[0], n_lds,
-                          tab.ctypes.data_as(C.c_void_p), NUM_HANDLERS,
+                          prog.nreg, tab.ctypes.data_as(C.c_void_p), NUM_HANDLERS,
                           rec.ctypes.data_as(C.c_void_p), rec.size, C.byref(nr),
                           masks.ctypes.data_as(C.c_void_p), masks.size, C.byref(nm))
     if rc != 0:

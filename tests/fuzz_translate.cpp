@@ -31,12 +31,14 @@
 struct Prog {
     std::vector<uint32_t> code;
     uint32_t n_consts, n_leaves, n_lds, n_spill, n_probes;
+    uint32_t nreg;                 // register layout: MG_NREG or MG_NREG_W4
 };
 
 static uint32_t ins_w0(uint32_t op, uint32_t w) { return op | (w << 8); }
 
 static Prog valid_program(std::mt19937_64& rng) {
     Prog p;
+    p.nreg = rng() % 2 ? MG_NREG : MG_NREG_W4;
     p.n_consts = 1 + rng() % 8;
     p.n_leaves = 1 + rng() % 8;
     p.n_spill = rng() % (MG_MAX_LDS + MG_MAX_PSLOTS + 1);
@@ -46,8 +48,8 @@ static Prog valid_program(std::mt19937_64& rng) {
     for (uint32_t i = 0; i < n; ++i) {
         uint32_t op = 1 + rng() % (MG_NUM_OPS - 1);
         uint32_t w = 1 + rng() % MG_MAX_WIDTH, imm = 0;
-        const uint32_t d = rng() % MG_NREG, a = rng() % MG_NREG, b = rng() % MG_NREG,
-                       c = rng() % MG_NREG;
+        const uint32_t d = rng() % p.nreg, a = rng() % p.nreg, b = rng() % p.nreg,
+                       c = rng() % p.nreg;
         switch (op) {
         case MG_CONST: imm = rng() % p.n_consts; break;
         case MG_LEAF: imm = rng() % p.n_leaves; break;
@@ -103,7 +105,7 @@ static void check_records(const Prog& p, const std::vector<uint32_t>& rec, const
             continue;
         }
         CHECK(w[0] >= 1 && w[0] <= MGA_NUM_HANDLERS);   // handler table index + 1
-        CHECK(w[1] < 8 * MG_NREG && w[2] < 8 * MG_NREG);
+        CHECK(w[1] < 8 * p.nreg && w[2] < 8 * p.nreg);
         CHECK(w[1] % 8 == 0 && w[2] % 8 == 0);
     }
     CHECK(pool.words.size() % 8 == 0);
@@ -116,7 +118,7 @@ static int run_one(const Prog& p, const uint32_t* hoff, bool must_accept) {
     for (uint32_t i = 0; i < p.n_leaves; ++i) gens[i] = {1 + i * 31 % 256, 0, p.n_consts, 20, 40, 60};
     std::string err;
     const int rc = mg_validate(&err, p.code.data(), n, p.n_consts, gens.data(), p.n_leaves,
-                               p.n_lds, p.n_spill, p.n_probes);
+                               p.n_lds, p.n_spill, p.n_probes, p.nreg);
     if (must_accept && rc != MG_OK) {
         fprintf(stderr, "valid program rejected: %s\n", err.c_str());
         abort();
@@ -127,17 +129,18 @@ static int run_one(const Prog& p, const uint32_t* hoff, bool must_accept) {
     }
     std::vector<uint32_t> rec;
     MaskPool pool;
-    mg_translate_records(hoff, p.code.data(), n, p.n_consts, p.n_lds < 6 ? p.n_lds : 6, rec, pool);
+    mg_translate_records(hoff, p.code.data(), n, p.n_consts, p.n_lds < 6 ? p.n_lds : 6, p.nreg,
+                         rec, pool);
     check_records(p, rec, pool);
     // the exported entry: exact-size buffers, then too-small ones
     uint32_t nw = 0, nm = 0;
     std::vector<uint32_t> out(rec.size() + 8), masks(pool.words.size() + 8);
-    int rc2 = mg_translate(p.code.data(), n, p.n_consts, p.n_lds < 6 ? p.n_lds : 6, hoff,
+    int rc2 = mg_translate(p.code.data(), n, p.n_consts, p.n_lds < 6 ? p.n_lds : 6, p.nreg, hoff,
                            MGA_NUM_HANDLERS, out.data(), (uint32_t)out.size(), &nw, masks.data(),
                            (uint32_t)masks.size(), &nm);
     CHECK(rc2 == MG_OK && nw == rec.size() && nm == pool.words.size());
     if (nw > 8) {
-        rc2 = mg_translate(p.code.data(), n, p.n_consts, p.n_lds < 6 ? p.n_lds : 6, hoff,
+        rc2 = mg_translate(p.code.data(), n, p.n_consts, p.n_lds < 6 ? p.n_lds : 6, p.nreg, hoff,
                            MGA_NUM_HANDLERS, out.data(), nw - 8, &nw, masks.data(),
                            (uint32_t)masks.size(), &nm);
         CHECK(rc2 == MG_E_ARG);
@@ -163,12 +166,23 @@ int main(int argc, char** argv) {
     }
     // null / degenerate arguments of the exported entry
     uint32_t nw, nm;
-    CHECK(mg_translate(nullptr, 1, 0, 0, hoff.data(), MGA_NUM_HANDLERS, nullptr, 0, &nw, nullptr,
-                       0, &nm) == MG_E_ARG);
-    CHECK(mg_translate(nullptr, 0, 0, 0, hoff.data(), MGA_NUM_HANDLERS - 1, nullptr, 0, &nw,
+    CHECK(mg_translate(nullptr, 1, 0, 0, MG_NREG, hoff.data(), MGA_NUM_HANDLERS, nullptr, 0, &nw,
                        nullptr, 0, &nm) == MG_E_ARG);
-    CHECK(mg_translate(nullptr, 0, 0, MG_MAX_LDS + 1, hoff.data(), MGA_NUM_HANDLERS, nullptr, 0,
+    CHECK(mg_translate(nullptr, 0, 0, 0, MG_NREG, hoff.data(), MGA_NUM_HANDLERS - 1, nullptr, 0,
                        &nw, nullptr, 0, &nm) == MG_E_ARG);
+    CHECK(mg_translate(nullptr, 0, 0, MG_MAX_LDS + 1, MG_NREG, hoff.data(), MGA_NUM_HANDLERS,
+                       nullptr, 0, &nw, nullptr, 0, &nm) == MG_E_ARG);
+    // a slot count no layout has, and a 16-slot program offered to the 11-slot layout
+    CHECK(mg_translate(nullptr, 0, 0, 0, 12, hoff.data(), MGA_NUM_HANDLERS, nullptr, 0, &nw,
+                       nullptr, 0, &nm) == MG_E_ARG);
+    {
+        const uint32_t code[4] = {ins_w0(MG_CONST, 8), 13u, 0u, 0u};   // dst slot 13
+        std::vector<uint32_t> out(64), masks(64);
+        CHECK(mg_translate(code, 1, 1, 0, MG_NREG_W4, hoff.data(), MGA_NUM_HANDLERS, out.data(),
+                           64, &nw, masks.data(), 64, &nm) == MG_E_ARG);
+        CHECK(mg_translate(code, 1, 1, 0, MG_NREG, hoff.data(), MGA_NUM_HANDLERS, out.data(),
+                           64, &nw, masks.data(), 64, &nm) == MG_OK);
+    }
     printf("{\"iterations\": %ld, \"valid_accepted\": %ld, \"mutated_accepted\": %ld, "
            "\"random_accepted\": %ld}\n", iters, accepted, mutated_ok, random_ok);
     return 0;

@@ -15,9 +15,10 @@ test checked lane by lane.
 
 The module runs on the register layout of its process (``MYTHGPU_NREG``):
 the default 16 slots, and — from ``tests/test_gpu_layout.py``, in a fresh
-process with ``MYTHGPU_NREG=11 MYTHGPU_LDS_SLOTS=5`` — the four-wave 11-slot
-layout (``libmythgpu_w4.so``) that ``bench.py`` runs C2 on.  Programs are
-compiled for the layout's slots and translated for its LDS regions.
+process with ``MYTHGPU_NREG=11`` — the four-wave 11-slot layout that
+``bench.py`` runs C2 on (the library's second interpreter, chosen by the
+context: ``Engine(nreg=11)``).  Programs are compiled for the layout's slots
+and translated for its LDS regions.
 """
 
 import ctypes as C
@@ -28,7 +29,7 @@ import pytest
 
 import bench
 from mythril_amd import irdefs, shard
-from mythril_amd.build import LAYOUT_LDS_SLOTS, lib_for_layout
+from mythril_amd.build import LAYOUT_LDS_SLOTS
 from mythril_amd.engine import default_leafgen, handler_variants, unpack_bits
 
 pytestmark = pytest.mark.gpu
@@ -38,19 +39,18 @@ SEED = bench.SEED
 FULL = {w: bench.default_units(w) for w in ("c2", "c3", "c4", "c5")}
 # (family, variant) handlers of the programs verified lane by lane below
 CHECKED = set()
-# the LDS spill regions of this process's layout (the context reads the same
-# variable; bench.apply_layout sets it per layout)
+# the LDS spill regions of this process's layout (the context's)
 LDS = int(os.environ.get("MYTHGPU_LDS_SLOTS", LAYOUT_LDS_SLOTS[irdefs.NREG]))
 
 
 def test_layout_of_this_process(engine):
-    """The library, its slot count and the compiler's agree on one layout."""
-    got = C.c_uint32 * 4
-    cfg = got()
-    assert engine.lib.mg_config(cfg, 4) == 0
-    assert cfg[1] == irdefs.NREG
-    assert os.path.basename(bench.engine_lib_path()) == os.path.basename(lib_for_layout(irdefs.NREG))
-    assert LDS == LAYOUT_LDS_SLOTS[irdefs.NREG]
+    """The context, the compiler and the translator agree on one layout."""
+    from mythril_amd import asmgen
+    assert engine.nreg == irdefs.NREG and engine.lds_slots == LDS == LAYOUT_LDS_SLOTS[irdefs.NREG]
+    with asmgen.layout(irdefs.NREG):
+        assert engine.lib.mg_asm_digest_layout(irdefs.NREG).decode() == asmgen.digest()
+    _, p, _, _ = bench.compile_unit(("c2", 0))
+    assert p.nreg == irdefs.NREG
     print("layout: %d slots, %d LDS regions, %s" % (irdefs.NREG, LDS,
                                                      os.path.basename(bench.engine_lib_path())))
 
@@ -228,8 +228,8 @@ def test_jit_attach_refuses_another_interpreter_and_stray_entries(engine, monkey
     with pytest.raises(EngineError, match="another interpreter"):
         engine.jit_attach([lp], stale)
 
-    def stray(fps):
-        return real(fps).replace("\t.quad mg_jp0 - . + 16\n", "\t.quad 16\n")
+    def stray(fps, nreg=None):
+        return real(fps, nreg).replace("\t.quad mg_jp0 - . + 16\n", "\t.quad 16\n")
     monkeypatch.setattr(jit, "table_asm", stray)
     bad = jit.compile_batch([(p1, None, d1)])
     monkeypatch.undo()

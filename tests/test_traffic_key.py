@@ -31,29 +31,40 @@ def _run_json(code: str):
 
 def kernel_key_as_bench(workload: str, dags: int):
     """bench.kernel_key of a default ``bench.py --workload <workload>`` run,
-    computed in a fresh process under the register layout bench.py picks for
-    the workload (bench.apply_layout, before the compiler is imported)."""
+    computed in a fresh process: the batch's register layout chosen as
+    bench.py chooses it (mythril_amd/layout.py over the 16-slot programs)."""
     return _run_json(
         "import json, os, bench\n"
-        "bench.apply_layout(%r)\n"
         "from mythril_amd import asmgen\n"
-        "corpus = bench.build_corpus(%d, min(8, os.cpu_count() or 1), workload=%r)\n"
-        "print(json.dumps(bench.kernel_key(asmgen.digest(), %r, %d, 20, True, corpus)))\n"
-        % (workload, dags, workload, workload, dags))
+        "w = min(8, os.cpu_count() or 1)\n"
+        "nreg, corpus = bench.choose_layout(bench.build_corpus(%d, w, workload=%r, nreg=16), w, "
+        "None, %r)\n"
+        "with asmgen.layout(nreg):\n"
+        "    dg = asmgen.digest()\n"
+        "print(json.dumps(bench.kernel_key(dg, %r, %d, 20, True, corpus, nreg)))\n"
+        % (dags, workload, workload, workload, dags))
 
 
 def test_bench_register_layouts():
-    """C2 runs the 11-slot, four-wave layout with five LDS regions; the query
-    streams the 16-slot default with six."""
+    """the layout is chosen per batch from its 16-slot
+    programs (mythril_amd/layout.py) — C2 runs the 11-slot, four-wave layout
+    with five LDS regions, the query streams the 16-slot default with six
+     — in ONE process, no import-time switch."""
     got = _run_json(
         "import json, os, bench\n"
+        "from mythril_amd import layout\n"
+        "from mythril_amd.engine import lds_slots_for\n"
         "out = {}\n"
-        "for w in ('c2', 'c3', 'c4', 'c5'):\n"
-        "    for k in ('MYTHGPU_NREG', 'MYTHGPU_LDS_SLOTS'):\n"
-        "        os.environ.pop(k, None)\n"
-        "    out[w] = [bench.apply_layout(w), bench.LDS_SLOTS]\n"
+        "for wl in ('c2', 'c3', 'c4', 'c5'):\n"
+        "    c16 = bench.build_corpus(bench.default_units(wl), 8, workload=wl, nreg=16)\n"
+        "    nreg, corpus = bench.choose_layout(c16, 8, None, wl)\n"
+        "    assert all(p.nreg == nreg for _, p, _, _ in corpus)\n"
+        "    out[wl] = [nreg, lds_slots_for(nreg), round(layout.mean_scratch_slots("
+        "[p for _, p, _, _ in c16]), 2)]\n"
         "print(json.dumps(out))\n")
-    assert got == {"c2": [11, 5], "c3": [16, 6], "c4": [16, 6], "c5": [16, 6]}
+    assert {w: v[:2] for w, v in got.items()} == {"c2": [11, 5], "c3": [16, 6], "c4": [16, 6],
+                                                  "c5": [16, 6]}
+    assert got["c2"][2] <= 3.0 < got["c4"][2] < got["c5"][2] < got["c3"][2]
 
 
 def test_traffic_json_keyed_to_this_tree():

@@ -19,20 +19,20 @@ def main():
     import bench
     w = sys.argv[1] if len(sys.argv) > 1 else "c3"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else bench.default_units(w)
-    bench.apply_layout(w)
     from mythril_amd import jit
-    from mythril_amd.engine import default_leafgen, get_engine
-    corpus = bench.build_corpus(n, 16, workload=w)
+    from mythril_amd.engine import default_leafgen, get_engine, lds_slots_for
+    nreg, corpus = bench.choose_layout(bench.build_corpus(n, 16, workload=w, nreg=16), 16, None, w)
+    print("layout %d slots" % nreg, flush=True)
     variants = {"base": (50, 70, 85), "noload": (50, 100, 100), "bnd_only": (50, 70, 100),
                 "pool_only": (50, 85, 85)}
     images = {}
     for k, pct in variants.items():
         t0 = time.time()
         images[k] = jit.compile_batch([(p, default_leafgen(p, pct), d) for d, p, _, _ in corpus],
-                                      workers=16, lds_slots=bench.LDS_SLOTS)
+                                      workers=16, lds_slots=lds_slots_for(nreg))
         print("image %s %.1f s" % (k, time.time() - t0), flush=True)
     import torch
-    eng = get_engine(0)
+    eng = get_engine(0, nreg=nreg)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     n_assign = 1 << 20
