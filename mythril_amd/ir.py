@@ -710,6 +710,32 @@ def _schedule(sinks: List[LNode]) -> List[LNode]:
     return lazy
 
 
+def _schedule_demand(sinks: List[LNode]) -> List[LNode]:
+    """Evaluation order driven by the sinks: in sink order, each sink's
+    operands not yet scheduled in post-order (a value is computed right
+    before the first sink that needs it, not where the source built it)."""
+    seen, out = set(), []
+    for s in sorted(sinks, key=lambda n: (n.birth, n.id)):
+        stack = [(s, False)]
+        while stack:
+            n, done = stack.pop()
+            if done:
+                out.append(n)
+                continue
+            if n.id in seen:
+                continue
+            seen.add(n.id)
+            stack.append((n, True))
+            for a in reversed(n.args):
+                if a.id not in seen:
+                    stack.append((a, False))
+    return out
+
+
+# experiment (round 6): MYTHRIL_GPU_SCHEDULE=demand (Python compiler only)
+SCHEDULE = _os.environ.get("MYTHRIL_GPU_SCHEDULE", "source")
+
+
 def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
     """A ROOT that directly follows the instruction computing its operand is
     folded into that instruction (MG_ROOT_FLAG): one dispatch fewer per
@@ -1271,7 +1297,7 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
         if n.op in (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO):
             n.imm = n.width
             n.width = 1
-    order, fused = _fuse_roots(_schedule(sinks))
+    order, fused = _fuse_roots(_schedule_demand(sinks) if SCHEDULE == "demand" else _schedule(sinks))
     const_values = sorted({n.imm & ((1 << 256) - 1) for n in order if n.op == I.CONST} |
                           {v & ((1 << 256) - 1) for v in extra_consts})
     const_index = {v: i for i, v in enumerate(const_values)}
