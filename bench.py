@@ -390,13 +390,14 @@ def main():
     # 16-slot programs, recompiled for it when it is the four-wave one
     nreg, corpus = choose_layout(corpus16, workers, mine, args.workload)
     from mythril_amd import layout as LAY
-    layout_rule = {"nreg": nreg, "rule": "four waves when the 16-slot programs hold <= %.1f "
-                   "scratch spill slots each on average (mythril_amd/layout.py)"
-                   % LAY.W4_MAX_SCRATCH_SLOTS,
-                   "mean_scratch_slots_16": round(LAY.mean_scratch_slots(
-                       [p for _, p, _, _ in corpus16]), 3),
+    progs16 = [p for _, p, _, _ in corpus16]
+    layout_rule = {"nreg": nreg, "rule": "four waves when the 16-slot programs average >= %.2f "
+                   "heavy records and <= %.1f scratch spill slots (mythril_amd/layout.py)"
+                   % (LAY.W4_MIN_HEAVY_SHARE, LAY.W4_MAX_SCRATCH_SLOTS),
+                   "mean_scratch_slots_16": round(LAY.mean_scratch_slots(progs16), 3),
+                   "mean_heavy_share_16": round(LAY.mean_heavy_share(progs16), 4),
                    "explicit": explicit_layout() is not None}
-    del corpus16
+    del corpus16, progs16
     global LDS_SLOTS
     from mythril_amd.engine import lds_slots_for
     LDS_SLOTS = lds_slots_for(nreg)

@@ -25,6 +25,7 @@
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -2205,6 +2206,34 @@ static std::vector<int> schedule(const std::vector<LN>& ln, const Chunks& sinks)
     return lazy;
 }
 
+// ir._schedule_demand: the sinks in (birth, id) order, each sink's operands
+// not yet scheduled in post-order (a value right before its first consumer)
+static std::vector<int> schedule_demand(const std::vector<LN>& ln, const Chunks& sinks) {
+    std::vector<int> ss(sinks.begin(), sinks.end());
+    std::sort(ss.begin(), ss.end(), [&](int a, int b) {
+        if (ln[a].birth != ln[b].birth) return ln[a].birth < ln[b].birth;
+        return a < b;
+    });
+    std::vector<char> seen(ln.size(), 0);
+    std::vector<int> out;
+    std::vector<std::pair<int, bool>> stack;
+    for (int s : ss) {
+        stack.push_back({s, false});
+        while (!stack.empty()) {
+            auto [n, done] = stack.back();
+            stack.pop_back();
+            if (done) { out.push_back(n); continue; }
+            if (seen[n]) continue;
+            seen[n] = 1;
+            stack.push_back({n, true});
+            const auto& args = ln[n].args;
+            for (size_t k = args.size(); k-- > 0;)
+                if (!seen[args[k]]) stack.push_back({args[k], false});
+        }
+    }
+    return out;
+}
+
 static std::vector<int> fuse_roots(const std::vector<LN>& ln, const std::vector<int>& order,
                                    std::unordered_set<int>& fused) {
     std::vector<int> out;
@@ -3020,8 +3049,33 @@ static void compile(const mgc_input* in, mgc_result* res) {
     const_values.erase(std::unique(const_values.begin(), const_values.end()), const_values.end());
     std::unordered_map<U, int, UHash> const_index;
     for (size_t i = 0; i < const_values.size(); i++) const_index[const_values[i]] = (int)i;
-    Alloc al(lw.ln, order, const_index, fused, in->nreg, in->remat_mode, in->remat_k, in->keep_clean != 0);
-    al.run();
+    Alloc al0(lw.ln, order, const_index, fused, in->nreg, in->remat_mode, in->remat_k,
+              in->keep_clean != 0);
+    al0.run();
+    // eval form: the sink-driven order too, and the cheaper allocation
+    // (ir.compile_constraints_py: scratch spill slots, then spill + reload
+    // records, then instructions); search programs keep source order
+    const Alloc* alp = &al0;
+    std::unordered_set<int> fused2;
+    std::vector<int> order2;
+    std::unique_ptr<Alloc> al2;
+    if (!in->solve && !in->leaf_pools) {
+        order2 = fuse_roots(lw.ln, schedule_demand(lw.ln, sinks), fused2);
+        try {
+            al2.reset(new Alloc(lw.ln, order2, const_index, fused2, in->nreg, in->remat_mode,
+                                in->remat_k, in->keep_clean != 0));
+            al2->run();
+        } catch (const Unsupported&) {
+            al2.reset();
+        }
+        auto cost = [](const Alloc& a) {
+            return std::make_tuple(std::max(0, a.n_lds - LDS_TIER), a.n_spill + a.n_reload,
+                                   (int)a.ins.size());
+        };
+        if (al2 && cost(*al2) < cost(al0)) alp = al2.get();
+    }
+    const Alloc& al = *alp;
+    const std::vector<int>& ord = alp == &al0 ? order : order2;
     tp[6] = now_us();
     res->code.resize(4 * al.ins.size());
     for (size_t k = 0; k < al.ins.size(); k++) {
@@ -3159,8 +3213,8 @@ static void compile(const mgc_input* in, mgc_result* res) {
         }
     }
     std::vector<int> hist(MG_NUM_OPS, 0);
-    for (int n : order) hist[lw.ln[n].op]++;
-    o += "],\"lnodes\":" + std::to_string(order.size());
+    for (int n : ord) hist[lw.ln[n].op]++;
+    o += "],\"lnodes\":" + std::to_string(ord.size());
     o += ",\"spills\":" + std::to_string(al.n_spill);
     o += ",\"reloads\":" + std::to_string(al.n_reload);
     o += ",\"hist\":[";
@@ -3177,7 +3231,7 @@ static void compile(const mgc_input* in, mgc_result* res) {
     {
         std::vector<char> seen(MG_NUM_OPS, 0);
         bool first = true;
-        for (int n : order) {
+        for (int n : ord) {
             int op = lw.ln[n].op;
             if (seen[op]) continue;
             seen[op] = 1;

@@ -732,8 +732,17 @@ def _schedule_demand(sinks: List[LNode]) -> List[LNode]:
     return out
 
 
-# experiment (round 6): MYTHRIL_GPU_SCHEDULE=demand (Python compiler only)
-SCHEDULE = _os.environ.get("MYTHRIL_GPU_SCHEDULE", "source")
+def _alloc_cost(n_lds: int, n_spill: int, n_reload: int, n_ins: int) -> Tuple[int, int, int]:
+    """Static cost of an allocation, compared lexicographically: spill slots
+    past the LDS tier (per-lane scratch, the HBM round trips a memory-bound
+    program waits on), then spill and reload records, then instructions."""
+    return (max(0, n_lds - LDS_TIER), n_spill + n_reload, n_ins)
+
+
+# A/B of the schedule choice (this Python specification only, with
+# MYTHRIL_GPU_COMPILER=py: it emits the native compiler's programs, so an
+# A/B through it measures the native default against source order)
+SCHEDULE_CHOICE = _os.environ.get("MYTHRIL_GPU_SCHEDULE_CHOICE", "1") != "0"
 
 
 def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
@@ -1297,11 +1306,27 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
         if n.op in (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO):
             n.imm = n.width
             n.width = 1
-    order, fused = _fuse_roots(_schedule_demand(sinks) if SCHEDULE == "demand" else _schedule(sinks))
+    order, fused = _fuse_roots(_schedule(sinks))
     const_values = sorted({n.imm & ((1 << 256) - 1) for n in order if n.op == I.CONST} |
                           {v & ((1 << 256) - 1) for v in extra_consts})
     const_index = {v: i for i, v in enumerate(const_values)}
     ins, n_lds, n_spill, n_reload = _allocate(order, const_index, fused, nreg)
+    if not solve and not leaf_pools and SCHEDULE_CHOICE:
+        # eval form (round 6): the sink-driven order too, and the one whose
+        # allocation costs less (the query streams' calldata words and
+        # store-chain reads are built early and read late: C3 -29 % spill
+        # records, C4 -48 %; C2's random DAGs mostly keep source order).
+        # Search programs keep source order: their compile latency is in
+        # front of every query, and their leaf pools follow that order.
+        order2, fused2 = _fuse_roots(_schedule_demand(sinks))
+        try:
+            alt = _allocate(order2, const_index, fused2, nreg)
+        except Unsupported:
+            alt = None
+        if alt is not None and _alloc_cost(alt[1], alt[2], alt[3], len(alt[0])) < \
+                _alloc_cost(n_lds, n_spill, n_reload, len(ins)):
+            ins, n_lds, n_spill, n_reload = alt
+            order, fused = order2, fused2
     code = np.zeros((len(ins), 4), dtype=np.uint32)
     for k, (op, width, d, a, b, c, imm, *fl) in enumerate(ins):
         code[k, 0] = op | (width << 8) | (fl[0] if fl else 0)

@@ -21,9 +21,17 @@ C5         5.50                                          -11 %
 C3         14.92                                         -11 %
 =========  ===========================================  ===================
 
-so the rule is: the four-wave layout when the batch's 16-slot programs hold
-at most ``W4_MAX_SCRATCH_SLOTS`` scratch spill slots per program on average.
-The statistic is static (the compiler's spill-slot count, ``Program.n_lds``
+and the scratch count alone is not enough: with the sink-driven schedule
+(round 6) C4's programs fall to 2.94 scratch slots at 16, yet C4 on the
+four-wave layout lost 26-31 % (``profiles/r06/sched/``).  What C2 has and
+the query streams lack is heavy arithmetic: C2's programs are 8.5 % MUL /
+division / umul_noovfl records (``ir.heavy_share``; every one of them at
+least 1 %), C3 / C4 / C5 0.14 / 0 / 0.25 % — C2 is VALU-issue-bound (VALU
+active 0.92 of SIMD cycles at three waves), the streams wait on memory.  So
+the rule is: the four-wave layout when the batch's 16-slot programs average
+at least ``W4_MIN_HEAVY_SHARE`` heavy records AND at most
+``W4_MAX_SCRATCH_SLOTS`` scratch spill slots per program.  Both statistics
+are static (the compiler's records and spill-slot count, ``Program.n_lds``
 minus the 16-slot layout's LDS tier), known before anything is launched.
 """
 
@@ -34,8 +42,10 @@ from .ir import Program
 DEFAULT = 16
 FOUR_WAVES = 11
 # mean scratch spill slots per 16-slot program at or below which a batch
-# runs the four-wave layout (between C2's 1.80 and C4's 4.38, above)
+# may run the four-wave layout (between C2's 1.80 and C4's 4.38, above)
 W4_MAX_SCRATCH_SLOTS = 3.0
+# mean share of heavy records (ir.heavy_share) at or above which it does
+W4_MIN_HEAVY_SHARE = 0.02
 
 
 def scratch_slots(p: Program) -> int:
@@ -50,13 +60,20 @@ def mean_scratch_slots(progs: Sequence[Program]) -> float:
     return sum(scratch_slots(p) for p in progs) / max(1, len(progs))
 
 
+def mean_heavy_share(progs: Sequence[Program]) -> float:
+    from .ir import heavy_share
+    return sum(heavy_share(p) for p in progs) / max(1, len(progs))
+
+
 def choose(progs16: Sequence[Program]) -> int:
     """The register layout (slots) for a batch, from its programs compiled
     for the 16-slot layout."""
     if any(p.nreg != DEFAULT for p in progs16):
         raise ValueError("the rule reads 16-slot programs")
-    return FOUR_WAVES if progs16 and mean_scratch_slots(progs16) <= W4_MAX_SCRATCH_SLOTS \
-        else DEFAULT
+    if progs16 and mean_heavy_share(progs16) >= W4_MIN_HEAVY_SHARE and \
+            mean_scratch_slots(progs16) <= W4_MAX_SCRATCH_SLOTS:
+        return FOUR_WAVES
+    return DEFAULT
 
 
 def describe(nreg: int) -> str:

@@ -234,6 +234,11 @@ class World:
         self.storage = Storage(CONTRACT, concrete_storage)
         self.kfm = KeccakFunctionManager()
         self.next_tx = 0
+        # ground truth of the stream (recall labels): why the path became
+        # infeasible, once it has (every later query of the world is UNSAT),
+        # and whether any transaction wrote a WalletLibrary pending entry
+        self.dead: Optional[str] = None
+        self.pending_written = False
 
     def tx(self, creation: bool = False) -> "Tx":
         t = Tx(self, self.next_tx, creation)
@@ -244,7 +249,14 @@ class World:
         q = Query(c.raw for c in list(self.constraints) + list(extra))
         if extra:                              # a module's check: "open" unless labelled
             q.label = getattr(extra[-1], "check_label", "open")
+        if self.dead:                          # the path itself is infeasible
+            q.label = "unsat: " + self.dead
         return q
+
+    def kill_path(self, why: str) -> None:
+        """The path just became infeasible (by the stream's construction)."""
+        if self.dead is None:
+            self.dead = why
 
 
 class Tx:
@@ -573,7 +585,11 @@ def _wallet_call(t: Tx, kind: int, checks: List[S.Bool], rng: random.Random) -> 
         t.require(S.UGT(idx, bv(0)))
         value = t.arg(1)
         spent = t.sload(bv(0x105))
-        checks.append(S.Not(S.BVAddNoOverflow(spent, value, False)))
+        # no transaction of the stream writes m_spentToday (slot 0x105): it is
+        # 0 under the creation's storage, and 0 + value cannot overflow
+        checks.append(_label(S.Not(S.BVAddNoOverflow(spent, value, False)),
+                             "unsat: m_spentToday (slot 0x105) is never written, so "
+                             "spent + value cannot overflow"))
         t.require(S.Not(S.UGT(spent + value, t.sload(bv(0x106)))))
         return
     else:
@@ -583,12 +599,26 @@ def _wallet_call(t: Tx, kind: int, checks: List[S.Bool], rng: random.Random) -> 
     t.require(S.Not(idx == bv(0)))
     pending = t.mapping(op, _W_PENDING)                         # m_pending[_operation]
     needed = t.sload(pending)
-    t.jumpi(needed == bv(0), taken=rng.randrange(2) == 0)
+    zero = rng.randrange(2) == 0
+    t.jumpi(needed == bv(0), taken=zero)
+    # ground truth: a pending entry (a keccak slot of m_pending, a multiple of
+    # 64 in its interval) holds 0 unless an earlier transaction wrote one
+    if not zero and not t.world.pending_written:
+        t.world.kill_path("m_pending[op].yetNeeded is 0 (no earlier transaction wrote a "
+                          "pending entry), so the needed != 0 branch is infeasible")
     bit = t.sload(pending + bv(1))                              # ownersDone
     t.require(S.Not((bit & bv(1)) == bv(0)) if name == "revoke(bytes32)" else
               ((bit & bv(1)) == bv(0)))
-    checks.append(S.Not(S.BVSubNoUnderflow(needed, bv(1), False)))
+    if name == "revoke(bytes32)":
+        # pending + 1 is 1 mod 64: no keccak slot, no constant slot is ever
+        # written there, so ownersDone is 0
+        t.world.kill_path("ownersDone (slot pending + 1) is never written, so revoke's "
+                          "require(ownersDone & 1) fails")
+    chk = S.Not(S.BVSubNoUnderflow(needed, bv(1), False))
+    checks.append(chk if zero else _label(chk, "unsat: the needed == 0 branch was not taken, "
+                                                "so needed - 1 cannot underflow"))
     t.sstore(pending, needed - bv(1))
+    t.world.pending_written = True
 
 
 def c4_queries(n: int = 256, seed: int = 0xC4) -> List[List[N.Node]]:

@@ -5,10 +5,15 @@
 For the first ``N`` queries of each stream (C1 / C3 / C4 / C5, the queries
 tools/search_bench.py searches):
 
-* ``unsat`` — the stream generator labels the query's check UNSAT by
-  construction (``workloads.query_label``: the SafeMath ``require`` on the
-  same path that rules it out).  As a cross-check the planter is still run
-  on it with a small budget and must find nothing;
+* ``unsat`` — the stream generator labels the query UNSAT by construction
+  (``workloads.query_label``: the SafeMath ``require`` on the same path that
+  rules the check out, or — round 6 — the step at which a WalletLibrary
+  path became infeasible: an m_pending entry nobody wrote, revoke's
+  ownersDone, the never-written m_spentToday), or the host refutation
+  proves it (``mythril_amd/refute.py``: exact per-pair order and interval
+  reasoning, brute-force-checked in tests/test_refute.py; the reason names
+  it).  As a cross-check the planter is still run on it with a small budget
+  and must find nothing;
 * ``sat`` — ``tests/planted.py`` found a model (ABI-aware scenarios + local
   search, independent of the engine's search) and ``oracle/smtlib_ref.py``
   accepts it; the model is stored, so tests/test_recall_labels.py re-checks
@@ -46,6 +51,12 @@ def label_one(item):
     from mythril_amd import workloads as W
     q = W.queries(name, N)[i]
     why = W.query_label(q)
+    if not why.startswith("unsat"):
+        import mythril_amd.model as M
+        from mythril_amd.refute import refuted
+        if any(refuted(b) for b in M.dependence_buckets(q) if len(b) > 1):
+            why = "unsat: refuted on the host (mythril_amd/refute.py: contradictory order / " \
+                  "interval atoms)"
     if why.startswith("unsat"):
         asg = planted.plant(q, seed=i, restarts=2, steps=60)
         if asg is not None:

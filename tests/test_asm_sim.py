@@ -452,7 +452,7 @@ def test_index_mode_text_invariants():
 
 
 @pytest.mark.parametrize("workload,unit,n_lds,jit", [("c3", 16, 6, False), ("c3", 16, 6, True),
-                                                     ("c3", 40, 2, True), ("c5", 33, 6, True),
+                                                     ("c3", 41, 2, True), ("c5", 46, 6, True),
                                                      ("c4", 9, 6, False)])
 def test_spill_placement_stand_in_units(workload, unit, n_lds, jit):
     """Spill placement (mg_host.cpp place_spills, round 5): one-limb values
