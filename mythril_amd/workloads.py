@@ -668,16 +668,19 @@ def _env(t: Tx, name: str, w: int = 256) -> S.BitVec:
 
 
 def _call(t: Tx, to: S.BitVec, checks: List[S.Bool], pc: int, checked: bool,
-          value: Optional[S.BitVec] = None) -> S.BitVec:
+          value: Optional[S.BitVec] = None, not_attacker: Optional[str] = None) -> S.BitVec:
     """A CALL (``instructions.py:1920-2135``): ``retval_{pc}`` on the stack;
     the external-call module asks ``UGT(gas, 2300) ∧ to == ATTACKER``
     (``external_calls.py:79-84``), the unchecked-retval module
     ``retval == 1`` / ``retval == 0`` (``unchecked_retval.py:85-89``) when the
     result is not checked, the state-change module ``UGT(gas, 2300)`` with a
-    positive value (``state_change_external_calls.py:47-62,196``)."""
+    positive value (``state_change_external_calls.py:47-62,196``).
+    ``not_attacker``: why the target can never be the attacker (the
+    external-call check is then UNSAT by construction: recall labels)."""
     gas = _env(t, "gas")
     ret = _env(t, "retval_%d" % pc)
-    checks.append(S.And(S.UGT(gas, bv(2300)), to == bv(ACTORS[1])))
+    chk = S.And(S.UGT(gas, bv(2300)), to == bv(ACTORS[1]))
+    checks.append(_label(chk, "unsat: " + not_attacker) if not_attacker else chk)
     if value is not None:
         checks.append(S.And(S.UGT(gas, bv(2300)), S.UGT(value, bv(0))))
     if checked:
@@ -686,6 +689,14 @@ def _call(t: Tx, to: S.BitVec, checks: List[S.Bool], pc: int, checked: bool,
         checks.append(ret == bv(1))
         checks.append(ret == bv(0))
     return ret
+
+
+# deposits move msg.value out of the sender's ether (Tx: UGE(balance[caller],
+# callvalue), then balance[caller] -= callvalue) into its balances[] entry, and
+# withdrawals move it back: entry + ether stays at most the sender's ether
+# before its first deposit, so entry + msg.value <= that, below 2^256
+_DEPOSIT_NO_OVERFLOW = ("unsat: deposits move msg.value out of the sender's ether (bounded by "
+                        "its balance), so balances[sender] + msg.value cannot overflow")
 
 
 def _ether_thief(t: Tx, checks: List[S.Bool], amount: S.BitVec) -> None:
@@ -707,6 +718,7 @@ def _calls_session(rng: random.Random, out: List[List[N.Node]]) -> None:
     w = World(concrete_storage=True)
     c = w.tx(creation=True)
     c.sstore(bv(0), c.arg_address(0))                           # fixed_address = addr
+    stored = False                                              # slot 1 written yet
     for _ in range(1 + rng.randrange(2)):
         t = w.tx()
         checks: List[S.Bool] = []
@@ -716,12 +728,16 @@ def _calls_session(rng: random.Random, out: List[List[N.Node]]) -> None:
         t.nonpayable()
         if name == "setstoredaddress(address)":
             t.sstore(bv(1), t.arg_address(0))
+            stored = True
         else:
             if name == "calluseraddress(address)":
                 to = t.arg_address(0)
             else:                                               # fixed / stored address
                 to = bv(ADDR_MASK) & t.sload(bv(1 if name == "callstoredaddress()" else 0))
-            _call(t, to, checks, 0x90 + len(name), checked=False)
+            never = None
+            if name == "callstoredaddress()" and not stored:
+                never = "stored_address (slot 1) was never set, so the call target is 0"
+            _call(t, to, checks, 0x90 + len(name), checked=False, not_attacker=never)
             if name == "reentrancy()":
                 t.sstore(bv(2), bv(0))                          # statevar = 0 after the call
         out.append(w.query())
@@ -740,6 +756,7 @@ def _etherstore_session(rng: random.Random, out: List[List[N.Node]]) -> None:
     w = World(concrete_storage=True)
     c = w.tx(creation=True)
     c.sstore(bv(0), bv(10 ** 18))                               # withdrawalLimit = 1 ether
+    withdrawn = False                                           # lastWithdrawTime written yet
     for _ in range(1 + rng.randrange(3)):
         t = w.tx()
         checks: List[S.Bool] = []
@@ -747,7 +764,8 @@ def _etherstore_session(rng: random.Random, out: List[List[N.Node]]) -> None:
             t.dispatch(ETHERSTORE_FUNCS, ETHERSTORE_FUNCS.index(selector("depositFunds()")))
             slot = t.mapping(t.sender(), 2)
             cur = t.sload(slot)
-            checks.append(S.Not(S.BVAddNoOverflow(cur, t.callvalue, False)))
+            checks.append(_label(S.Not(S.BVAddNoOverflow(cur, t.callvalue, False)),
+                                 _DEPOSIT_NO_OVERFLOW))
             t.sstore(slot, cur + t.callvalue)
         else:
             t.dispatch(ETHERSTORE_FUNCS, ETHERSTORE_FUNCS.index(selector("withdrawFunds(uint256)")))
@@ -758,7 +776,10 @@ def _etherstore_session(rng: random.Random, out: List[List[N.Node]]) -> None:
             t.require(S.ULE(amt, t.sload(bv(0))))
             now = _env(t, "timestamp")
             last = t.sload(t.mapping(t.sender(), 1))
-            checks.append(S.Not(S.BVAddNoOverflow(last, bv(604800), False)))
+            chk = S.Not(S.BVAddNoOverflow(last, bv(604800), False))
+            checks.append(chk if withdrawn else _label(
+                chk, "unsat: lastWithdrawTime[sender] is 0 until a withdrawal, so last + "
+                     "604800 cannot overflow"))
             t.require(S.UGE(now, last + bv(604800)))
             _call(t, t.sender(), checks, 0x1F3, checked=True, value=amt)
             _ether_thief(t, checks, amt)
@@ -766,6 +787,7 @@ def _etherstore_session(rng: random.Random, out: List[List[N.Node]]) -> None:
             checks.append(S.Not(S.BVSubNoUnderflow(bal, amt, False)))
             t.sstore(slot_b, bal - amt)
             t.sstore(t.mapping(t.sender(), 1), now)
+            withdrawn = True
         out.append(w.query())
         for chk in checks:
             out.append(w.query([chk]))
@@ -861,7 +883,8 @@ def _returnvalue_session(rng: random.Random, out: List[List[N.Node]]) -> None:
         t.dispatch(funcs, funcs.index(selector(name)))
         t.nonpayable()
         _call(t, bv(ADDR_MASK) & t.sload(bv(0)), checks, 0x60 + len(name),
-              checked=name == "callchecked()")
+              checked=name == "callchecked()",
+              not_attacker="the call target is the constant callee address (slot 0)")
         out.append(w.query())
         for chk in checks:
             out.append(w.query([chk]))
@@ -882,6 +905,7 @@ def _rubixi_session(rng: random.Random, out: List[List[N.Node]]) -> None:
     c = w.tx(creation=True)
     c.sstore(bv(_R_FEEPCT), bv(10))
     c.sstore(bv(_R_MULT), bv(300))
+    creator = False                                             # slot 5 written yet
     for _ in range(1 + rng.randrange(3)):
         t = w.tx()
         checks: List[S.Bool] = []
@@ -921,11 +945,15 @@ def _rubixi_session(rng: random.Random, out: List[List[N.Node]]) -> None:
             t.dispatch(RUBIXI_FUNCS, RUBIXI_FUNCS.index(selector("dynamicPyramid()")))
             t.nonpayable()
             t.sstore(bv(_R_CREATOR), t.sender())
+            creator = True
         else:
             name = "collectFeesInEther(uint256)" if kind == 2 else "collectPercentOfFees(uint256)"
             t.dispatch(RUBIXI_FUNCS, RUBIXI_FUNCS.index(selector(name)))
             t.nonpayable()
             t.jumpi(t.sender() == bv(ADDR_MASK) & t.sload(bv(_R_CREATOR)), taken=True)
+            if not creator:
+                w.kill_path("creator (slot 5) is 0 until dynamicPyramid() runs, so the "
+                            "onlyowner test msg.sender == creator fails")
             fees = t.sload(bv(_R_FEES))
             arg = t.arg(0)
             if kind == 2:
@@ -954,6 +982,7 @@ def _timelock_session(rng: random.Random, out: List[List[N.Node]]) -> None:
                                          "balances(address)", "lockTime(address)"))
     w = World(concrete_storage=True)
     w.tx(creation=True)
+    locked = False                                              # a lockTime entry written yet
     for _ in range(1 + rng.randrange(3)):
         t = w.tx()
         checks: List[S.Bool] = []
@@ -963,15 +992,20 @@ def _timelock_session(rng: random.Random, out: List[List[N.Node]]) -> None:
         if kind == 0:
             t.dispatch(funcs, funcs.index(selector("deposit()")))
             b = t.sload(slot_b)
-            checks.append(S.Not(S.BVAddNoOverflow(b, t.callvalue, False)))
+            checks.append(_label(S.Not(S.BVAddNoOverflow(b, t.callvalue, False)),
+                                 _DEPOSIT_NO_OVERFLOW))
             t.sstore(slot_b, b + t.callvalue)
             checks.append(S.Not(S.BVAddNoOverflow(now, bv(604800), False)))
             t.sstore(slot_l, now + bv(604800))
+            locked = True
         elif kind == 1:
             t.dispatch(funcs, funcs.index(selector("increaseLockTime(uint256)")))
             t.nonpayable()
             cur = t.sload(slot_l)
-            checks.append(S.Not(S.BVAddNoOverflow(cur, t.arg(0), False)))
+            chk = S.Not(S.BVAddNoOverflow(cur, t.arg(0), False))
+            checks.append(chk if locked else _label(
+                chk, "unsat: lockTime[sender] is 0 until a deposit, so lockTime + "
+                     "timeToIncrease cannot overflow"))
             t.sstore(slot_l, cur + t.arg(0))
         else:
             t.dispatch(funcs, funcs.index(selector("withdraw()")))
@@ -997,6 +1031,7 @@ def _weakrandom_session(rng: random.Random, out: List[List[N.Node]]) -> None:
     c.sstore(bv(1), bv(50))
     c.sstore(bv(2), bv(prize // 50))
     c.sstore(bv(3), bv(1))
+    sold = 0                                                    # nextTicket, concretely
     for _ in range(1 + rng.randrange(2)):
         t = w.tx()
         checks: List[S.Bool] = []
@@ -1005,8 +1040,11 @@ def _weakrandom_session(rng: random.Random, out: List[List[N.Node]]) -> None:
         for k in range(1 + rng.randrange(3)):
             price, nxt = t.sload(bv(2)), t.sload(bv(4))
             t.jumpi(S.And(S.UGE(money, price), S.ULT(nxt, t.sload(bv(1)))), taken=True)
-            checks.append(S.Not(S.BVAddNoOverflow(nxt, bv(1), False)))
+            checks.append(_label(S.Not(S.BVAddNoOverflow(nxt, bv(1), False)),
+                                 "unsat: nextTicket is the tickets sold so far (at most 6), "
+                                 "so nextTicket + 1 cannot overflow"))
             t.sstore(bv(4), nxt + bv(1))
+            sold += 1
             slot = t.sha3(S.Concat(nxt, bv(5)))
             t.sstore(slot, t.sender())
             t.sstore(slot + bv(1), t.sload(bv(3)))
@@ -1016,6 +1054,9 @@ def _weakrandom_session(rng: random.Random, out: List[List[N.Node]]) -> None:
                 taken=False)
         if rng.randrange(2):
             t.jumpi(t.sload(bv(4)) == t.sload(bv(1)), taken=True)
+            if sold != 50:
+                w.kill_path("nextTicket (%d tickets sold) is not totalTickets = 50, so "
+                            "chooseWinner() is unreachable" % sold)
             cb = bv(ADDR_MASK) & _env(t, "coinbase")
             s1 = t.sload(t.sha3(S.Concat(S.URem(cb, t.sload(bv(1))), bv(5))))
             s2 = t.sload(t.sha3(S.Concat(S.URem(t.sender(), t.sload(bv(1))), bv(5))))

@@ -376,8 +376,13 @@ def plant(roots: Sequence[N.Node], seed: int = 0, restarts: int = 12,
                 break
             want = set().union(*(q.syms[i] for i in bad)) if bad else set()
             improved = False
+            # (a calldata argument may be a hash an earlier transaction
+            # computed: WalletLibrary's confirm(op) of the pending entry an
+            # earlier addOwner keyed by keccak(msg.data))
+            outs = sorted({h for t, _ in asg.funcs.values() for _, h in t})
             for key in [k for k in sc.k if sc.knob_symbols(k) & want]:
-                for v in sc.candidates(key):
+                extra = outs if key[0] in ("word", "dword") else []
+                for v in sc.candidates(key) + extra:
                     cand = sc.with_knob(key, v)
                     a2 = cand.assignment()
                     s2, bad2 = score(q, a2)
