@@ -239,6 +239,7 @@ class World:
         # and whether any transaction wrote a WalletLibrary pending entry
         self.dead: Optional[str] = None
         self.pending_written = False
+        self.allowance_written = False         # BECToken: any approve / increaseApproval
 
     def tx(self, creation: bool = False) -> "Tx":
         t = Tx(self, self.next_tx, creation)
@@ -434,6 +435,11 @@ def _bec_transfer(t: Tx, checks: List[S.Bool], from_arg: bool) -> None:
     if from_arg:                                                # allowed[_from][msg.sender]
         allow = t.sload(t.sha3(S.Concat(t.sender(), t.mapping(frm, _ALLOW))))
         t.require(S.Not(S.UGT(value, allow)))
+        if not t.world.allowance_written:
+            # no allowance entry was ever stored (concrete storage: 0), and
+            # value > 0 was required above
+            t.world.kill_path("transferFrom before any approve: allowed[from][msg.sender] = 0 "
+                              "< value")
     # SafeMath.sub: assert(b <= a); SUB annotated by the integer module
     t.require(S.Not(S.UGT(value, bal_from)))
     checks.append(_label(S.Not(S.BVSubNoUnderflow(bal_from, value, False)),
@@ -491,6 +497,7 @@ def _bec_approve(t: Tx, checks: List[S.Bool], increase: bool) -> None:
     spender, value = t.arg_address(0), t.arg(1)
     outer = t.mapping(t.sender(), _ALLOW)
     slot = t.sha3(S.Concat(spender, outer))                     # allowed[owner][spender]
+    t.world.allowance_written = True
     if increase:
         cur = t.sload(slot)
         checks.append(_label(S.Not(S.BVAddNoOverflow(cur, value, False)),
@@ -1110,7 +1117,23 @@ def c5_queries(n: int = 1024, seed: int = 0xC5) -> List[List[N.Node]]:
     return out[:n]
 
 
-WORKLOADS = {"c1": c1_queries, "c3": c3_queries, "c4": c4_queries, "c5": c5_queries}
+def c3_overflow_queries(n: int = 64, seed: int = 0xC3) -> List[List[N.Node]]:
+    """The C3 stream's open checks only — batchTransfer's ``cnt * value``
+    after two receivers, each on its own path (the transactions before it
+    differ) — for recall: the 64-query C3 prefix holds
+    two.  Checks on a path an earlier transaction made infeasible are labelled
+    unsat and left out, so each one here is SAT by construction (``cnt = 2``,
+    ``value = 2^255`` makes ``amount`` 0).  Not a BASELINE configuration."""
+    m = 32 * n
+    while True:
+        out = [q for q in c3_queries(m, seed) if query_label(q) == "open"]
+        if len(out) >= n:
+            return out[:n]
+        m *= 2
+
+
+WORKLOADS = {"c1": c1_queries, "c3": c3_queries, "c4": c4_queries, "c5": c5_queries,
+             "c3o": c3_overflow_queries}
 
 
 def queries(name: str, n: Optional[int] = None, seed: Optional[int] = None) -> List[List[N.Node]]:

@@ -3,7 +3,9 @@
 ``tests/golden/recall_labels.json``.
 
 For the first ``N`` queries of each stream (C1 / C3 / C4 / C5, the queries
-tools/search_bench.py searches):
+tools/search_bench.py searches, and — round 6 — ``c3o``: the C3 stream's
+batchTransfer overflow checks alone, SAT by construction, so C3's recall does
+not rest on two queries):
 
 * ``unsat`` — the stream generator labels the query UNSAT by construction
   (``workloads.query_label``: the SafeMath ``require`` on the same path that
@@ -33,7 +35,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
 
 N = 64
-WORKLOADS = ("c1", "c3", "c4", "c5")
+WORKLOADS = ("c1", "c3", "c4", "c5", "c3o")
 OUT = os.path.join(HERE, "recall_labels.json")
 
 
