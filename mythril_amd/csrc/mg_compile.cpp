@@ -1045,6 +1045,8 @@ struct Lowerer {
 // search-mode model construction (mythril_amd/solve.py Solver)
 // ---------------------------------------------------------------------------
 static const int PASSES = 6;
+static const int MAX_REFUSALS = 4;          // solve.MAX_REFUSALS
+static const int SCHEDULE_MIN_SCRATCH = 10; // ir.SCHEDULE_MIN_SCRATCH
 static const int MAX_DOMAIN = 16;
 static const int MAX_BRANCHES = 4;
 static const int MAX_OR = 64;
@@ -1152,6 +1154,14 @@ struct Solver {
     std::unordered_map<int, int> depth;
     bool unsat = false;
     bool dead = false;                      // run: a root folded to false
+    // run repeats the construction after refusing the definition that made
+    // a root fold to false: leaves by id, generated leaves by their ordinal
+    // in the construction (key)
+    std::unordered_map<int, int> aux_seq;
+    std::unordered_set<int> refused;
+    // leaves defined from an overflow test's atoms (the module's check)
+    bool wrap_ctx = false;
+    std::unordered_set<int> wrap_defs;
 
     std::vector<std::pair<int, bool>> rw_stack_;
 
@@ -1826,10 +1836,12 @@ struct Solver {
     bool try_define(int leaf, int e) {
         if (ln[leaf].op != MG_LEAF || repl_find(leaf)) return false;
         if (selectors.count(leaf) && ln[e].op != MG_CONST) return false;
+        if (!refused.empty() && refused.count(key(leaf))) return false;
         if (ln[e].width > ln[leaf].width && !(ln[e].op == MG_CONST && shr(ln[e].imm, ln[leaf].width).zero()))
             return false;
         if (depends(e, leaf)) return false;
         repl_put(leaf, e);
+        if (wrap_ctx) wrap_defs.insert(leaf);
         leaf_imm[leaf] = (int)ln[leaf].imm.w[0];
         leaf_node[leaf] = leaf;
         if (dm_valid) dm.set(leaf_imm[leaf]);   // the mask only grows here
@@ -1892,7 +1904,13 @@ struct Solver {
     }
     int aux(int width) {
         n_aux++;
-        return lw.leaf("aux#" + std::to_string(n_aux), width, K_AUX, "");
+        int leaf = lw.leaf("aux#" + std::to_string(n_aux), width, K_AUX, "");
+        aux_seq.emplace(leaf, (int)aux_seq.size());
+        return leaf;
+    }
+    int key(int leaf) const {
+        auto it = aux_seq.find(leaf);
+        return it == aux_seq.end() ? leaf : -1 - it->second;
     }
 
     int define(const Chunks& atoms_) {
@@ -2119,6 +2137,39 @@ struct Solver {
         return ln[x].op == MG_ULT && ln[ln[x].args[0]].op == MG_ADD && contains(ln[ln[x].args[0]].args, ln[x].args[1]);
     }
 
+    // the definition (index into the insertion-ordered definitions) that
+    // completes root r's folding to false: the shortest prefix under which
+    // it folds to false ends with it; -1 when r is false with none
+    // (solve.Solver._culprit)
+    int culprit(int r) {
+        const std::vector<std::pair<int, int>> items = repl.items;
+        auto set_prefix = [&](size_t m) {
+            repl_truncate(0);
+            for (size_t i = 0; i < m; i++) repl_put(items[i].first, items[i].second);
+            dm_valid = false;
+        };
+        auto false_under = [&](size_t m) {
+            set_prefix(m);
+            Memo fresh;
+            int x = rewrite(r, fresh);
+            return ln[x].op == MG_CONST && !(ln[x].imm.w[0] & 1);
+        };
+        int res;
+        if (false_under(0)) {
+            res = -1;
+        } else {
+            size_t lo = 0, hi = items.size();   // false_under(hi) holds
+            while (hi - lo > 1) {
+                size_t mid = (lo + hi) / 2;
+                if (false_under(mid)) hi = mid;
+                else lo = mid;
+            }
+            res = (int)hi - 1;
+        }
+        set_prefix(items.size());
+        return res;
+    }
+
     void run(Chunks& roots, std::vector<std::pair<int, int>>& defs_out) {
         int64_t saved_birth = lw.birth;
         lw.birth = 0;
@@ -2131,36 +2182,39 @@ struct Solver {
         Chunks order;
         for (int r : roots) if (is_wrap_test(r)) order.push_back(r);
         for (int r : roots) if (!is_wrap_test(r)) order.push_back(r);
+        const std::vector<std::pair<int, int>> base = repl.items;
         Memo memo;
-        run_memo = &memo;
-        for (int pass = 0; pass < PASSES; pass++) {
-            int found = 0;
-            Chunks every;
-            for (int r : order) {
-                Chunks at = atoms(r, memo);
-                const int rr = rewrite(r, memo);
-                if (ln[rr].op == MG_CONST && !(ln[rr].imm.w[0] & 1)) {
-                    // a root folded to false under the construction: the
-                    // group needs no program beyond it (model._ground_value)
-                    dead = true;
-                    roots = {rr};
-                    defs_out.clear();
-                    lw.birth = saved_birth;
-                    run_memo = &base_memo;
-                    return;
-                }
-                append(every, at);
-                found += define(at);
+        for (int attempt = 0; attempt <= MAX_REFUSALS; attempt++) {
+            int at_pass = -1;
+            const int d = passes(order, memo, at_pass);
+            if (d < 0) break;
+            // a root folded to false under the construction: completed by
+            // an overflow test's definition or in the first pass, the
+            // query's own conditions meeting (the group needs no program
+            // beyond that root, model._ground_value); otherwise heuristic
+            // commits conflicting: refuse the definition that completed it
+            // and construct again, up to MAX_REFUSALS times
+            // (solve.Solver.run)
+            int k = at_pass > 0 && attempt < MAX_REFUSALS ? culprit(d) : -1;
+            if (k >= 0 && wrap_defs.count(repl.items[k].first)) k = -1;  // the check's own choice
+            if (k < 0) {
+                dead = true;
+                roots = {rewrite(d, memo)};
+                defs_out.clear();
+                lw.birth = saved_birth;
+                run_memo = &base_memo;
+                return;
             }
-            if (found) for (auto& a : every) a = rewrite(a, memo);
-            Chunks extra;
-            for (int part : joint_bounds(every)) append(extra, atoms(part, memo));
-            if (!extra.empty()) {
-                found += define(extra);
-                append(every, extra);
-            }
-            found += ranges(every);
-            if (!found) break;
+            refused.insert(key(repl.items[k].first));
+            repl_truncate(0);
+            for (auto& kv : base) repl_put(kv.first, kv.second);
+            dm_valid = false;
+            or_seen.clear();
+            joint_done.clear();
+            n_branch = 0;
+            aux_seq.clear();
+            wrap_defs.clear();
+            depth.clear();
         }
         for (auto& r : roots) r = rewrite(r, memo);
         defs_out.clear();
@@ -2171,6 +2225,40 @@ struct Solver {
         }
         lw.birth = saved_birth;
         run_memo = &base_memo;
+    }
+
+    // the definition passes over a fresh memo; the first root that folds to
+    // false (and the pass it folded in), or -1 (solve.Solver._passes)
+    int passes(const Chunks& order, Memo& memo, int& at_pass) {
+        memo.dense.clear();
+        run_memo = &memo;
+        for (int pass = 0; pass < PASSES; pass++) {
+            int found = 0;
+            Chunks every;
+            for (int r : order) {
+                wrap_ctx = is_wrap_test(r);
+                Chunks at = atoms(r, memo);
+                const int rr = rewrite(r, memo);
+                if (ln[rr].op == MG_CONST && !(ln[rr].imm.w[0] & 1)) {
+                    wrap_ctx = false;
+                    at_pass = pass;
+                    return r;
+                }
+                append(every, at);
+                found += define(at);
+            }
+            wrap_ctx = false;
+            if (found) for (auto& a : every) a = rewrite(a, memo);
+            Chunks extra;
+            for (int part : joint_bounds(every)) append(extra, atoms(part, memo));
+            if (!extra.empty()) {
+                found += define(extra);
+                append(every, extra);
+            }
+            found += ranges(every);
+            if (!found) break;
+        }
+        return -1;
     }
 };
 
@@ -3052,14 +3140,16 @@ static void compile(const mgc_input* in, mgc_result* res) {
     Alloc al0(lw.ln, order, const_index, fused, in->nreg, in->remat_mode, in->remat_k,
               in->keep_clean != 0);
     al0.run();
-    // eval form: the sink-driven order too, and the cheaper allocation
-    // (ir.compile_constraints_py: scratch spill slots, then spill + reload
-    // records, then instructions); search programs keep source order
+    // eval form: the sink-driven order too when the source order keeps at
+    // least SCHEDULE_MIN_SCRATCH spill slots in scratch, and the cheaper
+    // allocation (ir.compile_constraints_py: scratch spill slots, then
+    // spill + reload records, then instructions); search programs keep
+    // source order
     const Alloc* alp = &al0;
     std::unordered_set<int> fused2;
     std::vector<int> order2;
     std::unique_ptr<Alloc> al2;
-    if (!in->solve && !in->leaf_pools) {
+    if (!in->solve && !in->leaf_pools && al0.n_lds - LDS_TIER >= SCHEDULE_MIN_SCRATCH) {
         order2 = fuse_roots(lw.ln, schedule_demand(lw.ln, sinks), fused2);
         try {
             al2.reset(new Alloc(lw.ln, order2, const_index, fused2, in->nreg, in->remat_mode,

@@ -743,6 +743,15 @@ def _alloc_cost(n_lds: int, n_spill: int, n_reload: int, n_ins: int) -> Tuple[in
 # MYTHRIL_GPU_COMPILER=py: it emits the native compiler's programs, so an
 # A/B through it measures the native default against source order)
 SCHEDULE_CHOICE = _os.environ.get("MYTHRIL_GPU_SCHEDULE_CHOICE", "1") != "0"
+# the sink-driven order is tried only for a program whose source order keeps
+# at least this many spill slots in per-lane scratch: the alternated A/B of
+# the unconditional choice (profiles/r06/sched2/) gave C3 +3.6 % (source
+# order: 15.1 scratch slots per program) but C4 -2.1 % and C5 -0.5 %, whose
+# programs mostly keep fewer than 10 (C4 4.4) — there the sink-driven
+# order's fewer spill records do not pay for the leaf loads it moves next
+# to their readers.  (The env value is for that A/B, Python specification
+# only; mg_compile.cpp SCHEDULE_MIN_SCRATCH is the same constant.)
+SCHEDULE_MIN_SCRATCH = int(_os.environ.get("MYTHRIL_GPU_SCHEDULE_MIN_SCRATCH", "10"))
 
 
 def _fuse_roots(order: List[LNode]) -> Tuple[List[LNode], set]:
@@ -1311,7 +1320,8 @@ def compile_constraints_py(constraints: Sequence[Node], probes: Sequence[Node] =
                           {v & ((1 << 256) - 1) for v in extra_consts})
     const_index = {v: i for i, v in enumerate(const_values)}
     ins, n_lds, n_spill, n_reload = _allocate(order, const_index, fused, nreg)
-    if not solve and not leaf_pools and SCHEDULE_CHOICE:
+    if not solve and not leaf_pools and SCHEDULE_CHOICE and \
+            n_lds - LDS_TIER >= SCHEDULE_MIN_SCRATCH:
         # eval form (round 6): the sink-driven order too, and the one whose
         # allocation costs less (the query streams' calldata words and
         # store-chain reads are built early and read late: C3 -29 % spill

@@ -10,7 +10,8 @@ Which layout wins depends on the programs.  The fourth wave fills VALU
 issue slots, and the five fewer slots cost spills: a batch whose 16-slot
 programs already keep values in per-lane scratch beyond the LDS tier gets
 more of them at 11 slots, and scratch round trips are what such a batch
-waits on.  Measured (alternated A/B on one box, ``profiles/r05/nreg/``):
+waits on.  Measured (alternated A/Bs on one box, ``profiles/r05/nreg/``,
+round-5 compiler):
 
 =========  ===========================================  ===================
 workload   scratch spill slots per program at 16 slots  11 slots vs 16
@@ -21,18 +22,20 @@ C5         5.50                                          -11 %
 C3         14.92                                         -11 %
 =========  ===========================================  ===================
 
-and the scratch count alone is not enough: with the sink-driven schedule
-(round 6) C4's programs fall to 2.94 scratch slots at 16, yet C4 on the
+and the scratch count alone is not enough: with the round-6 schedule
+choice C4's programs fall to 2.45 scratch slots at 16 (C2 1.77, C5 3.98,
+C3 10.74: ``profiles/r06/r6p/`` ``config.layout_rule``), yet C4 on the
 four-wave layout lost 26-31 % (``profiles/r06/sched/``).  What C2 has and
 the query streams lack is heavy arithmetic: C2's programs are 8.5 % MUL /
 division / umul_noovfl records (``ir.heavy_share``; every one of them at
-least 1 %), C3 / C4 / C5 0.14 / 0 / 0.25 % — C2 is VALU-issue-bound (VALU
-active 0.92 of SIMD cycles at three waves), the streams wait on memory.  So
-the rule is: the four-wave layout when the batch's 16-slot programs average
-at least ``W4_MIN_HEAVY_SHARE`` heavy records AND at most
-``W4_MAX_SCRATCH_SLOTS`` scratch spill slots per program.  Both statistics
-are static (the compiler's records and spill-slot count, ``Program.n_lds``
-minus the 16-slot layout's LDS tier), known before anything is launched.
+least 1 %), C3 / C4 / C5 0.14 / 0 / 0.26 % — C2 is VALU-issue-bound (VALU
+active 0.92 of SIMD cycles at three waves, 0.998 at four), the streams
+wait on memory.  So the rule is: the four-wave layout when the batch's
+16-slot programs average at least ``W4_MIN_HEAVY_SHARE`` heavy records AND
+at most ``W4_MAX_SCRATCH_SLOTS`` scratch spill slots per program.  Both
+statistics are static (the compiler's records and spill-slot count,
+``Program.n_lds`` minus the 16-slot layout's LDS tier), known before
+anything is launched.
 """
 
 from typing import Sequence
@@ -42,7 +45,7 @@ from .ir import Program
 DEFAULT = 16
 FOUR_WAVES = 11
 # mean scratch spill slots per 16-slot program at or below which a batch
-# may run the four-wave layout (between C2's 1.80 and C4's 4.38, above)
+# may run the four-wave layout (between C2's 1.77 and C5's 3.98, above)
 W4_MAX_SCRATCH_SLOTS = 3.0
 # mean share of heavy records (ir.heavy_share) at or above which it does
 W4_MIN_HEAVY_SHARE = 0.02

@@ -49,6 +49,7 @@ MAX_BRANCHES = 4         # disjuncts of an ``or`` split by a selector
 MAX_OR = 64              # such splits per program
 BRANCH_DEPTH = 2
 SELECTOR_WIDTH = 8
+MAX_REFUSALS = 4         # definitions refused after killing a root, per run
 
 
 _PREDICATES = (I.EQ, I.ULT, I.ULE, I.SLT, I.SLE, I.UMULNO)
@@ -82,6 +83,10 @@ class _Overlay(dict):
         return self.parent[k] if v is None else v
 
 
+def _is_false(x) -> bool:
+    return x.op == I.CONST and not x.imm & 1
+
+
 def _mask(w: int) -> int:
     return (1 << w) - 1
 
@@ -109,6 +114,13 @@ class Solver:
         self.depth: Dict[int, int] = {}
         self.unsat = False
         self.dead = False                        # run: a root folded to false
+        self.refused: set = set()                # leaves (_key) whose definition killed a root
+        # a generated leaf's ordinal in this construction (run repeats the
+        # construction; the same ordinal is the same choice)
+        self.aux_seq: Dict[int, int] = {}
+        # leaves defined from an overflow test's atoms (the module's check)
+        self._wrap_ctx = False
+        self.wrap_defs: set = set()
 
     # -- rewriting -------------------------------------------------------------
     def _interval(self, n):
@@ -716,11 +728,15 @@ class Solver:
             return False
         if leaf.id in self.selectors and e.op != I.CONST:
             return False                         # a selector only commits to a branch
+        if self.refused and self._key(leaf.id) in self.refused:
+            return False                         # its definition killed a root (run)
         if e.width > leaf.width and not (e.op == I.CONST and e.imm >> leaf.width == 0):
             return False
         if self._depends(e, leaf):
             return False
         self.repl[leaf.id] = e
+        if self._wrap_ctx:
+            self.wrap_defs.add(leaf.id)
         self.leaf_imm[leaf.id] = leaf.imm
         self.leaf_node[leaf.id] = leaf
         self._dm = None
@@ -783,7 +799,15 @@ class Solver:
 
     def _aux(self, width: int):
         self.n_aux += 1
-        return self.lw.leaf("aux#%d" % self.n_aux, width, "aux", "")
+        leaf = self.lw.leaf("aux#%d" % self.n_aux, width, "aux", "")
+        self.aux_seq[leaf.id] = len(self.aux_seq)
+        return leaf
+
+    def _key(self, leaf_id: int):
+        """A leaf's identity across repeated constructions (run): its id, or
+        a generated leaf's ordinal."""
+        k = self.aux_seq.get(leaf_id)
+        return leaf_id if k is None else -1 - k
 
     def _define(self, atoms) -> int:
         n = 0
@@ -989,6 +1013,32 @@ class Solver:
                 return False
         return own
 
+    def _culprit(self, r) -> Optional[int]:
+        """The definition (index into the insertion-ordered definitions) that
+        completes root ``r``'s folding to false: the shortest prefix under
+        which it folds to false ends with it.  None when ``r`` is false with
+        no definitions at all."""
+        items = list(self.repl.items())
+        saved = self.repl
+
+        def false_under(m: int) -> bool:
+            self.repl = dict(items[:m])
+            self._dm = None
+            return _is_false(self.rewrite(r, {}))
+        lo, hi = 0, len(items)                   # false_under(hi) holds
+        if false_under(0):
+            lo = None
+        else:
+            while hi - lo > 1:                   # false_under(lo) is False
+                mid = (lo + hi) // 2
+                if false_under(mid):
+                    hi = mid
+                else:
+                    lo = mid
+        self.repl = saved
+        self._dm = None
+        return None if lo is None else hi - 1
+
     def run(self, roots):
         # new nodes are born with their latest operand (ir._schedule places
         # them there), not after the whole query
@@ -1001,24 +1051,64 @@ class Solver:
         # query's last constraint; its wrap-around choice must win over the
         # bounds the path constraints put on the same operands)
         order = sorted(roots, key=lambda r: not self._is_wrap_test(r))
+        base = list(self.repl.items())
+        for attempt in range(MAX_REFUSALS + 1):
+            dead, at_pass = self._passes(order)
+            if dead is None:
+                break
+            # a root folded to false under the construction.  When the
+            # definition that completed it came from the overflow test (the
+            # module's check: a SafeMath check whose require is on the path)
+            # or the first pass, that is the query's own conditions meeting:
+            # the group needs no program beyond that root
+            # (model._ground_value).  Otherwise it is heuristic commits
+            # conflicting (the C3 overflow checks after an approve: a
+            # table-arm commit and a branch split): refuse the definition
+            # that completed the false root and construct again, up to
+            # MAX_REFUSALS times
+            k = self._culprit(dead) if at_pass and attempt < MAX_REFUSALS else None
+            if k is not None and list(self.repl)[k] in self.wrap_defs:
+                k = None                         # the check's own choice: not refused
+            if k is None:
+                self.dead = True
+                self.lw.birth = saved_birth
+                return [self.rewrite(dead, self._memo)], {}
+            self.refused.add(self._key(list(self.repl)[k]))
+            self.repl = dict(base)
+            self._dm = None
+            self.or_seen = set()
+            self.joint_done = set()
+            self.n_branch = 0
+            self.aux_seq = {}
+            self.wrap_defs = set()
+            self.depth = {}
+        memo = self._memo
+        new_roots = [self.rewrite(r, memo) for r in roots]
+        by_id = self.leaf_node
+        defs = {by_id[k].imm: self.rewrite(e, memo) for k, e in self.repl.items()}
+        self.lw.birth = saved_birth
+        return new_roots, defs
+
+    def _passes(self, order):
+        """The definition passes: (the first root that folds to false, the
+        pass it folded in), or (None, None)."""
         # one memo for the whole run: rewrite drops the entries a new
         # definition reaches (later roots see the new definitions folded)
         memo: Dict[int, object] = {}
         self._memo = memo
-        for _ in range(PASSES):
+        for at_pass in range(PASSES):
             found = 0
             every = []
             for r in order:
+                self._wrap_ctx = self._is_wrap_test(r)
                 atoms = self._atoms(r, memo)
                 rr = self.rewrite(r, memo)
                 if rr.op == I.CONST and not rr.imm & 1:
-                    # a root folded to false under the construction: the
-                    # group needs no program beyond it (model._ground_value)
-                    self.dead = True
-                    self.lw.birth = saved_birth
-                    return [rr], {}
+                    self._wrap_ctx = False
+                    return r, at_pass
                 every += atoms
                 found += self._define(atoms)
+            self._wrap_ctx = False
             # intervals from the bounds of all conjuncts together: per
             # expression (x >= 2 from one constraint, x <= 2 from another make
             # x = 2 — through a concat, its low byte), then per leaf
@@ -1033,8 +1123,4 @@ class Solver:
             found += self._ranges(every)
             if not found:
                 break
-        new_roots = [self.rewrite(r, memo) for r in roots]
-        by_id = self.leaf_node
-        defs = {by_id[k].imm: self.rewrite(e, memo) for k, e in self.repl.items()}
-        self.lw.birth = saved_birth
-        return new_roots, defs
+        return None, None

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Sweep: the native compiler (include/mythcc.h) against the Python
 specification (ir.compile_constraints_py + solve.py) on many more inputs
-than tests/test_native_compiler.py holds — C2 corpus DAGs [lo, hi) in eval
-form and every independent group of the C1 / C3 / C4 stand-in streams in
+than tests/test_native_compiler.py holds — C2 corpus DAGs [lo, hi) and the
+first QUERIES C3 / C4 / C5 bench units in eval form, and every independent group of the C1 / C3 / C4 / C5 / c3o stand-in streams in
 search form (solve + hints + ABI presets, and the plain search form).
 Prints running (compiles, mismatches) per part; every program must be
 identical.
@@ -53,7 +53,12 @@ def main():
     for d in range(lo, hi):
         both("c2/%d" % d, make_dag(d)[0])
     print("c2 compiles %d mismatches %d" % (n, bad), flush=True)
-    for wl in ("c1", "c3", "c4"):
+    import bench
+    for wl in ("c3", "c4", "c5"):                # the bench units, eval form
+        for d in range(nq):
+            both("%s-eval/%d" % (wl, d), bench.workload_roots(wl, d))
+        print("%s eval compiles %d mismatches %d" % (wl, n, bad), flush=True)
+    for wl in ("c1", "c3", "c4", "c5", "c3o"):
         for qi, q in enumerate(W.queries(wl, nq, seed=seed)):
             for bi, b in enumerate(M.dependence_buckets(q)):
                 both("%s/%d/%d" % (wl, qi, bi), b, (), leaf_pools=True, const_keys=True,
