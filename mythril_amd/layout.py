@@ -23,9 +23,11 @@ C3         14.92                                         -11 %
 =========  ===========================================  ===================
 
 and the scratch count alone is not enough: with the round-6 schedule
-choice C4's programs fall to 2.45 scratch slots at 16 (C2 1.77, C5 3.98,
-C3 10.74: ``profiles/r06/r6p/`` ``config.layout_rule``), yet C4 on the
-four-wave layout lost 26-31 % (``profiles/r06/sched/``).  What C2 has and
+choice C4's programs fell to 2.45 scratch slots at 16 (C2 1.77, C5 3.98,
+C3 10.74: ``profiles/r06/r6p/`` ``config.layout_rule``; with the choice
+gated on 10 scratch slots, C2 1.80, C4 4.00, C5 4.55, C3 10.96:
+``profiles/r06/r6g/``), yet C4 on the four-wave layout lost 26-31 %
+(``profiles/r06/sched/``).  What C2 has and
 the query streams lack is heavy arithmetic: C2's programs are 8.5 % MUL /
 division / umul_noovfl records (``ir.heavy_share``; every one of them at
 least 1 %), C3 / C4 / C5 0.14 / 0 / 0.26 % — C2 is VALU-issue-bound (VALU
@@ -45,7 +47,7 @@ from .ir import Program
 DEFAULT = 16
 FOUR_WAVES = 11
 # mean scratch spill slots per 16-slot program at or below which a batch
-# may run the four-wave layout (between C2's 1.77 and C5's 3.98, above)
+# may run the four-wave layout (between C2's 1.80 and C4's 4.00, above)
 W4_MAX_SCRATCH_SLOTS = 3.0
 # mean share of heavy records (ir.heavy_share) at or above which it does
 W4_MIN_HEAVY_SHARE = 0.02
