@@ -87,6 +87,28 @@ def test_query_streams_identical(workload):
         assert presets > 0          # BECToken batchTransfer reads _receivers at ABI offsets
 
 
+def test_refused_commits_identical():
+    """The construction's refusals (solve.Solver.run / _culprit, round 6):
+    c3o queries whose groups needed a refused commit (7, 16) and a SafeMath
+    check whose group is refused into a live program, in both compilers."""
+    from mythril_amd import workloads as W
+    import mythril_amd.model as M
+    qs = [W.queries("c3o", 64)[i] for i in (7, 16)] + [W.queries("c3", 64)[0]]
+    for q in qs:
+        for b in M.dependence_buckets(q):
+            _both(b, (), leaf_pools=True, const_keys=True, solve=True, search_hints=True,
+                  abi_presets=True)
+
+
+def test_stream_bench_units_identical():
+    """The eval form of the C3 / C4 / C5 bench units (the gated schedule
+    choice of round 6 picks per program)."""
+    import bench
+    for wl in ("c3", "c4", "c5"):
+        for d in range(4):
+            _both(bench.workload_roots(wl, d))
+
+
 def test_unsupported_and_errors():
     from mythril_amd.smt import node as N
     x = N.bv_var("x", 300)
