@@ -289,7 +289,10 @@ _CMP = {"s_cmp_eq_u32": lambda a, b: a == b, "s_cmp_lg_u32": lambda a, b: a != b
 # ---------------------------------------------------------------------------
 
 RECORD_SGPRS = frozenset(range(BANK0, BANK0 + 8))
-_TARGETS: Dict[int, frozenset] = {}
+# memos of a template's analysis, keyed by the template list's id() and
+# holding the list itself: a hit must be that very list (a layout switch
+# drops the templates, and a new list may reuse a dropped one's id)
+_TARGETS: Dict[int, tuple] = {}
 
 
 def _branch_targets(lines: Sequence[str]) -> frozenset:
@@ -297,14 +300,14 @@ def _branch_targets(lines: Sequence[str]) -> frozenset:
     fall-through points: no join, no state reset)."""
     key = id(lines)
     hit = _TARGETS.get(key)
-    if hit is None:
+    if hit is None or hit[0] is not lines:
         out = set()
         for l in lines:
             t = l.strip()
             if t.startswith(("s_branch", "s_cbranch")):
                 out.add(t.split()[1])
-        hit = _TARGETS[key] = frozenset(out)
-    return hit
+        hit = _TARGETS[key] = (lines, frozenset(out))
+    return hit[1]
 
 
 _REACH: Dict[int, object] = {}
@@ -319,8 +322,8 @@ def _reach_reads(lines: Sequence[str]):
     as a literal stays unmaterialized there."""
     key = id(lines)
     hit = _REACH.get(key)
-    if hit is not None and len(hit[0]) == len(lines):
-        return hit
+    if hit is not None and hit[0] is lines:
+        return hit[1]
     n = len(lines)
     uses: List[frozenset] = []
     succ: List[Tuple[int, ...]] = []
@@ -368,7 +371,7 @@ def _reach_reads(lines: Sequence[str]):
             if len(acc) != k:
                 changed = True
     out = ([frozenset(r) for r in R], at)
-    _REACH[key] = out
+    _REACH[key] = (lines, out)
     return out
 
 
@@ -969,7 +972,7 @@ def coalesce_cached(hot: List[str]) -> List[str]:
     return back
 
 
-_FIELDS: Dict[int, Tuple[int, ...]] = {}
+_FIELDS: Dict[int, tuple] = {}            # id(template) -> (template, fields)
 _SPEC: Dict[tuple, tuple] = {}
 _TAG = "@T@"
 
@@ -993,18 +996,19 @@ def fields_read(lines: Sequence[str]) -> Tuple[int, ...]:
     """Record words a template reads (its s40..s47 operands)."""
     key = id(lines)
     hit = _FIELDS.get(key)
-    if hit is None:
-        used = set()
-        for l in lines:
-            used.update(int(x) for x in re.findall(r"@F(\d)", l))
-            for m in re.finditer(r"s\[?(\d+)(?::(\d+)\])?", l):
-                lo = int(m.group(1))
-                hi = int(m.group(2)) if m.group(2) else lo
-                used.update(k - BANK0 for k in range(lo, hi + 1) if BANK0 <= k < BANK0 + 8)
-            if l.startswith("@@CALL"):
-                used.update((G.F_D, G.F_A, G.F_B, G.F_W, G.F_MOFF))
-        hit = _FIELDS[key] = tuple(sorted(used))
-    return hit
+    if hit is not None and hit[0] is lines:
+        return hit[1]
+    used = set()
+    for l in lines:
+        used.update(int(x) for x in re.findall(r"@F(\d)", l))
+        for m in re.finditer(r"s\[?(\d+)(?::(\d+)\])?", l):
+            lo = int(m.group(1))
+            hi = int(m.group(2)) if m.group(2) else lo
+            used.update(k - BANK0 for k in range(lo, hi + 1) if BANK0 <= k < BANK0 + 8)
+        if l.startswith("@@CALL"):
+            used.update((G.F_D, G.F_A, G.F_B, G.F_W, G.F_MOFF))
+    _FIELDS[key] = (lines, tuple(sorted(used)))
+    return _FIELDS[key][1]
 
 
 def specialize_cached(name: str, var: int, rec: Sequence[int], tag: str):

@@ -277,3 +277,22 @@ def test_code_skipped_by_a_folded_branch_is_inert():
     assert call is None
     assert "s_setpc" not in text and "s_swappc" not in text and "gpr_idx" not in text
     assert "v_mov_b32 v1, v2" in text and "v_mov_b32 v0" not in text
+
+
+def test_layout_switch_does_not_reuse_a_dropped_template_analysis():
+    """Template analyses (branch targets, reach sets, record fields) are
+    memoised by the template list's id(); a layout switch drops the
+    templates and a new list may reuse an old id, so a memo hit must be the
+    very list (round 6: a stale entry made a regenerated template's labels
+    look unreached)."""
+    from mythril_amd import asmgen as G
+    x = [".Lfoo_%=:", "    s_branch .Lfoo_%="]
+    assert jit._branch_targets(x) == frozenset({".Lfoo_%="})
+    key = id(x)
+    y = [".Lbar_%=:", "    s_branch .Lbar_%="]
+    jit._TARGETS[id(y)] = jit._TARGETS.pop(key)   # as if y had reused x's id
+    assert jit._branch_targets(y) == frozenset({".Lbar_%="})
+    with G.layout(11):
+        jit.template("MUL", 0)
+    t16 = jit.template("MUL", 0)
+    assert jit._branch_targets(t16) == jit._branch_targets(list(t16))
