@@ -56,3 +56,23 @@ def test_every_stream_has_sat_and_the_overflow_streams_unsat_labels():
              for s, rows in LABELS["streams"].items()}
     assert all(c["sat"] > 0 for c in count.values()), count
     assert count["c3"]["unsat"] > 0, count
+
+
+def test_no_sat_labelled_group_compiles_to_its_false_root():
+    """The model construction never kills a satisfiable group (round 6:
+    refused commits, solve.Solver.run): for every SAT-labelled query, no
+    independent group compiles to its constant-false root (13 c3o groups
+    and C5 query 52 did before)."""
+    import mythril_amd.model as M
+    dead = []
+    for stream, rows in LABELS["streams"].items():
+        qs = W.queries(stream, LABELS["n"])
+        for r in rows:
+            if r["label"] != "sat":
+                continue
+            for b in M.dependence_buckets(qs[r["i"]]):
+                if len(b) < 2:
+                    continue
+                if M._ground_value(M._compile_search_uncached(b)) is False:
+                    dead.append((stream, r["i"]))
+    assert not dead, dead
